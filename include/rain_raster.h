@@ -1,0 +1,173 @@
+/*
+ * rain_raster.h — C ABI of the MI355X-native differentiable Gaussian-splat rasterizer.
+ *
+ * This is the drop-in boundary for the reference's `_C` extension
+ * (sharonal10/rain submodules/diff_gaussian_rasterization/ext.cpp:4-7, rasterize_points.cu:24-212).
+ * Every entry point takes plain device pointers, sizes and a HIP stream handle (as void*);
+ * no torch types cross this boundary.  The Python host side (rain_amd/diff_gaussian_rasterization)
+ * mirrors the reference's pybind signatures on top of these functions; INTEGRATION.md shows the
+ * ctypes binding a maintainer would add to the reference instead of its pybind module.
+ *
+ * Conventions (identical to the reference kernels):
+ *   - all float tensors are fp32, contiguous; means3D/scales [P,3], rotations [P,4] (w,x,y,z),
+ *     opacities [P,1], shs [P,M,3], colors_precomp [P,3], cov3D_precomp [P,6];
+ *   - viewmatrix/projmatrix are 16 floats, column-major (the transposed torch matrices);
+ *   - optional inputs are NULL (the reference passes empty tensors, i.e. nullptr);
+ *   - image outputs are planar CHW.
+ * Return value: 0 on success, otherwise an rr_status code; rr_last_error() gives the text
+ * (the reference raises std::runtime_error / AT_ERROR in the same situations).
+ */
+#ifndef RAIN_RASTER_H
+#define RAIN_RASTER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum rr_status {
+    RR_OK = 0,
+    RR_ERR_ARG = 1,     /* bad sizes / missing required pointer  (reference: AT_ERROR, rasterize_points.cu:47-49) */
+    RR_ERR_HIP = 2,     /* HIP runtime / kernel error            (reference: CHECK_CUDA, auxiliary.h:155-162) */
+    RR_ERR_CAPACITY = 3 /* workspace smaller than the *_bytes() query */
+};
+
+/* Per-frame settings: the scalar fields of GaussianRasterizationSettings
+ * (diff_gaussian_rasterization/__init__.py:148-161) plus P, D, M. */
+typedef struct rr_frame {
+    int P;              /* number of Gaussians (means3D.size(0)) */
+    int D;              /* active SH degree (settings.sh_degree) */
+    int M;              /* SH coefficient stride, sh.size(1), 0 if no SH */
+    int width, height;  /* image_width, image_height */
+    float tan_fovx, tan_fovy;
+    float scale_modifier;
+    float low_pass;     /* RAIN-GS 2D dilation (forward.cu:99-100); 0.3 in vanilla 3DGS */
+    int prefiltered;
+    int debug;          /* sync + check after every launch (auxiliary.h:155-162) */
+} rr_frame;
+
+/* Camera / per-frame device arrays (reference args of the same names). */
+typedef struct rr_camera {
+    const float* background; /* [3] */
+    const float* viewmatrix; /* [16] */
+    const float* projmatrix; /* [16] */
+    const float* campos;     /* [3] */
+} rr_camera;
+
+/* Gaussian inputs.  Exactly one of shs / colors_precomp, and one of (scales, rotations) /
+ * cov3D_precomp must be non-NULL (checked by the Python layer, __init__.py:183-187). */
+typedef struct rr_gaussians {
+    const float* means3D;
+    const float* shs;
+    const float* colors_precomp;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+} rr_gaussians;
+
+/* ---- scratch sizing (replaces GeometryState/ImageState/BinningState::fromChunk,
+ *      rasterizer_impl.cu:144-183, and required<T>() rasterizer_impl.h:56-62) ---- */
+size_t rr_geometry_bytes(int P);
+size_t rr_image_bytes(int width, int height);
+size_t rr_binning_bytes(int num_rendered, int width, int height);
+size_t rr_backward_workspace_bytes(int P);
+
+/*
+ * Forward, stage 1 (replaces Rasterizer::forward rasterizer_impl.cu:213-277):
+ * preprocess every Gaussian, stable-sort visible Gaussians by depth, prefix-sum their tile
+ * counts, and read back the pair count L (the one device->host sync the reference also has,
+ * rasterizer_impl.cu:273).  Writes radii[P] (int32) and *num_rendered.
+ */
+int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii,
+                        void* geom_buffer, size_t geom_bytes, void* image_buffer, size_t image_bytes,
+                        int* num_rendered, void* stream);
+
+/*
+ * Forward, stage 2 (replaces rasterizer_impl.cu:279-329): expand (tile, Gaussian) pairs in
+ * depth order, stable-sort them by tile, find per-tile ranges and alpha-blend every tile.
+ * out_color [3,H,W], out_depth [1,H,W] are fully written.
+ */
+int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
+                      void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
+                      int num_rendered, float* out_color, float* out_depth, void* stream);
+
+/* Gradient outputs of _C.rasterize_gaussians_backward (rasterize_points.cu:145-153,190).
+ * All arrays are fully written (no pre-zeroing needed). */
+typedef struct rr_grads {
+    float* dL_dmeans2D;   /* [P,3]  (z stays 0) */
+    float* dL_dcolors;    /* [P,3] */
+    float* dL_dopacity;   /* [P,1] */
+    float* dL_dmeans3D;   /* [P,3] */
+    float* dL_dcov3D;     /* [P,6] */
+    float* dL_dsh;        /* [P,M,3] (may be NULL when M == 0) */
+    float* dL_dscales;    /* [P,3] */
+    float* dL_drotations; /* [P,4] */
+} rr_grads;
+
+/*
+ * Backward (replaces Rasterizer::backward rasterizer_impl.cu:334-430 and the zero-filled
+ * allocations of rasterize_points.cu:145-153).  dL_dpix is [3,H,W].
+ */
+int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
+                const void* geom_buffer, const void* image_buffer, const void* binning_buffer,
+                int num_rendered, const float* dL_dpix, void* workspace, size_t workspace_bytes,
+                const rr_grads* out, void* stream);
+
+/* markVisible (rasterize_points.cu:193-212, rasterizer_impl.cu:43-55,130-142): present[P] as 0/1 bytes. */
+int rr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                    uint8_t* present, void* stream);
+
+/* ---- diagnostics ---- */
+const char* rr_last_error(void);
+const char* rr_version(void);
+
+/* Per-stage frame statistics of the last forward on this thread (L, visible count, L_eff...). */
+typedef struct rr_frame_stats {
+    int64_t num_rendered;  /* L */
+    int64_t num_visible;   /* V */
+    int64_t l_eff;         /* sum over tiles of max n_contrib (needs rr_read_frame_stats) */
+    int64_t tiles;         /* T */
+} rr_frame_stats;
+int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* image_buffer, rr_frame_stats* out,
+                        void* stream);
+
+/* Device pointers into the private scratch layout (tests compare them with the oracle's
+ * binning state: per-tile pair order, ranges, n_contrib, final_T). */
+typedef struct rr_debug_views {
+    const uint32_t* point_list; /* [L] Gaussian ids in per-tile depth order */
+    const uint32_t* ranges;     /* [T][2] */
+    const uint32_t* tile_max;   /* [T] max n_contrib per tile */
+    const float* final_T;       /* [H*W] */
+    const uint32_t* n_contrib;  /* [H*W] */
+    const float* splats;        /* [P][12] packed per-Gaussian records (see rr_common.hpp) */
+} rr_debug_views;
+int rr_debug_get_views(const rr_frame* f, const void* geom_buffer, const void* image_buffer,
+                       const void* binning_buffer, int num_rendered, rr_debug_views* out);
+
+/* Kernel timing with HIP events on the launch stream (bench.py's live roofline numbers).
+ * rr_profile_enable(1) starts recording every stage; rr_profile_collect() synchronizes, adds
+ * the elapsed ms per stage into ms[RR_NUM_STAGES] / counts, and clears the record. */
+enum rr_stage {
+    RR_STAGE_PREPROCESS = 0,
+    RR_STAGE_DEPTH_SORT,
+    RR_STAGE_SCAN,
+    RR_STAGE_DUPLICATE,
+    RR_STAGE_TILE_SORT,
+    RR_STAGE_RANGES,
+    RR_STAGE_BLEND_FWD,
+    RR_STAGE_BLEND_BWD,
+    RR_STAGE_GAUSS_BWD,
+    RR_STAGE_MEMSET,
+    RR_NUM_STAGES
+};
+int rr_profile_enable(int enable);
+int rr_profile_collect(double* ms, int64_t* counts);
+const char* rr_stage_name(int stage);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAIN_RASTER_H */

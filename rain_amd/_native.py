@@ -1,0 +1,153 @@
+"""ctypes binding of the C-ABI rasterizer library (include/rain_raster.h).
+
+This is the product path: it loads ``rain_amd/lib/librain_raster.so`` (built by
+rain_amd/_build.py for gfx950) and raises if it is missing — there is no CPU fallback.
+torch is imported first so that the HIP runtime torch ships (SONAME libamdhip64.so.7) is the
+one the library binds to; torch tensors only provide device memory and the stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the HIP library; see module docstring)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_PKG, "lib")
+RASTER_LIB = os.path.join(LIB_DIR, "librain_raster.so")
+KNN_LIB = os.path.join(LIB_DIR, "librain_knn.so")
+
+STAGES = ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd", "blend_bwd",
+          "gauss_bwd", "memset"]
+
+
+class RRFrame(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int), ("width", ctypes.c_int),
+                ("height", ctypes.c_int), ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float),
+                ("scale_modifier", ctypes.c_float), ("low_pass", ctypes.c_float), ("prefiltered", ctypes.c_int),
+                ("debug", ctypes.c_int)]
+
+
+class RRCamera(ctypes.Structure):
+    _fields_ = [("background", ctypes.c_void_p), ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
+                ("campos", ctypes.c_void_p)]
+
+
+class RRGaussians(ctypes.Structure):
+    _fields_ = [("means3D", ctypes.c_void_p), ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
+                ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p), ("rotations", ctypes.c_void_p),
+                ("cov3D_precomp", ctypes.c_void_p)]
+
+
+class RRGrads(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D",
+                                                "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")]
+
+
+class RRFrameStats(ctypes.Structure):
+    _fields_ = [("num_rendered", ctypes.c_int64), ("num_visible", ctypes.c_int64), ("l_eff", ctypes.c_int64),
+                ("tiles", ctypes.c_int64)]
+
+
+class RRDebugViews(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("point_list", "ranges", "tile_max", "final_T", "n_contrib",
+                                                "splats")]
+
+
+# every symbol include/rain_raster.h declares (tests check the .so exports all of them)
+RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
+                  "rr_forward_geometry", "rr_forward_render", "rr_backward", "rr_mark_visible", "rr_last_error",
+                  "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_profile_enable",
+                  "rr_profile_collect", "rr_stage_name"]
+
+_raster = None
+_knn = None
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise ImportError(
+            f"rain_amd: native library {path} is missing. Build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (hipcc, gfx950). There is no CPU fallback for the rasterizer.")
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def raster():
+    """The loaded librain_raster.so with argtypes set."""
+    global _raster
+    if _raster is None:
+        L = _load(RASTER_LIB)
+        vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        for name in ("rr_geometry_bytes", "rr_backward_workspace_bytes"):
+            getattr(L, name).restype = sz
+            getattr(L, name).argtypes = [ci]
+        L.rr_image_bytes.restype = sz
+        L.rr_image_bytes.argtypes = [ci, ci]
+        L.rr_binning_bytes.restype = sz
+        L.rr_binning_bytes.argtypes = [ci, ci, ci]
+        fp, cp, gp = ctypes.POINTER(RRFrame), ctypes.POINTER(RRCamera), ctypes.POINTER(RRGaussians)
+        L.rr_forward_geometry.restype = ci
+        L.rr_forward_geometry.argtypes = [fp, cp, gp, vp, vp, sz, vp, sz, ctypes.POINTER(ci), vp]
+        L.rr_forward_render.restype = ci
+        L.rr_forward_render.argtypes = [fp, cp, gp, vp, vp, vp, vp, sz, ci, vp, vp, vp]
+        L.rr_backward.restype = ci
+        L.rr_backward.argtypes = [fp, cp, gp, vp, vp, vp, vp, ci, vp, vp, sz, ctypes.POINTER(RRGrads), vp]
+        L.rr_mark_visible.restype = ci
+        L.rr_mark_visible.argtypes = [ci, vp, vp, vp, vp, vp]
+        L.rr_last_error.restype = ctypes.c_char_p
+        L.rr_version.restype = ctypes.c_char_p
+        L.rr_read_frame_stats.restype = ci
+        L.rr_read_frame_stats.argtypes = [fp, vp, vp, ctypes.POINTER(RRFrameStats), vp]
+        L.rr_debug_get_views.restype = ci
+        L.rr_debug_get_views.argtypes = [fp, vp, vp, vp, ci, ctypes.POINTER(RRDebugViews)]
+        L.rr_profile_enable.restype = ci
+        L.rr_profile_enable.argtypes = [ci]
+        L.rr_profile_collect.restype = ci
+        L.rr_profile_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+        L.rr_stage_name.restype = ctypes.c_char_p
+        L.rr_stage_name.argtypes = [ci]
+        _raster = L
+    return _raster
+
+
+def knn():
+    global _knn
+    if _knn is None:
+        L = _load(KNN_LIB)
+        L.sk_dist_cuda2.restype = ctypes.c_int
+        L.sk_dist_cuda2.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_size_t, ctypes.c_void_p]
+        L.sk_workspace_bytes.restype = ctypes.c_size_t
+        L.sk_workspace_bytes.argtypes = [ctypes.c_int]
+        L.sk_last_error.restype = ctypes.c_char_p
+        _knn = L
+    return _knn
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = raster().rr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg}")
+
+
+def stream_of(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+class Profiler:
+    """Per-stage kernel time via HIP events recorded by the library on the launch stream."""
+
+    def __enter__(self):
+        raster().rr_profile_enable(1)
+        return self
+
+    def __exit__(self, *exc):
+        raster().rr_profile_enable(0)
+
+    @staticmethod
+    def collect():
+        n = len(STAGES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        check(raster().rr_profile_collect(ms, cnt), "profile collect")
+        return {STAGES[i]: (ms[i], cnt[i]) for i in range(n)}

@@ -1,0 +1,521 @@
+// rr_api.hip — C-ABI entry points (include/rain_raster.h): scratch carving, stage ordering,
+// rocPRIM sorts/scans, the single device->host sync, debug checks and event timing.
+//
+// Replaces CudaRasterizer::Rasterizer::{forward,backward,markVisible}
+// (rasterizer_impl.cu:130-142,187-430) and the pybind wrappers (rasterize_points.cu:24-212).
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rain_raster.h"
+#include "rr_common.hpp"
+#include "rr_kernels.hpp"
+
+using namespace rr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// Bump allocator over an opaque byte buffer (rasterizer_impl.h:10-16 `obtain`).
+struct Carver {
+    char* base;
+    size_t off = 0;
+    explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+    template <typename T>
+    T* take(size_t n) {
+        off = align_up(off);
+        T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+// rasterizer_impl.cu:24-39
+uint32_t higher_msb(uint32_t n) {
+    uint32_t msb = sizeof(n) * 4;
+    uint32_t step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step;
+        else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+
+inline int grid_x(int W) { return (W + TILE_X - 1) / TILE_X; }
+inline int grid_y(int H) { return (H + TILE_Y - 1) / TILE_Y; }
+
+// ---- temp-storage queries (rocPRIM two-phase API) ----
+size_t depth_sort_temp(int P) {
+    size_t bytes = 0;
+    if (P > 0)
+        (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                        rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)P, 0,
+                                        32, (hipStream_t)0);
+    return bytes;
+}
+size_t scan_temp(int P) {
+    size_t bytes = 0;
+    if (P > 0)
+        (void)rocprim::inclusive_scan(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)P,
+                                      rocprim::plus<uint32_t>(), (hipStream_t)0);
+    return bytes;
+}
+template <typename K>
+size_t tile_sort_temp(int L, int bits) {
+    size_t bytes = 0;
+    if (L > 0)
+        (void)rocprim::radix_sort_pairs(nullptr, bytes, (const K*)nullptr, (K*)nullptr, (const uint32_t*)nullptr,
+                                        (uint32_t*)nullptr, (size_t)L, 0, bits, (hipStream_t)0);
+    return bytes;
+}
+
+// ---- scratch layouts ----
+struct Geom {
+    Splat* splats;
+    uint32_t* tiles;
+    uint32_t* depth_keys;
+    uint32_t* depth_keys_sorted;
+    uint32_t* idx_sorted;
+    uint32_t* tiles_sorted;
+    uint32_t* offsets;
+    uint32_t* counters;  // [0] visible count
+    void* temp;
+    size_t temp_bytes;
+    size_t total;
+};
+Geom carve_geom(void* buf, int P) {
+    Carver c(buf);
+    Geom g;
+    const size_t n = (size_t)std::max(P, 1);
+    g.splats = c.take<Splat>(n);
+    g.tiles = c.take<uint32_t>(n);
+    g.depth_keys = c.take<uint32_t>(n);
+    g.depth_keys_sorted = c.take<uint32_t>(n);
+    g.idx_sorted = c.take<uint32_t>(n);
+    g.tiles_sorted = c.take<uint32_t>(n);
+    g.offsets = c.take<uint32_t>(n);
+    g.counters = c.take<uint32_t>(4);
+    g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
+    g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
+    g.total = align_up(c.off);
+    return g;
+}
+
+struct Img {
+    float* final_T;
+    uint32_t* n_contrib;
+    uint2* ranges;
+    uint32_t* tile_max;
+    size_t total;
+};
+Img carve_img(void* buf, int W, int H) {
+    Carver c(buf);
+    Img m;
+    const size_t N = (size_t)std::max(W * H, 1);
+    const size_t T = (size_t)std::max(grid_x(W) * grid_y(H), 1);
+    m.final_T = c.take<float>(N);
+    m.n_contrib = c.take<uint32_t>(N);
+    m.ranges = c.take<uint2>(T);
+    m.tile_max = c.take<uint32_t>(T);
+    m.total = align_up(c.off);
+    return m;
+}
+
+struct Bin {
+    void* keys;
+    void* keys_sorted;
+    uint32_t* vals;
+    uint32_t* point_list;
+    void* temp;
+    size_t temp_bytes;
+    bool wide;  // 32-bit tile keys (T > 65536)
+    int bits;
+    size_t total;
+};
+Bin carve_bin(void* buf, int L, int W, int H) {
+    Carver c(buf);
+    Bin b;
+    const int T = grid_x(W) * grid_y(H);
+    b.wide = T > 65536;
+    b.bits = (int)higher_msb((uint32_t)T);
+    const size_t n = (size_t)std::max(L, 1);
+    if (b.wide) {
+        b.keys = c.take<uint32_t>(n);
+        b.keys_sorted = c.take<uint32_t>(n);
+    } else {
+        b.keys = c.take<uint16_t>(n);
+        b.keys_sorted = c.take<uint16_t>(n);
+    }
+    b.vals = c.take<uint32_t>(n);
+    b.point_list = c.take<uint32_t>(n);
+    b.temp_bytes = b.wide ? tile_sort_temp<uint32_t>(L, b.bits) : tile_sort_temp<uint16_t>(L, b.bits);
+    b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
+    b.total = align_up(c.off);
+    return b;
+}
+
+// ---- event timing (bench.py reads per-stage kernel time through rr_profile_collect) ----
+struct EvRec {
+    int stage;
+    hipEvent_t a, b;
+};
+bool g_prof = false;
+std::vector<EvRec> g_recs;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t ev_get() {
+    if (!g_pool.empty()) {
+        hipEvent_t e = g_pool.back();
+        g_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct StageTimer {
+    int stage;
+    hipStream_t st;
+    hipEvent_t a = nullptr;
+    StageTimer(int s, hipStream_t stream) : stage(s), st(stream) {
+        if (g_prof) {
+            a = ev_get();
+            (void)hipEventRecord(a, st);
+        }
+    }
+    ~StageTimer() {
+        if (g_prof) {
+            hipEvent_t b = ev_get();
+            (void)hipEventRecord(b, st);
+            g_recs.push_back({stage, a, b});
+        }
+    }
+};
+
+// Launch check: always catch launch errors; with `debug`, synchronise and check the kernel
+// (CHECK_CUDA, auxiliary.h:155-162).
+int check(const rr_frame* f, hipStream_t st, const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && f && f->debug) {
+        e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = hipGetLastError();
+    }
+    if (e != hipSuccess) return fail(RR_ERR_HIP, std::string("[HIP ERROR] in ") + what + ": " + hipGetErrorString(e));
+    return RR_OK;
+}
+#define RR_CHECK(call, what)                                                              \
+    do {                                                                                  \
+        hipError_t _e = (call);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(RR_ERR_HIP, std::string("[HIP ERROR] ") + what + ": " + hipGetErrorString(_e)); \
+    } while (0)
+#define RR_STAGE_CHECK(what)                   \
+    do {                                       \
+        int _rc = check(f, st, what);          \
+        if (_rc != RR_OK) return _rc;          \
+    } while (0)
+
+int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, bool forward) {
+    if (!f || !cam || !g) return fail(RR_ERR_ARG, "null frame/camera/gaussians");
+    if (f->P < 0 || f->width <= 0 || f->height <= 0) return fail(RR_ERR_ARG, "bad P/width/height");
+    if (f->P == 0) return RR_OK;
+    if (!g->means3D || (forward && !g->opacities)) return fail(RR_ERR_ARG, "means3D and opacities are required");
+    if (!cam->background || !cam->viewmatrix || !cam->projmatrix || !cam->campos)
+        return fail(RR_ERR_ARG, "camera arrays are required");
+    if ((g->shs == nullptr) == (g->colors_precomp == nullptr))
+        return fail(RR_ERR_ARG, "Please provide excatly one of either SHs or precomputed colors!");
+    const bool sr = g->scales && g->rotations;
+    if (sr == (g->cov3D_precomp != nullptr))
+        return fail(RR_ERR_ARG,
+                    "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (g->shs && (f->D < 0 || f->D > 3 || f->M < (f->D + 1) * (f->D + 1)))
+        return fail(RR_ERR_ARG, "sh_degree must be 0..3 and sh.size(1) >= (degree+1)^2");
+    return RR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rr_last_error(void) { return g_err.c_str(); }
+const char* rr_version(void) { return "rain_amd-raster 0.1 gfx950"; }
+
+size_t rr_geometry_bytes(int P) { return carve_geom(nullptr, P).total; }
+size_t rr_image_bytes(int width, int height) { return carve_img(nullptr, width, height).total; }
+size_t rr_binning_bytes(int num_rendered, int width, int height) {
+    return carve_bin(nullptr, num_rendered, width, height).total;
+}
+size_t rr_backward_workspace_bytes(int P) { return align_up((size_t)std::max(P, 1) * GACC_STRIDE * sizeof(float)); }
+
+int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii, void* geom_buffer,
+                        size_t geom_bytes, void* image_buffer, size_t image_bytes, int* num_rendered, void* stream) {
+    int rc = validate(f, cam, g, true);
+    if (rc) return rc;
+    if (!num_rendered) return fail(RR_ERR_ARG, "num_rendered is null");
+    *num_rendered = 0;
+    const int P = f->P, W = f->width, H = f->height;
+    if (P == 0) return RR_OK;
+    if (!radii || !geom_buffer || !image_buffer) return fail(RR_ERR_ARG, "null output buffer");
+    const Geom gm = carve_geom(geom_buffer, P);
+    const Img im = carve_img(image_buffer, W, H);
+    if (geom_bytes < gm.total || image_bytes < im.total) return fail(RR_ERR_CAPACITY, "scratch buffer too small");
+    hipStream_t st = (hipStream_t)stream;
+
+    PreArgs a{};
+    a.P = P; a.D = f->D; a.M = f->M; a.W = W; a.H = H; a.gx = grid_x(W); a.gy = grid_y(H);
+    a.prefiltered = f->prefiltered;
+    a.tanfovx = f->tan_fovx; a.tanfovy = f->tan_fovy;
+    a.focal_y = H / (2.0f * f->tan_fovy);
+    a.focal_x = W / (2.0f * f->tan_fovx);
+    a.scale_modifier = f->scale_modifier; a.low_pass = f->low_pass;
+    a.means3D = g->means3D; a.shs = g->shs; a.colors_precomp = g->colors_precomp; a.opacities = g->opacities;
+    a.scales = g->scales; a.rotations = g->rotations; a.cov3D_precomp = g->cov3D_precomp;
+    a.view = cam->viewmatrix; a.proj = cam->projmatrix; a.campos = cam->campos;
+    a.radii = radii; a.splats = gm.splats; a.tiles = gm.tiles; a.depth_keys = gm.depth_keys;
+    a.num_visible = gm.counters;
+
+    RR_CHECK(hipMemsetAsync(gm.counters, 0, 4 * sizeof(uint32_t), st), "memset counters");
+    {
+        StageTimer tm(RR_STAGE_PREPROCESS, st);
+        launch_preprocess(a, st);
+    }
+    RR_STAGE_CHECK("preprocess");
+    {
+        StageTimer tm(RR_STAGE_DEPTH_SORT, st);
+        size_t tb = gm.temp_bytes;
+        RR_CHECK(rocprim::radix_sort_pairs(gm.temp, tb, gm.depth_keys, gm.depth_keys_sorted,
+                                           rocprim::counting_iterator<uint32_t>(0), gm.idx_sorted, (size_t)P, 0, 32,
+                                           st),
+                 "depth sort");
+    }
+    RR_STAGE_CHECK("depth sort");
+    {
+        StageTimer tm(RR_STAGE_SCAN, st);
+        launch_gather_tiles(P, gm.idx_sorted, gm.tiles, gm.tiles_sorted, st);
+        size_t tb = gm.temp_bytes;
+        RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, gm.tiles_sorted, gm.offsets, (size_t)P,
+                                         rocprim::plus<uint32_t>(), st),
+                 "tile-count scan");
+    }
+    RR_STAGE_CHECK("scan");
+    uint32_t L = 0;
+    RR_CHECK(hipMemcpyAsync(&L, gm.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, st), "read L");
+    RR_CHECK(hipStreamSynchronize(st), "sync L");
+    if (L > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^31 tile/Gaussian pairs");
+    *num_rendered = (int)L;
+    return RR_OK;
+}
+
+int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
+                      void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
+                      int num_rendered, float* out_color, float* out_depth, void* stream) {
+    int rc = validate(f, cam, g, true);
+    if (rc) return rc;
+    const int P = f->P, W = f->width, H = f->height, L = num_rendered;
+    if (P == 0) return RR_OK;
+    if (!out_color || !out_depth || !geom_buffer || !image_buffer || (L > 0 && !binning_buffer))
+        return fail(RR_ERR_ARG, "null buffer");
+    const Geom gm = carve_geom(geom_buffer, P);
+    const Img im = carve_img(image_buffer, W, H);
+    const Bin bn = carve_bin(binning_buffer, L, W, H);
+    if (L > 0 && binning_bytes < bn.total) return fail(RR_ERR_CAPACITY, "binning buffer too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int gx = grid_x(W), gy = grid_y(H), T = gx * gy;
+
+    if (L > 0) {
+        {
+            StageTimer tm(RR_STAGE_DUPLICATE, st);
+            if (bn.wide)
+                launch_duplicate<uint32_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy,
+                                           (uint32_t*)bn.keys, bn.vals, st);
+            else
+                launch_duplicate<uint16_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy,
+                                           (uint16_t*)bn.keys, bn.vals, st);
+        }
+        RR_STAGE_CHECK("duplicate");
+        {
+            StageTimer tm(RR_STAGE_TILE_SORT, st);
+            size_t tb = bn.temp_bytes;
+            if (bn.wide)
+                RR_CHECK(rocprim::radix_sort_pairs(bn.temp, tb, (const uint32_t*)bn.keys, (uint32_t*)bn.keys_sorted,
+                                                   (const uint32_t*)bn.vals, bn.point_list, (size_t)L, 0, bn.bits,
+                                                   st),
+                         "tile sort");
+            else
+                RR_CHECK(rocprim::radix_sort_pairs(bn.temp, tb, (const uint16_t*)bn.keys, (uint16_t*)bn.keys_sorted,
+                                                   (const uint32_t*)bn.vals, bn.point_list, (size_t)L, 0, bn.bits,
+                                                   st),
+                         "tile sort");
+        }
+        RR_STAGE_CHECK("tile sort");
+    }
+    {
+        StageTimer tm(RR_STAGE_RANGES, st);
+        RR_CHECK(hipMemsetAsync(im.ranges, 0, (size_t)T * sizeof(uint2), st), "memset ranges");
+        if (L > 0) {
+            if (bn.wide) launch_ranges<uint32_t>(L, (const uint32_t*)bn.keys_sorted, im.ranges, st);
+            else launch_ranges<uint16_t>(L, (const uint16_t*)bn.keys_sorted, im.ranges, st);
+        }
+    }
+    RR_STAGE_CHECK("ranges");
+    {
+        StageTimer tm(RR_STAGE_BLEND_FWD, st);
+        BlendFwdArgs b{};
+        b.W = W; b.H = H; b.gx = gx; b.gy = gy;
+        b.ranges = im.ranges; b.point_list = bn.point_list; b.splats = gm.splats; b.bg = cam->background;
+        b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
+        b.out_color = out_color; b.out_depth = out_depth;
+        launch_blend_fwd(b, st);
+    }
+    RR_STAGE_CHECK("blend forward");
+    return RR_OK;
+}
+
+int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
+                const void* geom_buffer, const void* image_buffer, const void* binning_buffer, int num_rendered,
+                const float* dL_dpix, void* workspace, size_t workspace_bytes, const rr_grads* out, void* stream) {
+    int rc = validate(f, cam, g, false);
+    if (rc) return rc;
+    const int P = f->P, W = f->width, H = f->height, L = num_rendered;
+    if (P == 0) return RR_OK;
+    if (!out || !dL_dpix || !radii || !geom_buffer || !image_buffer || !workspace)
+        return fail(RR_ERR_ARG, "null buffer");
+    if (!out->dL_dmeans2D || !out->dL_dcolors || !out->dL_dopacity || !out->dL_dmeans3D || !out->dL_dcov3D ||
+        !out->dL_dscales || !out->dL_drotations || (f->M > 0 && !out->dL_dsh))
+        return fail(RR_ERR_ARG, "null gradient output");
+    if (workspace_bytes < rr_backward_workspace_bytes(P)) return fail(RR_ERR_CAPACITY, "workspace too small");
+    const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
+    const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
+    const Bin bn = carve_bin(const_cast<void*>(binning_buffer), L, W, H);
+    hipStream_t st = (hipStream_t)stream;
+    const int gx = grid_x(W), gy = grid_y(H);
+    float* gacc = static_cast<float*>(workspace);
+    {
+        StageTimer tm(RR_STAGE_MEMSET, st);
+        RR_CHECK(hipMemsetAsync(gacc, 0, (size_t)P * GACC_STRIDE * sizeof(float), st), "memset accumulators");
+    }
+    if (L > 0) {
+        StageTimer tm(RR_STAGE_BLEND_BWD, st);
+        BlendBwdArgs b{};
+        b.W = W; b.H = H; b.gx = gx; b.gy = gy;
+        b.ranges = im.ranges; b.point_list = bn.point_list; b.splats = gm.splats; b.tile_max = im.tile_max;
+        b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.bg = cam->background; b.dL_dpix = dL_dpix;
+        b.gacc = gacc;
+        launch_blend_bwd(b, st);
+    }
+    RR_STAGE_CHECK("blend backward");
+    {
+        StageTimer tm(RR_STAGE_GAUSS_BWD, st);
+        GaussBwdArgs a{};
+        a.P = P; a.D = f->D; a.M = f->M;
+        a.tanfovx = f->tan_fovx; a.tanfovy = f->tan_fovy;
+        a.focal_y = H / (2.0f * f->tan_fovy);
+        a.focal_x = W / (2.0f * f->tan_fovx);
+        a.scale_modifier = f->scale_modifier; a.low_pass = f->low_pass;
+        a.means3D = g->means3D; a.shs = g->shs; a.scales = g->scales; a.rotations = g->rotations;
+        a.cov3D_precomp = g->cov3D_precomp; a.view = cam->viewmatrix; a.proj = cam->projmatrix;
+        a.campos = cam->campos; a.radii = radii; a.gacc = gacc;
+        a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
+        a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = f->M > 0 ? out->dL_dsh : nullptr;
+        a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
+        launch_gauss_bwd(a, st);
+    }
+    RR_STAGE_CHECK("gaussian backward");
+    return RR_OK;
+}
+
+int rr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
+                    void* stream) {
+    (void)projmatrix;
+    if (P < 0) return fail(RR_ERR_ARG, "bad P");
+    if (P == 0) return RR_OK;
+    if (!means3D || !viewmatrix || !present) return fail(RR_ERR_ARG, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    launch_mark_visible(P, means3D, viewmatrix, present, st);
+    return check(nullptr, st, "mark_visible");
+}
+
+int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* image_buffer, rr_frame_stats* out,
+                        void* stream) {
+    if (!f || !out) return fail(RR_ERR_ARG, "null");
+    std::memset(out, 0, sizeof(*out));
+    const int P = f->P, W = f->width, H = f->height;
+    const int T = grid_x(W) * grid_y(H);
+    out->tiles = T;
+    if (P == 0) return RR_OK;
+    const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
+    const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t vis = 0, L = 0;
+    std::vector<uint32_t> tm(T);
+    RR_CHECK(hipMemcpyAsync(&vis, gm.counters, 4, hipMemcpyDeviceToHost, st), "stats");
+    RR_CHECK(hipMemcpyAsync(&L, gm.offsets + (P - 1), 4, hipMemcpyDeviceToHost, st), "stats");
+    RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
+    RR_CHECK(hipStreamSynchronize(st), "stats");
+    out->num_visible = vis;
+    out->num_rendered = L;
+    int64_t s = 0;
+    for (uint32_t v : tm) s += v;
+    out->l_eff = s;
+    return RR_OK;
+}
+
+int rr_debug_get_views(const rr_frame* f, const void* geom_buffer, const void* image_buffer,
+                       const void* binning_buffer, int num_rendered, rr_debug_views* out) {
+    if (!f || !out) return fail(RR_ERR_ARG, "null");
+    const Geom gm = carve_geom(const_cast<void*>(geom_buffer), f->P);
+    const Img im = carve_img(const_cast<void*>(image_buffer), f->width, f->height);
+    const Bin bn = carve_bin(const_cast<void*>(binning_buffer), num_rendered, f->width, f->height);
+    out->point_list = bn.point_list;
+    out->ranges = reinterpret_cast<const uint32_t*>(im.ranges);
+    out->tile_max = im.tile_max;
+    out->final_T = im.final_T;
+    out->n_contrib = im.n_contrib;
+    out->splats = reinterpret_cast<const float*>(gm.splats);
+    return RR_OK;
+}
+
+int rr_profile_enable(int enable) {
+    g_prof = enable != 0;
+    return RR_OK;
+}
+
+int rr_profile_collect(double* ms, int64_t* counts) {
+    for (auto& r : g_recs) {
+        RR_CHECK(hipEventSynchronize(r.b), "profile sync");
+        float e = 0.f;
+        RR_CHECK(hipEventElapsedTime(&e, r.a, r.b), "profile elapsed");
+        if (ms) ms[r.stage] += e;
+        if (counts) counts[r.stage] += 1;
+        g_pool.push_back(r.a);
+        g_pool.push_back(r.b);
+    }
+    g_recs.clear();
+    return RR_OK;
+}
+
+const char* rr_stage_name(int stage) {
+    static const char* names[RR_NUM_STAGES] = {"preprocess", "depth_sort", "scan", "duplicate", "tile_sort",
+                                               "ranges", "blend_fwd", "blend_bwd", "gauss_bwd", "memset"};
+    return (stage >= 0 && stage < RR_NUM_STAGES) ? names[stage] : "?";
+}
+
+}  // extern "C"

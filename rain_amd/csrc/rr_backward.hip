@@ -1,0 +1,411 @@
+// rr_backward.hip — backward kernels of the MI355X rasterizer.
+//
+//   k_blend_bwd        per-tile back-to-front replay (backward.cu:389-547 semantics)
+//   k_gauss_bwd<DEG>   one thread per Gaussian: the reference's computeCov2DCUDA
+//                      (backward.cu:133-264) + preprocessCUDA (backward.cu:336-386, SH bwd :9-128,
+//                      cov3D bwd :268-331) fused, writing every gradient output exactly once
+//                      (so the host allocates them uninitialised — no zero-fill pass).
+//
+// Gradient accumulation: the reference issues 9 fp32 atomicAdds per contributing
+// (pixel, Gaussian) pair.  On MI355X float atomics are executed memory-side at ~1.3 TB/s
+// chip-wide, so here each wave first sums its 64 pixels' contributions with DPP (no LDS),
+// lane 63 parks the 9 wave sums in LDS, and after each 256-pair round the workgroup adds the
+// four waves' sums and issues ONE atomic per (tile, Gaussian, component), laid out so that a
+// pair's 9 adds fall into one 64-B line.  Pairs no pixel of a wave touched are skipped by ballot.
+#include "rr_common.hpp"
+#include "rr_kernels.hpp"
+
+namespace rr {
+
+__global__ __launch_bounds__(256) void k_blend_bwd(BlendBwdArgs a) {
+    const int tile = blockIdx.x;
+    const int tx = tile % a.gx, ty = tile / a.gx;
+    const int t = threadIdx.x;
+    const int w = t >> 6;
+    const int lane = t & 63;
+    const int px = tx * TILE_X + (t & 15), py = ty * TILE_Y + (t >> 4);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+
+    __shared__ float4 s_a[TILE_PIX];
+    __shared__ float4 s_b[TILE_PIX];
+    __shared__ float4 s_c[TILE_PIX];
+    __shared__ uint32_t s_id[TILE_PIX];
+    __shared__ float s_g[4][TILE_PIX * NGRAD];
+
+    const uint2 range = a.ranges[tile];
+    const int nmax = (int)a.tile_max[tile];  // pairs past this index were blended by no pixel
+    const size_t HW = (size_t)a.H * a.W;
+    const int pix = a.W * py + px;
+
+    const float T_final = inside ? a.final_T[pix] : 0.f;
+    float T = T_final;
+    const int last_contributor = inside ? (int)a.n_contrib[pix] : 0;
+    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+    if (inside) {
+        dp0 = a.dL_dpix[pix];
+        dp1 = a.dL_dpix[HW + pix];
+        dp2 = a.dL_dpix[2 * HW + pix];
+    }
+    const float bg_dot_dpixel = a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2;
+    float ar0 = 0.f, ar1 = 0.f, ar2 = 0.f;  // accum_rec
+    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;  // last_color
+    float last_alpha = 0.f;
+    const float ddelx_dx = 0.5f * a.W;
+    const float ddely_dy = 0.5f * a.H;
+
+    for (int base = 0; base < nmax; base += TILE_PIX) {
+        __syncthreads();
+        const int k = base + t;
+        if (k < nmax) {
+            const uint32_t g = a.point_list[range.x + nmax - 1 - k];
+            const Splat s = a.splats[g];
+            s_id[t] = g;
+            s_a[t] = s.a;
+            s_b[t] = s.b;
+            s_c[t] = s.c;
+        }
+        __syncthreads();
+        const int cnt = min(TILE_PIX, nmax - base);
+        for (int j = 0; j < cnt; j++) {
+            const int contributor = nmax - 1 - (base + j);
+            const float4 A = s_a[j];
+            const float4 B = s_b[j];
+            const float dx = A.x - pfx, dy = A.y - pfy;
+            const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
+            const float G = __expf(power);
+            const float alpha = fminf(0.99f, B.y * G);
+            const bool act = contributor < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
+            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
+            if (act) {
+                T = __fdividef(T, 1.f - alpha);
+                const float dchannel_dcolor = alpha * T;
+                const float4 Cc = s_c[j];
+                ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
+                ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1;
+                ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2;
+                lc0 = Cc.x;
+                lc1 = Cc.y;
+                lc2 = Cc.z;
+                float dL_dalpha = (Cc.x - ar0) * dp0 + (Cc.y - ar1) * dp1 + (Cc.z - ar2) * dp2;
+                g6 = dchannel_dcolor * dp0;
+                g7 = dchannel_dcolor * dp1;
+                g8 = dchannel_dcolor * dp2;
+                dL_dalpha *= T;
+                last_alpha = alpha;
+                dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
+                const float dL_dG = B.y * dL_dalpha;
+                const float gdx = G * dx, gdy = G * dy;
+                const float dG_ddelx = -gdx * A.z - gdy * A.w;
+                const float dG_ddely = -gdy * B.x - gdx * A.w;
+                g0 = dL_dG * dG_ddelx * ddelx_dx;
+                g1 = dL_dG * dG_ddely * ddely_dy;
+                g2 = -0.5f * gdx * dx * dL_dG;
+                g3 = -0.5f * gdx * dy * dL_dG;
+                g4 = -0.5f * gdy * dy * dL_dG;
+                g5 = G * dL_dalpha;
+            }
+            float* sg = &s_g[w][j * NGRAD];
+            if (__ballot(act) != 0ull) {
+                g0 = wave_sum_lane63(g0);
+                g1 = wave_sum_lane63(g1);
+                g2 = wave_sum_lane63(g2);
+                g3 = wave_sum_lane63(g3);
+                g4 = wave_sum_lane63(g4);
+                g5 = wave_sum_lane63(g5);
+                g6 = wave_sum_lane63(g6);
+                g7 = wave_sum_lane63(g7);
+                g8 = wave_sum_lane63(g8);
+                if (lane == 63) {
+                    sg[0] = g0; sg[1] = g1; sg[2] = g2; sg[3] = g3; sg[4] = g4;
+                    sg[5] = g5; sg[6] = g6; sg[7] = g7; sg[8] = g8;
+                }
+            } else if (lane == 63) {
+#pragma unroll
+                for (int c = 0; c < NGRAD; c++) sg[c] = 0.f;
+            }
+        }
+        __syncthreads();
+        // one atomic per (pair, component); consecutive lanes hit consecutive components of a pair
+#pragma unroll
+        for (int c = 0; c < NGRAD; c++) {
+            const int e = c * TILE_PIX + t;
+            const int pair = e / NGRAD;
+            if (pair < cnt) {
+                const float v = s_g[0][e] + s_g[1][e] + s_g[2][e] + s_g[3][e];
+                if (v != 0.f) atomicAdd(a.gacc + (size_t)s_id[pair] * GACC_STRIDE + (e - pair * NGRAD), v);
+            }
+        }
+    }
+}
+
+// ---- per-Gaussian backward -------------------------------------------------------------
+
+// SH backward (backward.cu:9-128): writes dL_dsh[0..K) and returns dL/d(dir) via dRGBd{x,y,z}.
+template <int DEG>
+__device__ __forceinline__ v3 sh_backward(v3 dir, const float* sh, v3 dL_dRGB, float* dsh) {
+    const float x = dir.x, y = dir.y, z = dir.z;
+    v3 dRGBdx = mk(0, 0, 0), dRGBdy = mk(0, 0, 0), dRGBdz = mk(0, 0, 0);
+    auto W = [&](int k, float s) {
+        dsh[3 * k + 0] = s * dL_dRGB.x;
+        dsh[3 * k + 1] = s * dL_dRGB.y;
+        dsh[3 * k + 2] = s * dL_dRGB.z;
+    };
+    W(0, RR_SH_C0);
+    if (DEG > 0) {
+        W(1, -RR_SH_C1 * y);
+        W(2, RR_SH_C1 * z);
+        W(3, -RR_SH_C1 * x);
+        dRGBdx = -RR_SH_C1 * load3(sh + 9);
+        dRGBdy = -RR_SH_C1 * load3(sh + 3);
+        dRGBdz = RR_SH_C1 * load3(sh + 6);
+        if (DEG > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            W(4, RR_SH_C2_0 * xy);
+            W(5, RR_SH_C2_1 * yz);
+            W(6, RR_SH_C2_2 * (2.f * zz - xx - yy));
+            W(7, RR_SH_C2_3 * xz);
+            W(8, RR_SH_C2_4 * (xx - yy));
+            const v3 s4 = load3(sh + 12), s5 = load3(sh + 15), s6 = load3(sh + 18), s7 = load3(sh + 21),
+                     s8 = load3(sh + 24);
+            dRGBdx = dRGBdx + ((RR_SH_C2_0 * y) * s4 + (RR_SH_C2_2 * 2.f * -x) * s6 + (RR_SH_C2_3 * z) * s7 +
+                               (RR_SH_C2_4 * 2.f * x) * s8);
+            dRGBdy = dRGBdy + ((RR_SH_C2_0 * x) * s4 + (RR_SH_C2_1 * z) * s5 + (RR_SH_C2_2 * 2.f * -y) * s6 +
+                               (RR_SH_C2_4 * 2.f * -y) * s8);
+            dRGBdz = dRGBdz + ((RR_SH_C2_1 * y) * s5 + (RR_SH_C2_2 * 2.f * 2.f * z) * s6 + (RR_SH_C2_3 * x) * s7);
+            if (DEG > 2) {
+                W(9, RR_SH_C3_0 * y * (3.f * xx - yy));
+                W(10, RR_SH_C3_1 * xy * z);
+                W(11, RR_SH_C3_2 * y * (4.f * zz - xx - yy));
+                W(12, RR_SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy));
+                W(13, RR_SH_C3_4 * x * (4.f * zz - xx - yy));
+                W(14, RR_SH_C3_5 * z * (xx - yy));
+                W(15, RR_SH_C3_6 * x * (xx - 3.f * yy));
+                const v3 s9 = load3(sh + 27), s10 = load3(sh + 30), s11 = load3(sh + 33), s12 = load3(sh + 36),
+                         s13 = load3(sh + 39), s14 = load3(sh + 42), s15 = load3(sh + 45);
+                dRGBdx = dRGBdx + ((RR_SH_C3_0 * 3.f * 2.f * xy) * s9 + (RR_SH_C3_1 * yz) * s10 +
+                                   (RR_SH_C3_2 * -2.f * xy) * s11 + (RR_SH_C3_3 * -3.f * 2.f * xz) * s12 +
+                                   (RR_SH_C3_4 * (-3.f * xx + 4.f * zz - yy)) * s13 + (RR_SH_C3_5 * 2.f * xz) * s14 +
+                                   (RR_SH_C3_6 * 3.f * (xx - yy)) * s15);
+                dRGBdy = dRGBdy + ((RR_SH_C3_0 * 3.f * (xx - yy)) * s9 + (RR_SH_C3_1 * xz) * s10 +
+                                   (RR_SH_C3_2 * (-3.f * yy + 4.f * zz - xx)) * s11 +
+                                   (RR_SH_C3_3 * -3.f * 2.f * yz) * s12 + (RR_SH_C3_4 * -2.f * xy) * s13 +
+                                   (RR_SH_C3_5 * -2.f * yz) * s14 + (RR_SH_C3_6 * -3.f * 2.f * xy) * s15);
+                dRGBdz = dRGBdz + ((RR_SH_C3_1 * xy) * s10 + (RR_SH_C3_2 * 4.f * 2.f * yz) * s11 +
+                                   (RR_SH_C3_3 * 3.f * (2.f * zz - xx - yy)) * s12 +
+                                   (RR_SH_C3_4 * 4.f * 2.f * xz) * s13 + (RR_SH_C3_5 * (xx - yy)) * s14);
+            }
+        }
+    }
+    return mk(dot(dRGBdx, dL_dRGB), dot(dRGBdy, dL_dRGB), dot(dRGBdz, dL_dRGB));
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const int M = a.M;
+    float* dsh = a.dL_dsh ? a.dL_dsh + (size_t)idx * M * 3 : nullptr;
+    float* dmean2 = a.dL_dmeans2D + 3 * (size_t)idx;
+    float* dcol = a.dL_dcolors + 3 * (size_t)idx;
+    float* dmean3 = a.dL_dmeans3D + 3 * (size_t)idx;
+    float* dcov = a.dL_dcov3D + 6 * (size_t)idx;
+    float* dscale = a.dL_dscales + 3 * (size_t)idx;
+    float4* drot = reinterpret_cast<float4*>(a.dL_drot) + idx;
+
+    if (!(a.radii[idx] > 0)) {  // untouched Gaussians: exact zeros (backward.cu:146,357)
+        dmean2[0] = dmean2[1] = dmean2[2] = 0.f;
+        dcol[0] = dcol[1] = dcol[2] = 0.f;
+        a.dL_dopacity[idx] = 0.f;
+        dmean3[0] = dmean3[1] = dmean3[2] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; i++) dcov[i] = 0.f;
+        if (dsh)
+            for (int i = 0; i < 3 * M; i++) dsh[i] = 0.f;
+        dscale[0] = dscale[1] = dscale[2] = 0.f;
+        *drot = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+
+    const float* gp = a.gacc + (size_t)idx * GACC_STRIDE;
+    const float4 ga = *reinterpret_cast<const float4*>(gp);
+    const float4 gb = *reinterpret_cast<const float4*>(gp + 4);
+    const float g8 = gp[8];
+    const float dm2x = ga.x, dm2y = ga.y;
+    const float dcx = ga.z, dcy = ga.w, dcz = gb.x;
+    dmean2[0] = dm2x;
+    dmean2[1] = dm2y;
+    dmean2[2] = 0.f;
+    dcol[0] = gb.z;
+    dcol[1] = gb.w;
+    dcol[2] = g8;
+    a.dL_dopacity[idx] = gb.y;
+
+    const v3 mean = load3(a.means3D + 3 * (size_t)idx);
+    float cov[6];
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    v3 scale = mk(0.f, 0.f, 0.f);
+    if (a.cov3D_precomp) {
+        const float* c = a.cov3D_precomp + 6 * (size_t)idx;
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov[i] = c[i];
+    } else {
+        q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        scale = load3(a.scales + 3 * (size_t)idx);
+        cov3d_from_scale_rot(scale, a.scale_modifier, q, cov);  // identical to the forward's value
+    }
+
+    // ---- computeCov2DCUDA (backward.cu:154-263) ----
+    const Proj2D pr = ewa_setup(mean, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view);
+    const float x_grad_mul = pr.txtz < -pr.limx || pr.txtz > pr.limx ? 0.f : 1.f;
+    const float y_grad_mul = pr.tytz < -pr.limy || pr.tytz > pr.limy ? 0.f : 1.f;
+    float ca, cb, cc;
+    ewa_cov2d(pr, cov, ca, cb, cc);
+    ca += a.low_pass;
+    cc += a.low_pass;
+    const float denom = ca * cc - cb * cb;
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const float(&T)[2][3] = pr.A;
+    float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (denom2inv != 0.f) {
+        dL_da = denom2inv * (-cc * cc * dcx + 2 * cb * cc * dcy + (denom - ca * cc) * dcz);
+        dL_dc = denom2inv * (-ca * ca * dcz + 2 * ca * cb * dcy + (denom - ca * cc) * dcx);
+        dL_db = denom2inv * 2 * (cb * cc * dcx - (denom + 2 * cb * cb) * dcy + ca * cb * dcz);
+        dc[0] = (T[0][0] * T[0][0] * dL_da + T[0][0] * T[1][0] * dL_db + T[1][0] * T[1][0] * dL_dc);
+        dc[3] = (T[0][1] * T[0][1] * dL_da + T[0][1] * T[1][1] * dL_db + T[1][1] * T[1][1] * dL_dc);
+        dc[5] = (T[0][2] * T[0][2] * dL_da + T[0][2] * T[1][2] * dL_db + T[1][2] * T[1][2] * dL_dc);
+        dc[1] = 2 * T[0][0] * T[0][1] * dL_da + (T[0][0] * T[1][1] + T[0][1] * T[1][0]) * dL_db +
+                2 * T[1][0] * T[1][1] * dL_dc;
+        dc[2] = 2 * T[0][0] * T[0][2] * dL_da + (T[0][0] * T[1][2] + T[0][2] * T[1][0]) * dL_db +
+                2 * T[1][0] * T[1][2] * dL_dc;
+        dc[4] = 2 * T[0][2] * T[0][1] * dL_da + (T[0][1] * T[1][2] + T[0][2] * T[1][1]) * dL_db +
+                2 * T[1][1] * T[1][2] * dL_dc;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) dcov[i] = dc[i];
+    const float V[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
+    const float dL_dT00 = 2 * (T[0][0] * V[0][0] + T[0][1] * V[0][1] + T[0][2] * V[0][2]) * dL_da +
+                          (T[1][0] * V[0][0] + T[1][1] * V[0][1] + T[1][2] * V[0][2]) * dL_db;
+    const float dL_dT01 = 2 * (T[0][0] * V[1][0] + T[0][1] * V[1][1] + T[0][2] * V[1][2]) * dL_da +
+                          (T[1][0] * V[1][0] + T[1][1] * V[1][1] + T[1][2] * V[1][2]) * dL_db;
+    const float dL_dT02 = 2 * (T[0][0] * V[2][0] + T[0][1] * V[2][1] + T[0][2] * V[2][2]) * dL_da +
+                          (T[1][0] * V[2][0] + T[1][1] * V[2][1] + T[1][2] * V[2][2]) * dL_db;
+    const float dL_dT10 = 2 * (T[1][0] * V[0][0] + T[1][1] * V[0][1] + T[1][2] * V[0][2]) * dL_dc +
+                          (T[0][0] * V[0][0] + T[0][1] * V[0][1] + T[0][2] * V[0][2]) * dL_db;
+    const float dL_dT11 = 2 * (T[1][0] * V[1][0] + T[1][1] * V[1][1] + T[1][2] * V[1][2]) * dL_dc +
+                          (T[0][0] * V[1][0] + T[0][1] * V[1][1] + T[0][2] * V[1][2]) * dL_db;
+    const float dL_dT12 = 2 * (T[1][0] * V[2][0] + T[1][1] * V[2][1] + T[1][2] * V[2][2]) * dL_dc +
+                          (T[0][0] * V[2][0] + T[0][1] * V[2][1] + T[0][2] * V[2][2]) * dL_db;
+    const float* vm = a.view;  // glm W[i][j] == vm[4j+i]
+    const float dL_dJ00 = vm[0] * dL_dT00 + vm[4] * dL_dT01 + vm[8] * dL_dT02;
+    const float dL_dJ02 = vm[2] * dL_dT00 + vm[6] * dL_dT01 + vm[10] * dL_dT02;
+    const float dL_dJ11 = vm[1] * dL_dT10 + vm[5] * dL_dT11 + vm[9] * dL_dT12;
+    const float dL_dJ12 = vm[2] * dL_dT10 + vm[6] * dL_dT11 + vm[10] * dL_dT12;
+    const v3 t = pr.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -a.focal_x * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -a.focal_y * tz2 * dL_dJ12;
+    const float dL_dtz = -a.focal_x * tz2 * dL_dJ00 - a.focal_y * tz2 * dL_dJ11 +
+                         (2 * a.focal_x * t.x) * tz3 * dL_dJ02 + (2 * a.focal_y * t.y) * tz3 * dL_dJ12;
+    v3 dmean = xform_vec_4x3_T(mk(dL_dtx, dL_dty, dL_dtz), a.view);
+
+    // ---- preprocessCUDA bwd: mean2D -> mean3D (backward.cu:360-377) ----
+    const float* pj = a.proj;
+    const float4 m_hom = xform_point_4x4(mean, pj);
+    const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+    const float mul1 = (pj[0] * mean.x + pj[4] * mean.y + pj[8] * mean.z + pj[12]) * m_w * m_w;
+    const float mul2 = (pj[1] * mean.x + pj[5] * mean.y + pj[9] * mean.z + pj[13]) * m_w * m_w;
+    dmean.x += (pj[0] * m_w - pj[3] * mul1) * dm2x + (pj[1] * m_w - pj[3] * mul2) * dm2y;
+    dmean.y += (pj[4] * m_w - pj[7] * mul1) * dm2x + (pj[5] * m_w - pj[7] * mul2) * dm2y;
+    dmean.z += (pj[8] * m_w - pj[11] * mul1) * dm2x + (pj[9] * m_w - pj[11] * mul2) * dm2y;
+
+    // ---- SH bwd (backward.cu:9-128); the clamp mask is recomputed from the forward SH value ----
+    if (a.shs) {
+        const float* sh = a.shs + (size_t)idx * M * 3;
+        const v3 cp = load3(a.campos);
+        const v3 dir_orig = mean - cp;
+        const float len = sqrtf(dot(dir_orig, dir_orig));
+        const v3 dir = mk(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+        const v3 rgb = sh_eval<DEG>(dir, sh);
+        v3 dL_dRGB = mk(gb.z, gb.w, g8);
+        dL_dRGB.x *= rgb.x < 0 ? 0.f : 1.f;
+        dL_dRGB.y *= rgb.y < 0 ? 0.f : 1.f;
+        dL_dRGB.z *= rgb.z < 0 ? 0.f : 1.f;
+        const v3 dL_ddir = sh_backward<DEG>(dir, sh, dL_dRGB, dsh);
+        constexpr int K = (DEG + 1) * (DEG + 1);
+        for (int i = 3 * K; i < 3 * M; i++) dsh[i] = 0.f;
+        // dnormvdv (auxiliary.h:96-106)
+        const v3 v = dir_orig;
+        const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+        dmean.x += ((+sum2 - v.x * v.x) * dL_ddir.x - v.y * v.x * dL_ddir.y - v.z * v.x * dL_ddir.z) * invsum32;
+        dmean.y += (-v.x * v.y * dL_ddir.x + (sum2 - v.y * v.y) * dL_ddir.y - v.z * v.y * dL_ddir.z) * invsum32;
+        dmean.z += (-v.x * v.z * dL_ddir.x - v.y * v.z * dL_ddir.y + (sum2 - v.z * v.z) * dL_ddir.z) * invsum32;
+    } else if (dsh) {
+        for (int i = 0; i < 3 * M; i++) dsh[i] = 0.f;
+    }
+    dmean3[0] = dmean.x;
+    dmean3[1] = dmean.y;
+    dmean3[2] = dmean.z;
+
+    // ---- cov3D bwd (backward.cu:268-331) ----
+    if (a.scales) {
+        const float r = q.x, x = q.y, y = q.z, z = q.w;
+        float R[3][3];
+        quat_rot(q, R);
+        const float s[3] = {a.scale_modifier * scale.x, a.scale_modifier * scale.y, a.scale_modifier * scale.z};
+        float Mm[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) Mm[i][j] = s[i] * R[j][i];
+        const float dS[3][3] = {{dc[0], 0.5f * dc[1], 0.5f * dc[2]},
+                                {0.5f * dc[1], dc[3], 0.5f * dc[4]},
+                                {0.5f * dc[2], 0.5f * dc[4], dc[5]}};
+        float dM[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                dM[i][j] = 2.0f * Mm[i][0] * dS[0][j] + 2.0f * Mm[i][1] * dS[1][j] + 2.0f * Mm[i][2] * dS[2][j];
+#pragma unroll
+        for (int i = 0; i < 3; i++) dscale[i] = R[0][i] * dM[i][0] + R[1][i] * dM[i][1] + R[2][i] * dM[i][2];
+        float Gm[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) Gm[i][j] = dM[i][j] * s[i];
+        float4 dq;
+        dq.x = 2 * z * (Gm[0][1] - Gm[1][0]) + 2 * y * (Gm[2][0] - Gm[0][2]) + 2 * x * (Gm[1][2] - Gm[2][1]);
+        dq.y = 2 * y * (Gm[1][0] + Gm[0][1]) + 2 * z * (Gm[2][0] + Gm[0][2]) + 2 * r * (Gm[1][2] - Gm[2][1]) -
+               4 * x * (Gm[2][2] + Gm[1][1]);
+        dq.z = 2 * x * (Gm[1][0] + Gm[0][1]) + 2 * r * (Gm[2][0] - Gm[0][2]) + 2 * z * (Gm[1][2] + Gm[2][1]) -
+               4 * y * (Gm[2][2] + Gm[0][0]);
+        dq.w = 2 * r * (Gm[0][1] - Gm[1][0]) + 2 * x * (Gm[2][0] + Gm[0][2]) + 2 * y * (Gm[1][2] + Gm[2][1]) -
+               4 * z * (Gm[1][1] + Gm[0][0]);
+        *drot = dq;
+    } else {
+        dscale[0] = dscale[1] = dscale[2] = 0.f;
+        *drot = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
+    const int T = a.gx * a.gy;
+    if (T == 0) return;
+    k_blend_bwd<<<T, TILE_PIX, 0, st>>>(a);
+}
+
+void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st) {
+    if (a.P == 0) return;
+    const int nb = (a.P + 255) / 256;
+    switch (a.shs ? a.D : 0) {
+        case 0: k_gauss_bwd<0><<<nb, 256, 0, st>>>(a); break;
+        case 1: k_gauss_bwd<1><<<nb, 256, 0, st>>>(a); break;
+        case 2: k_gauss_bwd<2><<<nb, 256, 0, st>>>(a); break;
+        default: k_gauss_bwd<3><<<nb, 256, 0, st>>>(a); break;
+    }
+}
+
+}  // namespace rr

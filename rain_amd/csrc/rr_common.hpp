@@ -1,0 +1,199 @@
+// rr_common.hpp — shared device helpers and data layout of the MI355X rasterizer.
+//
+// Layout decisions (see DESIGN.md §Data layout in HBM):
+//   * Splat (48 B, AoS, 16-B aligned): everything the per-tile blend kernels need for one
+//     Gaussian, so a (tile, Gaussian) pair costs one 4-B id load plus three 16-B loads of one
+//     record, instead of the reference's id + xy + conic_opacity + per-use rgb/depth gathers
+//     (forward.cu:310-349).
+//       a = {x_pix, y_pix, conic.x, conic.y}
+//       b = {conic.z, opacity, depth(view z), 0}
+//       c = {r, g, b, 0}        (SH colour, or colors_precomp copied in)
+//   * Backward accumulators: 16 floats (one 64-B line) per Gaussian, components
+//     0..1 dL/dmean2D(ndc), 2..4 dL/dconic (x,y,w), 5 dL/dopacity, 6..8 dL/dcolor.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rr {
+
+constexpr int TILE_X = 16;
+constexpr int TILE_Y = 16;
+constexpr int TILE_PIX = TILE_X * TILE_Y;  // 256 threads = 4 wave64 per tile
+constexpr int GACC_STRIDE = 16;            // floats per Gaussian in the backward accumulator
+constexpr int NGRAD = 9;                   // accumulated components per (tile, Gaussian) pair
+
+struct alignas(16) Splat {
+    float4 a;
+    float4 b;
+    float4 c;
+};
+
+// auxiliary.h:11-28
+#define RR_SH_C0 0.28209479177387814f
+#define RR_SH_C1 0.4886025119029199f
+#define RR_SH_C2_0 1.0925484305920792f
+#define RR_SH_C2_1 -1.0925484305920792f
+#define RR_SH_C2_2 0.31539156525252005f
+#define RR_SH_C2_3 -1.0925484305920792f
+#define RR_SH_C2_4 0.5462742152960396f
+#define RR_SH_C3_0 -0.5900435899266435f
+#define RR_SH_C3_1 2.890611442640554f
+#define RR_SH_C3_2 -0.4570457994644658f
+#define RR_SH_C3_3 0.3731763325901154f
+#define RR_SH_C3_4 -0.4570457994644658f
+#define RR_SH_C3_5 1.445305721320277f
+#define RR_SH_C3_6 -0.5900435899266435f
+
+struct v3 {
+    float x, y, z;
+};
+__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 operator-(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 operator*(float s, v3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+__device__ __forceinline__ v3 load3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+// ndc2Pix (auxiliary.h:30-33): evaluated in double like the reference.
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+// getRect (auxiliary.h:35-45): C truncation toward zero, clamped to [0, grid].
+__device__ __forceinline__ void tile_rect(float px, float py, int r, int gx, int gy, int& x0, int& y0, int& x1,
+                                          int& y1) {
+    x0 = min(gx, max(0, (int)((px - r) / TILE_X)));
+    y0 = min(gy, max(0, (int)((py - r) / TILE_Y)));
+    x1 = min(gx, max(0, (int)((px + r + TILE_X - 1) / TILE_X)));
+    y1 = min(gy, max(0, (int)((py + r + TILE_Y - 1) / TILE_Y)));
+}
+
+// Column-major 4x4 transforms (auxiliary.h:47-86).  Matrices live in device memory and are
+// indexed with wave-uniform offsets, so the compiler keeps them in SGPRs (s_load).
+__device__ __forceinline__ v3 xform_point_4x3(v3 p, const float* m) {
+    return mk(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+              m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+__device__ __forceinline__ float4 xform_point_4x4(v3 p, const float* m) {
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+__device__ __forceinline__ v3 xform_vec_4x3_T(v3 p, const float* m) {
+    return mk(m[0] * p.x + m[1] * p.y + m[2] * p.z, m[4] * p.x + m[5] * p.y + m[6] * p.z,
+              m[8] * p.x + m[9] * p.y + m[10] * p.z);
+}
+
+// Quaternion (r,x,y,z) -> row-major rotation (forward.cu:116-127 builds its transpose in glm).
+__device__ __forceinline__ void quat_rot(float4 q, float R[3][3]) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
+    R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
+    R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+}
+
+// Sigma = M^T M with M[i][j] = s_i R[j][i]  (forward.cu:129-140).  Used by the forward
+// preprocess AND recomputed by the backward (no cov3D round trip through HBM).
+__device__ __forceinline__ void cov3d_from_scale_rot(v3 scale, float mod, float4 q, float cov[6]) {
+    float R[3][3];
+    quat_rot(q, R);
+    const float s[3] = {mod * scale.x, mod * scale.y, mod * scale.z};
+    float M[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) M[i][j] = s[i] * R[j][i];
+    cov[0] = M[0][0] * M[0][0] + M[1][0] * M[1][0] + M[2][0] * M[2][0];
+    cov[1] = M[0][0] * M[0][1] + M[1][0] * M[1][1] + M[2][0] * M[2][1];
+    cov[2] = M[0][0] * M[0][2] + M[1][0] * M[1][2] + M[2][0] * M[2][2];
+    cov[3] = M[0][1] * M[0][1] + M[1][1] * M[1][1] + M[2][1] * M[2][1];
+    cov[4] = M[0][1] * M[0][2] + M[1][1] * M[1][2] + M[2][1] * M[2][2];
+    cov[5] = M[0][2] * M[0][2] + M[1][2] * M[1][2] + M[2][2] * M[2][2];
+}
+
+// EWA projection pieces shared by forward preprocess (forward.cu:63-102) and the backward
+// (backward.cu:154-189): clamped view-space mean t, A = J·W (glm's T[i][j] == A[i][j]).
+struct Proj2D {
+    v3 t;
+    float txtz, tytz, limx, limy;
+    float A[2][3];
+};
+__device__ __forceinline__ Proj2D ewa_setup(v3 mean, float fx, float fy, float tanfovx, float tanfovy,
+                                            const float* view) {
+    Proj2D p;
+    v3 t = xform_point_4x3(mean, view);
+    p.limx = 1.3f * tanfovx;
+    p.limy = 1.3f * tanfovy;
+    p.txtz = t.x / t.z;
+    p.tytz = t.y / t.z;
+    t.x = fminf(p.limx, fmaxf(-p.limx, p.txtz)) * t.z;
+    t.y = fminf(p.limy, fmaxf(-p.limy, p.tytz)) * t.z;
+    p.t = t;
+    const float J00 = fx / t.z, J02 = -(fx * t.x) / (t.z * t.z);
+    const float J11 = fy / t.z, J12 = -(fy * t.y) / (t.z * t.z);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        p.A[0][j] = J00 * view[4 * j + 0] + J02 * view[4 * j + 2];
+        p.A[1][j] = J11 * view[4 * j + 1] + J12 * view[4 * j + 2];
+    }
+    return p;
+}
+// (a, b, c) of A V A^T before dilation.
+__device__ __forceinline__ void ewa_cov2d(const Proj2D& p, const float cov[6], float& a, float& b, float& c) {
+    const float V[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
+    float B[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) B[i][j] = p.A[i][0] * V[0][j] + p.A[i][1] * V[1][j] + p.A[i][2] * V[2][j];
+    a = B[0][0] * p.A[0][0] + B[0][1] * p.A[0][1] + B[0][2] * p.A[0][2];
+    b = B[0][0] * p.A[1][0] + B[0][1] * p.A[1][1] + B[0][2] * p.A[1][2];
+    c = B[1][0] * p.A[1][0] + B[1][1] * p.A[1][1] + B[1][2] * p.A[1][2];
+}
+
+// SH -> RGB (forward.cu:9-60), degree known at compile time.  Returns the pre-clamp value.
+template <int DEG>
+__device__ __forceinline__ v3 sh_eval(v3 dir, const float* sh) {
+    v3 r = RR_SH_C0 * load3(sh);
+    if (DEG > 0) {
+        const float x = dir.x, y = dir.y, z = dir.z;
+        r = r - (RR_SH_C1 * y) * load3(sh + 3) + (RR_SH_C1 * z) * load3(sh + 6) - (RR_SH_C1 * x) * load3(sh + 9);
+        if (DEG > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            r = r + (RR_SH_C2_0 * xy) * load3(sh + 12);
+            r = r + (RR_SH_C2_1 * yz) * load3(sh + 15);
+            r = r + (RR_SH_C2_2 * (2.0f * zz - xx - yy)) * load3(sh + 18);
+            r = r + (RR_SH_C2_3 * xz) * load3(sh + 21);
+            r = r + (RR_SH_C2_4 * (xx - yy)) * load3(sh + 24);
+            if (DEG > 2) {
+                r = r + (RR_SH_C3_0 * y * (3.0f * xx - yy)) * load3(sh + 27);
+                r = r + (RR_SH_C3_1 * xy * z) * load3(sh + 30);
+                r = r + (RR_SH_C3_2 * y * (4.0f * zz - xx - yy)) * load3(sh + 33);
+                r = r + (RR_SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * load3(sh + 36);
+                r = r + (RR_SH_C3_4 * x * (4.0f * zz - xx - yy)) * load3(sh + 39);
+                r = r + (RR_SH_C3_5 * z * (xx - yy)) * load3(sh + 42);
+                r = r + (RR_SH_C3_6 * x * (xx - 3.0f * yy)) * load3(sh + 45);
+            }
+        }
+    }
+    return mk(r.x + 0.5f, r.y + 0.5f, r.z + 0.5f);
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave64 sum with DPP row shifts + row broadcasts; the total lands in lane 63.
+// 6 DPP-fused adds (row_shr 1/2/4/8, row_bcast15, row_bcast31) — no LDS traffic.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK,
+                                                                     0xf, true));
+}
+__device__ __forceinline__ float wave_sum_lane63(float v) {
+    v = dpp_add<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_add<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1,3
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2,3
+    return v;
+}
+
+}  // namespace rr

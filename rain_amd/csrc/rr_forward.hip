@@ -1,0 +1,280 @@
+// rr_forward.hip — forward kernels of the MI355X rasterizer.
+//
+//   k_preprocess<DEG>  one thread per Gaussian (forward.cu:144-246 semantics)
+//   k_gather_tiles     tile counts in depth order (input of the prefix sum)
+//   k_duplicate<K>     (tile, Gaussian) pairs in depth order, key = tile id only
+//   k_ranges<K>        per-tile [start, end) in the tile-sorted list (rasterizer_impl.cu:105-127)
+//   k_blend_fwd        per-tile front-to-back alpha blend (forward.cu:251-369)
+//   k_mark_visible     frustum test (rasterizer_impl.cu:43-55)
+//
+// Binning order: the reference sorts 64-bit (tile << 32 | depth_bits) keys emitted in Gaussian
+// index order with a stable radix sort.  Here visible Gaussians are first stable-sorted by
+// depth bits (P keys, 32 bits), their pairs are emitted in that order, and the pairs are then
+// stable-sorted by tile id only (msb(T) <= 15 bits, 16-bit keys).  Within a tile this yields the
+// same (depth, index) order as the reference, at a fraction of the sort traffic.
+#include "rr_common.hpp"
+#include "rr_kernels.hpp"
+
+namespace rr {
+
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    a.radii[idx] = 0;
+    a.tiles[idx] = 0;
+    a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
+
+    const v3 p = load3(a.means3D + 3 * (size_t)idx);
+    // in_frustum (auxiliary.h:128-153)
+    const v3 p_view = xform_point_4x3(p, a.view);
+    if (p_view.z <= 0.2f) {
+        if (a.prefiltered) __builtin_trap();
+        return;
+    }
+    const float4 p_hom = xform_point_4x4(p, a.proj);
+    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+    const float ppx = p_hom.x * p_w, ppy = p_hom.y * p_w;
+
+    float cov[6];
+    if (a.cov3D_precomp) {
+        const float* c = a.cov3D_precomp + 6 * (size_t)idx;
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov[i] = c[i];
+    } else {
+        const float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        cov3d_from_scale_rot(load3(a.scales + 3 * (size_t)idx), a.scale_modifier, q, cov);
+    }
+    const Proj2D pr = ewa_setup(p, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view);
+    float ca, cb, cc;
+    ewa_cov2d(pr, cov, ca, cb, cc);
+    ca += a.low_pass;
+    cc += a.low_pass;
+
+    const float det = ca * cc - cb * cb;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float cx = cc * det_inv, cy = -cb * det_inv, cz = ca * det_inv;
+    const float mid = 0.5f * (ca + cc);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+    const int radius = (int)my_radius;
+    const float px = ndc2pix(ppx, a.W), py = ndc2pix(ppy, a.H);
+    int x0, y0, x1, y1;
+    tile_rect(px, py, radius, a.gx, a.gy, x0, y0, x1, y1);
+    const int area = (x1 - x0) * (y1 - y0);
+    if (area == 0) return;
+
+    float4 rgb;
+    if (a.colors_precomp) {
+        const v3 c = load3(a.colors_precomp + 3 * (size_t)idx);
+        rgb = make_float4(c.x, c.y, c.z, 0.f);
+    } else {
+        const v3 cp = load3(a.campos);
+        v3 dir = p - cp;
+        const float len = sqrtf(dot(dir, dir));
+        dir = mk(dir.x / len, dir.y / len, dir.z / len);
+        const v3 c = sh_eval<DEG>(dir, a.shs + (size_t)idx * a.M * 3);
+        rgb = make_float4(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f), 0.f);
+    }
+    const float opacity = a.opacities[idx];
+    Splat s;
+    s.a = make_float4(px, py, cx, cy);
+    s.b = make_float4(cz, opacity, p_view.z, 0.f);
+    s.c = rgb;
+    a.splats[idx] = s;
+    a.radii[idx] = radius;
+    a.tiles[idx] = (uint32_t)area;
+    a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
+    atomicAdd(a.num_visible, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __restrict__ idx_sorted,
+                                                      const uint32_t* __restrict__ tiles,
+                                                      uint32_t* __restrict__ tiles_sorted) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P) return;
+    tiles_sorted[s] = tiles[idx_sorted[s]];
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __restrict__ idx_sorted,
+                                                   const uint32_t* __restrict__ offsets,
+                                                   const Splat* __restrict__ splats, const int* __restrict__ radii,
+                                                   int gx, int gy, K* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P) return;
+    const uint32_t g = idx_sorted[s];
+    const int r = radii[g];
+    if (r <= 0) return;
+    uint32_t off = s == 0 ? 0u : offsets[s - 1];
+    const float4 A = splats[g].a;
+    int x0, y0, x1, y1;
+    tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
+    for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) {
+            keys[off] = (K)(y * gx + x);
+            vals[off] = g;
+            off++;
+        }
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_ranges(int L, const K* __restrict__ keys, uint2* __restrict__ ranges) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L) return;
+    const uint32_t cur = keys[i];
+    if (i == 0) {
+        ranges[cur].x = 0;
+    } else {
+        const uint32_t prev = keys[i - 1];
+        if (cur != prev) {
+            ranges[prev].y = i;
+            ranges[cur].x = i;
+        }
+    }
+    if (i == L - 1) ranges[cur].y = L;
+}
+
+// One workgroup (4 wave64) per 16x16 tile, one thread per pixel.  Each round stages 256 splat
+// records in LDS (one coalesced id load + one 48-B record gather per thread); the inner loop
+// reads them as LDS broadcasts.  A round starts only if some pixel of the tile is still open
+// (__syncthreads_count, forward.cu:302-304); a wave whose 64 pixels are all saturated leaves the
+// inner loop on its own (divergent loop exit), so early termination is per wave, not per tile.
+__global__ __launch_bounds__(256) void k_blend_fwd(BlendFwdArgs a) {
+    const int tile = blockIdx.x;
+    const int tx = tile % a.gx, ty = tile / a.gx;
+    const int t = threadIdx.x;
+    const int px = tx * TILE_X + (t & 15), py = ty * TILE_Y + (t >> 4);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+    bool done = !inside;
+
+    __shared__ float4 s_a[TILE_PIX];
+    __shared__ float4 s_b[TILE_PIX];
+    __shared__ float4 s_c[TILE_PIX];
+    __shared__ uint32_t s_max[4];
+
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+    float T = 1.0f;
+    uint32_t contributor = 0, last_contributor = 0;
+    float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
+
+    for (int base = 0; base < n; base += TILE_PIX) {
+        if (__syncthreads_count(done) == TILE_PIX) break;
+        const int k = base + t;
+        if (k < n) {
+            const uint32_t g = a.point_list[range.x + k];
+            const Splat s = a.splats[g];
+            s_a[t] = s.a;
+            s_b[t] = s.b;
+            s_c[t] = s.c;
+        }
+        __syncthreads();
+        const int cnt = min(TILE_PIX, n - base);
+        for (int j = 0; !done && j < cnt; j++) {
+            contributor++;
+            const float4 A = s_a[j];
+            const float4 B = s_b[j];
+            const float dx = A.x - pfx, dy = A.y - pfy;
+            const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
+            if (power > 0.0f) continue;
+            const float alpha = fminf(0.99f, B.y * __expf(power));
+            if (alpha < 1.0f / 255.0f) continue;
+            const float test_T = T * (1 - alpha);
+            if (test_T < 0.0001f) {
+                done = true;
+                continue;
+            }
+            const float4 Cc = s_c[j];
+            C0 += Cc.x * alpha * T;
+            C1 += Cc.y * alpha * T;
+            C2 += Cc.z * alpha * T;
+            Dp += B.z * alpha * T;
+            T = test_T;
+            last_contributor = contributor;
+        }
+    }
+
+    // per-tile max contributor count: lets the backward skip pairs no pixel blended
+    uint32_t m = inside ? last_contributor : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if ((t & 63) == 0) s_max[t >> 6] = m;
+    __syncthreads();
+    if (t == 0) a.tile_max[tile] = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+
+    if (inside) {
+        const int pix = a.W * py + px;
+        const size_t HW = (size_t)a.H * a.W;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last_contributor;
+        a.out_color[pix] = C0 + T * a.bg[0];
+        a.out_color[HW + pix] = C1 + T * a.bg[1];
+        a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
+        a.out_depth[pix] = Dp;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
+                                                      const float* __restrict__ view, uint8_t* __restrict__ present) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const v3 pv = xform_point_4x3(load3(means3D + 3 * (size_t)i), view);
+    present[i] = pv.z <= 0.2f ? 0 : 1;
+}
+
+// ---------------------------------------------------------------------------------------
+// host launchers
+static inline int blocks_for(long n, int b = 256) { return (int)((n + b - 1) / b); }
+
+void launch_preprocess(const PreArgs& a, hipStream_t st) {
+    if (a.P == 0) return;
+    const int nb = blocks_for(a.P);
+    switch (a.colors_precomp ? 0 : a.D) {
+        case 0: k_preprocess<0><<<nb, 256, 0, st>>>(a); break;
+        case 1: k_preprocess<1><<<nb, 256, 0, st>>>(a); break;
+        case 2: k_preprocess<2><<<nb, 256, 0, st>>>(a); break;
+        default: k_preprocess<3><<<nb, 256, 0, st>>>(a); break;
+    }
+}
+
+void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint32_t* tiles, uint32_t* out, hipStream_t st) {
+    if (P == 0) return;
+    k_gather_tiles<<<blocks_for(P), 256, 0, st>>>(P, idx_sorted, tiles, out);
+}
+
+template <typename K>
+void launch_duplicate(int P, const uint32_t* idx_sorted, const uint32_t* offsets, const Splat* splats,
+                      const int* radii, int gx, int gy, K* keys, uint32_t* vals, hipStream_t st) {
+    if (P == 0) return;
+    k_duplicate<K><<<blocks_for(P), 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, keys, vals);
+}
+template void launch_duplicate<uint16_t>(int, const uint32_t*, const uint32_t*, const Splat*, const int*, int, int,
+                                         uint16_t*, uint32_t*, hipStream_t);
+template void launch_duplicate<uint32_t>(int, const uint32_t*, const uint32_t*, const Splat*, const int*, int, int,
+                                         uint32_t*, uint32_t*, hipStream_t);
+
+template <typename K>
+void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st) {
+    if (L == 0) return;
+    k_ranges<K><<<blocks_for(L), 256, 0, st>>>(L, keys, ranges);
+}
+template void launch_ranges<uint16_t>(int, const uint16_t*, uint2*, hipStream_t);
+template void launch_ranges<uint32_t>(int, const uint32_t*, uint2*, hipStream_t);
+
+void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
+    const int T = a.gx * a.gy;
+    if (T == 0) return;
+    k_blend_fwd<<<T, TILE_PIX, 0, st>>>(a);
+}
+
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
+    if (P == 0) return;
+    k_mark_visible<<<blocks_for(P), 256, 0, st>>>(P, means3D, view, present);
+}
+
+}  // namespace rr

@@ -1,0 +1,89 @@
+// rr_kernels.hpp — kernel argument blocks and host launchers shared by the .hip units.
+#pragma once
+#include "rr_common.hpp"
+
+namespace rr {
+
+struct PreArgs {
+    int P, D, M, W, H, gx, gy, prefiltered;
+    float tanfovx, tanfovy, focal_x, focal_y, scale_modifier, low_pass;
+    const float* means3D;
+    const float* shs;
+    const float* colors_precomp;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    int* radii;
+    Splat* splats;
+    uint32_t* tiles;
+    uint32_t* depth_keys;
+    uint32_t* num_visible;
+};
+
+struct BlendFwdArgs {
+    int W, H, gx, gy;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const Splat* splats;
+    const float* bg;
+    float* final_T;
+    uint32_t* n_contrib;
+    uint32_t* tile_max;
+    float* out_color;
+    float* out_depth;
+};
+
+struct BlendBwdArgs {
+    int W, H, gx, gy;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const Splat* splats;
+    const uint32_t* tile_max;
+    const float* final_T;
+    const uint32_t* n_contrib;
+    const float* bg;
+    const float* dL_dpix;
+    float* gacc;  // [P][GACC_STRIDE]
+};
+
+struct GaussBwdArgs {
+    int P, D, M;
+    float tanfovx, tanfovy, focal_x, focal_y, scale_modifier, low_pass;
+    const float* means3D;
+    const float* shs;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    const int* radii;
+    const float* gacc;
+    float* dL_dmeans2D;
+    float* dL_dcolors;
+    float* dL_dopacity;
+    float* dL_dmeans3D;
+    float* dL_dcov3D;
+    float* dL_dsh;
+    float* dL_dscales;
+    float* dL_drot;
+};
+
+void launch_preprocess(const PreArgs& a, hipStream_t st);
+void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint32_t* tiles, uint32_t* out, hipStream_t st);
+template <typename K>
+void launch_duplicate(int P, const uint32_t* idx_sorted, const uint32_t* offsets, const Splat* splats,
+                      const int* radii, int gx, int gy, K* keys, uint32_t* vals, hipStream_t st);
+template <typename K>
+void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st);
+void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
+
+void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);
+void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
+
+}  // namespace rr
