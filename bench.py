@@ -1,0 +1,291 @@
+#!/usr/bin/env python3
+"""Headline benchmark: train iters/sec + forward Mpix/sec, 1M Gaussians @ 1920x1080, SH degree 3
+(BASELINE.json metric; configs[2] at N=1, configs[3] view-sharded at N>1).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py ...)
+
+A "step" is one iteration of the reference's train.py loop (train.py:71-147) on every rank:
+lr update, render forward, L1+SSIM loss, backward through the MI355X rasterizer, (all-reduce),
+densification statistics, densify/prune every 100 iterations, Adam.  The timed window ends on an
+iteration that is a multiple of 100, so it contains floor(K/100) densify/prune events (the
+reference's 1-in-100 share).  value = iterations all ranks completed / wall time (max over ranks).
+
+Data: synthetic and seeded (no datasets offline) — 1M random Gaussians (SURVEY §8(d) bench
+variant), 200 Fibonacci-sphere cameras, ground-truth images rendered from a second random model.
+
+Extra objects on the JSON line:
+  roofline      dominant kernel of the timed region (HIP events on the launch stream), algorithmic
+                bytes per launch from SURVEY §8(d) x the frame's measured L / V / L_eff / T / N
+  cpu_baseline  the CPU oracle (oracle/raster_oracle.c, "port") on the same frame, rank 0, N=1
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+VALU_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--points", type=int, default=1_000_000)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--views", type=int, default=200)
+    p.add_argument("--sh-degree", type=int, default=3)
+    p.add_argument("--fwd-frames", type=int, default=50)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--no-profile", action="store_true", help="skip HIP-event stage timing in the timed region")
+    return p.parse_args()
+
+
+def algorithmic_bytes(stage, st, P, W, H, K):
+    """SURVEY §8(d) per-launch algorithmic bytes."""
+    L, V, Le, T, N = st["num_rendered"], st["num_visible"], st["l_eff"], st["tiles"], W * H
+    M = K
+    kb = 32 + math.ceil(math.log2(max(T, 2)))
+    return {
+        "preprocess": 20 * P + V * (99 + 12 * K),
+        "scan": 8 * P,
+        "duplicate": 4 * P + 16 * V + 12 * L,
+        "tile_sort": 24 * L * math.ceil(kb / 8),
+        "ranges": 8 * L + 16 * T,
+        "blend_fwd": 8 * T + 44 * Le + 24 * N,
+        "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
+        "gauss_bwd": 4 * P * (27 + 3 * M) + 4 * P + 88 * V + 4 * P + V * (143 + 24 * K),
+    }.get(stage)
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.manual_seed(0)
+    np.random.seed(0)
+
+    from rain_amd import _native, synthetic
+    from rain_amd.cameras import fibonacci_cameras
+    from rain_amd.diff_gaussian_rasterization import _C
+    from rain_amd.gaussian_model import GaussianModel, OptimizationParams
+    from rain_amd.renderer import PipelineParams, render
+    from rain_amd.train import TrainConfig, Trainer
+
+    P, W, H, D = args.points, args.width, args.height, args.sh_degree
+    cams = [c.to(dev) for c in fibonacci_cameras(args.views, W, H)]
+    extent = 4.0 * 1.1  # getNerfppNorm of the camera rig (dataset_readers.py:34-55): radius 4, x1.1
+
+    # ground truth: a second random model rendered from every view
+    gt_model = GaussianModel(D, device=dev)
+    gt_model.set_params(synthetic.random_gaussians(P, sh_degree=D, seed=1, bench=True, device=dev))
+    gt_model.active_sh_degree = D
+    pipe = PipelineParams()
+    bg = torch.zeros(3, device=dev)
+    with torch.no_grad():
+        gts = [render(c, gt_model, pipe, bg)["render"].clamp(0.0, 1.0).contiguous() for c in cams]
+    del gt_model
+
+    gauss = GaussianModel(D, divide_ratio=0.8, device=dev)
+    gauss.set_params(synthetic.random_gaussians(P, sh_degree=D, seed=0, bench=True, device=dev))
+    gauss.active_sh_degree = D
+    gauss.spatial_lr_scale = extent
+    opt = OptimizationParams()
+    gauss.training_setup(opt)
+    trainer = Trainer(gauss, cams, gts, opt, pipe, TrainConfig(seed=0), scene_extent=extent)
+
+    K, Wm = args.steps, args.warmup
+    end_iter = max(1000, int(math.ceil((Wm + K + 1) / 100.0)) * 100)
+    start_iter = end_iter - K - Wm + 1
+    it = start_iter
+    for _ in range(Wm):
+        trainer.step(it)
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    prof = not args.no_profile
+    if prof:
+        _native.raster().rr_profile_enable(1)
+        _native.Profiler.collect()  # drop anything recorded before the window
+    t0 = time.perf_counter()
+    views_used = []
+    for _ in range(K):
+        info = trainer.step(it)
+        views_used.append(info.view)
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    stage_ms = {}
+    if prof:
+        _native.raster().rr_profile_enable(0)
+        stage_ms = _native.Profiler.collect()
+    elapsed = t1 - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    iters_per_s = world * K / elapsed
+    ms_per_step = 1000.0 * elapsed / K
+
+    # forward-only throughput (preprocess -> blend incl. sorts and the L read-back), no autograd
+    Pn = gauss.get_xyz.shape[0]
+    with torch.no_grad():
+        for i in range(3):
+            render(cams[i], gauss, pipe, bg)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tf0 = time.perf_counter()
+        for i in range(args.fwd_frames):
+            render(cams[(rank * 7 + i) % len(cams)], gauss, pipe, bg)
+        torch.cuda.synchronize()
+        tf = time.perf_counter() - tf0
+    if world > 1:
+        e = torch.tensor([tf], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        tf = float(e.item())
+    fwd_mpix = world * args.fwd_frames * W * H / tf / 1e6
+
+    # frame statistics for the algorithmic-byte model (re-render the timed views, no grad)
+    stats = []
+    with torch.no_grad():
+        for v in sorted(set(views_used))[:16]:
+            s = _settings(cams[v], gauss, bg)
+            act = (gauss.get_xyz, gauss.get_opacity, gauss.get_scaling, gauss.get_rotation, gauss.get_features)
+            e = torch.Tensor([])
+            out = _C.rasterize_gaussians(s.bg, act[0], e, act[1], act[2], act[3], 1.0, e, s.viewmatrix,
+                                         s.projmatrix, s.tanfovx, s.tanfovy, H, W, act[4], D, s.campos, False, False,
+                                         0.3)
+            stats.append(_C.frame_stats(out[4], out[6], Pn, W, H))
+    mean_stats = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
+
+    roofline = None
+    kernels = {}
+    if stage_ms:
+        for name, (ms, cnt) in stage_ms.items():
+            if cnt:
+                kernels[name] = {"ms_per_launch": ms / cnt, "launches": int(cnt), "total_ms": ms}
+        dom = max((k for k in kernels if algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2) is not None),
+                  key=lambda k: kernels[k]["total_ms"])
+        byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2)
+        gbs = byts / (kernels[dom]["ms_per_launch"] * 1e-3) / 1e9
+        roofline = {"kernel": dom, "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(dom),
+                    "algorithmic_bytes_per_launch": int(byts)}
+        for k in kernels:
+            b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2)
+            if b is not None:
+                kernels[k]["algorithmic_GBps"] = round(b / (kernels[k]["ms_per_launch"] * 1e-3) / 1e9, 1)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = _cpu_baseline(gauss, cams[views_used[0]], bg, D, args.cpu_threads)
+
+    line = {
+        "metric": "train iters/sec + forward Mpix/sec, 1M Gaussians @ 1080p, 1/2/4/8 MI355X",
+        "value": round(iters_per_s, 3),
+        "unit": "train iters/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": Wm,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded random Gaussians, 200 Fibonacci-sphere cameras, GT = render of a second random model)",
+        "config": {"workload": f"train.py iteration (render fwd + L1/SSIM + bwd + densify stats + "
+                               f"densify/prune every 100 it + Adam), {P} Gaussians, {W}x{H}, SH {D}, "
+                               f"view-sharded dp{world}",
+                   "gaussians": P, "width": W, "height": H, "sh_degree": D, "views": args.views,
+                   "parallelism": f"dp{world} (view-sharded, RCCL all-reduce)" if world > 1 else "dp1",
+                   "iterations": [start_iter + Wm, end_iter]},
+        "forward_mpix_per_s": round(fwd_mpix, 2),
+        "gaussians_after": int(Pn),
+        "frame_stats": {k: int(v) for k, v in mean_stats.items()},
+        "roofline": roofline,
+        "kernels": kernels,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _settings(cam, gauss, bg):
+    from rain_amd.synthetic import settings_for
+
+    return settings_for(cam, gauss.active_sh_degree, bg=bg)
+
+
+def _pmc_traffic(kernel):
+    """HBM bytes per launch from a committed rocprofv3 PMC pass (tools/pmc_traffic.py), else null."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        v = d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        return int(v) if v is not None else None
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_baseline(gauss, cam, bg, D, threads):
+    """The oracle (test infrastructure, `port` of the reference algorithm) on the same frame."""
+    import numpy as np
+    import torch
+
+    from oracle import oracle as O
+
+    O.build()
+    nthr = threads or min(16, os.cpu_count() or 1)
+    with torch.no_grad():
+        s = _settings(cam, gauss, bg)
+        m = gauss.get_xyz.detach().float().cpu().numpy()
+        op = gauss.get_opacity.detach().float().cpu().numpy()
+        sc = gauss.get_scaling.detach().float().cpu().numpy()
+        ro = gauss.get_rotation.detach().float().cpu().numpy()
+        sh = gauss.get_features.detach().float().cpu().numpy()
+    st = O.Settings(image_height=s.image_height, image_width=s.image_width, tanfovx=s.tanfovx, tanfovy=s.tanfovy,
+                    bg=s.bg.cpu().numpy(), scale_modifier=1.0, viewmatrix=s.viewmatrix.cpu().numpy(),
+                    projmatrix=s.projmatrix.cpu().numpy(), sh_degree=D, campos=s.campos.cpu().numpy(),
+                    low_pass=0.3)
+    dpix = np.random.default_rng(0).standard_normal((3, s.image_height, s.image_width)).astype(np.float32)
+    t0 = time.perf_counter()
+    nr, color, radii, depth, state = O.forward(st, m, op, shs=sh, scales=sc, rotations=ro, nthreads=nthr)
+    t1 = time.perf_counter()
+    O.backward(state, st, m, radii, dpix, shs=sh, scales=sc, rotations=ro, nthreads=nthr)
+    t2 = time.perf_counter()
+    return {"value": round(1.0 / (t2 - t0), 4), "unit": "render fwd+bwd iters/s", "cores": int(O.lib().orc_threads()),
+            "kind": "port",
+            "sample": f"1 full {s.image_width}x{s.image_height} view, {m.shape[0]} Gaussians, SH {D}: forward "
+                      f"{t1 - t0:.2f}s + backward {t2 - t1:.2f}s (rasterizer only; loss/Adam not included)",
+            "forward_mpix_per_s": round(s.image_width * s.image_height / (t1 - t0) / 1e6, 4)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,162 @@
+"""Training step around the rasterizer.
+
+One call of ``Trainer.step`` is one iteration of train.py:71-147 — learning-rate update, SH-degree
+ramp, RAIN-GS low-pass schedule, render, L1+SSIM loss, backward, densification statistics,
+periodic densify/prune and opacity reset, Adam — executed on every rank of a view-sharded
+data-parallel group:
+
+* every rank holds the full Gaussian set and Adam state (replicas);
+* at step s rank r renders view ``perm[s*N + r]`` of a permutation shared by all ranks (the
+  reference's pop-random-without-replacement, train.py:87-89, done globally);
+* after backward ONE all-reduce (SUM) covers every parameter gradient (they are views into one
+  flat buffer) plus the per-view densification increments; gradients are then averaged, the
+  increments summed (N views add their norms exactly like N sequential iterations would); a second,
+  small all-reduce (MAX) merges max_radii2D;
+* Adam / densify then run identically on every rank (same RNG seed), so replicas stay equal.
+
+With world_size 1 there is no collective and the step is the reference's iteration.
+"""
+from __future__ import annotations
+
+import math
+import random
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from .gaussian_model import GaussianModel, OptimizationParams, low_pass_schedule
+from .loss import l1_loss, ssim_separable
+from .renderer import PipelineParams, render
+
+
+@dataclass
+class TrainConfig:
+    c2f: bool = True                 # RAIN-GS coarse-to-fine low-pass (train.py:95-107)
+    c2f_every_step: int = 1000
+    c2f_max_lowpass: float = 300.0
+    warmup_iter: int = 0             # abe_split warm-up (train.py:38-39,138)
+    ours: bool = False               # SH ramp from 5000 (train.py:79-85)
+    white_background: bool = False
+    seed: int = 0
+    densify: bool = True
+
+
+class ViewSampler:
+    """Shared permutation of camera indices; rank r takes the r-th of each group of N."""
+
+    def __init__(self, n_views: int, world: int, seed: int = 0):
+        self.n, self.world = n_views, world
+        self.rng = random.Random(seed)
+        self.perm: list[int] = []
+
+    def next_group(self):
+        out = []
+        for _ in range(self.world):
+            if not self.perm:
+                self.perm = list(range(self.n))
+                self.rng.shuffle(self.perm)
+            out.append(self.perm.pop())
+        return out
+
+
+@dataclass
+class StepInfo:
+    loss: float | None
+    num_gaussians: int
+    view: int
+    low_pass: float
+    densified: bool = False
+
+
+class Trainer:
+    def __init__(self, gaussians: GaussianModel, cameras, gt_images, opt: OptimizationParams | None = None,
+                 pipe: PipelineParams | None = None, cfg: TrainConfig | None = None, scene_extent: float = 1.0,
+                 group=None):
+        self.g = gaussians
+        self.cams = cameras
+        self.gt = gt_images
+        self.opt = opt or OptimizationParams()
+        self.pipe = pipe or PipelineParams()
+        self.cfg = cfg or TrainConfig()
+        self.extent = scene_extent
+        self.group = group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.sampler = ViewSampler(len(cameras), self.world, self.cfg.seed)
+        dev = gaussians.device
+        self.background = torch.tensor([1, 1, 1] if self.cfg.white_background else [0, 0, 0], dtype=torch.float32,
+                                       device=dev)
+        self.low_pass = 0.3
+        self.densify_gen = torch.Generator(device=dev).manual_seed(self.cfg.seed + 12345)
+        if self.cfg.warmup_iter > 0:
+            self.opt.densify_until_iter += self.cfg.warmup_iter
+
+    def step(self, iteration: int, sync_loss: bool = False) -> StepInfo:
+        g, opt, cfg = self.g, self.opt, self.cfg
+        g.update_learning_rate(iteration)
+        if cfg.ours:
+            if iteration >= 5000 and iteration % 1000 == 0:
+                g.oneupSHdegree()
+        elif iteration % 1000 == 0:
+            g.oneupSHdegree()
+
+        views = self.sampler.next_group()
+        vidx = views[self.rank]
+        cam = self.cams[vidx]
+        if cfg.c2f:
+            if iteration == 1 or (iteration % cfg.c2f_every_step == 0 and iteration < opt.densify_until_iter):
+                self.low_pass = low_pass_schedule(cam.image_height, cam.image_width, g.get_xyz.shape[0],
+                                                  cfg.c2f_max_lowpass)
+        else:
+            self.low_pass = 0.3
+
+        P = g.get_xyz.shape[0]
+        densify_phase = iteration < opt.densify_until_iter
+        flat = g.bind_flat_grad(extra=2 * P if (self.world > 1 and densify_phase) else 0)
+
+        pkg = render(cam, g, self.pipe, self.background, low_pass=self.low_pass)
+        image, vsp, vis, radii = pkg["render"], pkg["viewspace_points"], pkg["visibility_filter"], pkg["radii"]
+        gt = self.gt[vidx]
+        Ll1 = l1_loss(image, gt)
+        loss = (1.0 - opt.lambda_dssim) * Ll1 + opt.lambda_dssim * (1.0 - ssim_separable(image, gt))
+        loss.backward()
+
+        densified = False
+        with torch.no_grad():
+            nparam = flat.numel() - (2 * P if (self.world > 1 and densify_phase) else 0)
+            if self.world > 1:
+                if densify_phase:
+                    acc = flat[nparam:nparam + P]
+                    den = flat[nparam + P:]
+                    acc[vis] = torch.norm(vsp.grad[vis, :2], dim=-1)
+                    den[vis] = 1.0
+                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+                flat[:nparam].mul_(1.0 / self.world)
+            if densify_phase:
+                if self.world > 1:
+                    local = g.max_radii2D.clone()
+                    local[vis] = torch.max(local[vis], radii[vis].float())
+                    dist.all_reduce(local, op=dist.ReduceOp.MAX, group=self.group)
+                    g.max_radii2D = local
+                    g.xyz_gradient_accum += flat[nparam:nparam + P].unsqueeze(1)
+                    g.denom += flat[nparam + P:].unsqueeze(1)
+                else:
+                    g.max_radii2D[vis] = torch.max(g.max_radii2D[vis], radii[vis].float())
+                    g.add_densification_stats(vsp, vis)
+                if cfg.densify and iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0:
+                    size_threshold = 20 if iteration > opt.opacity_reset_interval else None
+                    abe_split = iteration <= cfg.warmup_iter
+                    g.densify_and_prune(opt.densify_grad_threshold, 0.005, self.extent, size_threshold, N=2,
+                                        abe_split=abe_split, generator=self.densify_gen)
+                    densified = True
+                if iteration % opt.opacity_reset_interval == 0 or (cfg.white_background and
+                                                                   iteration == opt.densify_from_iter):
+                    g.reset_opacity()
+            if iteration < opt.iterations:
+                # after densify_and_prune the parameters are new tensors with grad None, so this step
+                # skips them, exactly as the reference's optimizer.step() does (train.py:145-147)
+                g.optimizer.step()
+                g.optimizer.zero_grad(set_to_none=True)
+        return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
+                        view=vidx, low_pass=self.low_pass, densified=densified)
