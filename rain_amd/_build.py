@@ -25,6 +25,7 @@ CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-W
 
 LIBS = {
     "librain_raster.so": ["rr_forward.hip", "rr_backward.hip", "rr_api.hip"],
+    "librain_loss.so": ["loss.hip"],
     "librain_knn.so": ["knn.hip"],
 }
 

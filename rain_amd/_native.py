@@ -110,6 +110,27 @@ def raster():
     return _raster
 
 
+LOSS_LIB = os.path.join(LIB_DIR, "librain_loss.so")
+LOSS_SYMBOLS = ["rl_workspace_bytes", "rl_l1_ssim_forward", "rl_l1_ssim_backward", "rl_last_error"]
+_loss = None
+
+
+def loss_lib():
+    global _loss
+    if _loss is None:
+        L = _load(LOSS_LIB)
+        vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.rl_workspace_bytes.restype = ctypes.c_size_t
+        L.rl_workspace_bytes.argtypes = [ci, ci, ci]
+        L.rl_l1_ssim_forward.restype = ci
+        L.rl_l1_ssim_forward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, ctypes.c_size_t, vp, vp, vp]
+        L.rl_l1_ssim_backward.restype = ci
+        L.rl_l1_ssim_backward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, vp, vp, vp]
+        L.rl_last_error.restype = ctypes.c_char_p
+        _loss = L
+    return _loss
+
+
 def knn():
     global _knn
     if _knn is None:

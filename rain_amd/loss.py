@@ -1,10 +1,11 @@
 """Training loss (utils/loss_utils.py:6-53): loss = (1-λ)·L1 + λ·(1-SSIM), 11x11 Gaussian window σ=1.5.
 
-``ssim`` follows the reference exactly (depthwise 11x11 conv2d).  ``ssim_separable`` computes the
-same quantity with the window factored into 1x11 and 11x1 passes (the window is an outer product
-of the 1-D Gaussian, loss_utils.py:15-19); it is what the train step uses (5 filtered maps, 2 cheap
-1-D passes each instead of one 121-tap pass).  Both are pinned to the reference's ssim values by
-tests/golden/loss.npz.
+``ssim`` follows the reference exactly (depthwise 11x11 conv2d) and is the test reference.
+``fused_l1_ssim_loss`` is what the train step uses: the whole loss and its gradient in two HIP
+kernels (rain_amd/csrc/loss.hip) — the window is an outer product of the 1-D Gaussian
+(loss_utils.py:15-19), so it is applied as two 11-tap passes over an LDS tile.  ``ssim_separable``
+is the same factorisation in torch (a CPU-testable statement of what the kernel computes).  All are
+pinned to the reference's ssim values by tests/golden/loss.npz.
 """
 from __future__ import annotations
 
@@ -55,6 +56,68 @@ def _ssim(img1, img2, window, window_size, channel, size_average=True):
     if size_average:
         return ssim_map.mean()
     return ssim_map.mean(1).mean(1).mean(1)
+
+
+_WINDOW = None
+
+
+def _window_host():
+    """The reference's 1-D window gaussian(11, 1.5) (fp32 exp values normalised in fp32)."""
+    global _WINDOW
+    if _WINDOW is None:
+        import ctypes
+
+        g = gaussian(11, 1.5)
+        _WINDOW = (ctypes.c_float * 11)(*[float(v) for v in g])
+    return _WINDOW
+
+
+class _FusedL1SSIM(torch.autograd.Function):
+    """(1-λ)·L1 + λ·(1-SSIM) in two HIP kernels (rain_amd/csrc/loss.hip, include/rain_loss.h)."""
+
+    @staticmethod
+    def forward(ctx, img, gt, lambda_dssim):
+        import ctypes
+
+        from . import _native as N
+
+        L = N.loss_lib()
+        img = img.contiguous()
+        gt = gt.contiguous()
+        C, H, W = img.shape[-3:]
+        ws = torch.empty((L.rl_workspace_bytes(C, H, W),), dtype=torch.uint8, device=img.device)
+        loss = torch.empty((), dtype=torch.float32, device=img.device)
+        parts = torch.empty((3,), dtype=torch.float32, device=img.device)
+        rc = L.rl_l1_ssim_forward(img.data_ptr(), gt.data_ptr(), C, H, W, float(lambda_dssim), _window_host(),
+                                  ws.data_ptr(), ws.numel(), loss.data_ptr(), parts.data_ptr(), N.stream_of(img))
+        if rc:
+            raise RuntimeError(L.rl_last_error().decode())
+        ctx.save_for_backward(img, gt, ws)
+        ctx.lam = float(lambda_dssim)
+        ctx.mark_non_differentiable(parts)
+        return loss, parts
+
+    @staticmethod
+    def backward(ctx, grad_loss, _grad_parts):
+        from . import _native as N
+
+        img, gt, ws = ctx.saved_tensors
+        L = N.loss_lib()
+        C, H, W = img.shape[-3:]
+        dimg = torch.empty_like(img)
+        g = grad_loss.reshape(1).contiguous().float()
+        rc = L.rl_l1_ssim_backward(img.data_ptr(), gt.data_ptr(), C, H, W, ctx.lam, _window_host(), ws.data_ptr(),
+                                   g.data_ptr(), dimg.data_ptr(), N.stream_of(img))
+        if rc:
+            raise RuntimeError(L.rl_last_error().decode())
+        return dimg, None, None
+
+
+def fused_l1_ssim_loss(img, gt, lambda_dssim=0.2):
+    """Returns (loss, parts) where parts = [loss, L1, SSIM] (device, no sync)."""
+    if img.dim() != 3 or img.device.type != "cuda":
+        raise RuntimeError("fused_l1_ssim_loss expects a [C,H,W] tensor on a HIP device")
+    return _FusedL1SSIM.apply(img, gt, lambda_dssim)
 
 
 @lru_cache(maxsize=8)

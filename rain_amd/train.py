@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 
 from .gaussian_model import GaussianModel, OptimizationParams, low_pass_schedule
-from .loss import l1_loss, ssim_separable
+from .loss import fused_l1_ssim_loss
 from .renderer import PipelineParams, render
 
 
@@ -118,8 +118,8 @@ class Trainer:
         pkg = render(cam, g, self.pipe, self.background, low_pass=self.low_pass)
         image, vsp, vis, radii = pkg["render"], pkg["viewspace_points"], pkg["visibility_filter"], pkg["radii"]
         gt = self.gt[vidx]
-        Ll1 = l1_loss(image, gt)
-        loss = (1.0 - opt.lambda_dssim) * Ll1 + opt.lambda_dssim * (1.0 - ssim_separable(image, gt))
+        # (1-λ)·L1 + λ·(1-SSIM) (train.py:113-114) as one fused HIP forward/backward
+        loss, _parts = fused_l1_ssim_loss(image, gt, opt.lambda_dssim)
         loss.backward()
 
         densified = False
