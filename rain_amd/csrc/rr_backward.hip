@@ -1,143 +1,14 @@
 // rr_backward.hip — backward kernels of the MI355X rasterizer.
 //
-//   k_blend_bwd        per-tile back-to-front replay (backward.cu:389-547 semantics)
 //   k_gauss_bwd<DEG>   one thread per Gaussian: the reference's computeCov2DCUDA
 //                      (backward.cu:133-264) + preprocessCUDA (backward.cu:336-386, SH bwd :9-128,
 //                      cov3D bwd :268-331) fused, writing every gradient output exactly once
-//                      (so the host allocates them uninitialised — no zero-fill pass).
-//
-// Gradient accumulation: the reference issues 9 fp32 atomicAdds per contributing
-// (pixel, Gaussian) pair.  On MI355X float atomics are executed memory-side at ~1.3 TB/s
-// chip-wide, so here each wave first sums its 64 pixels' contributions with DPP (no LDS),
-// lane 63 parks the 9 wave sums in LDS, and after each 256-pair round the workgroup adds the
-// four waves' sums and issues ONE atomic per (tile, Gaussian, component), laid out so that a
-// pair's 9 adds fall into one 64-B line.  Pairs no pixel of a wave touched are skipped by ballot.
+//                      (so the host allocates them uninitialised — no zero-fill pass).  It consumes
+//                      the per-Gaussian accumulators the blend backward (rr_blend.hip) filled.
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
 namespace rr {
-
-__global__ __launch_bounds__(256) void k_blend_bwd(BlendBwdArgs a) {
-    const int tile = blockIdx.x;
-    const int tx = tile % a.gx, ty = tile / a.gx;
-    const int t = threadIdx.x;
-    const int w = t >> 6;
-    const int lane = t & 63;
-    const int px = tx * TILE_X + (t & 15), py = ty * TILE_Y + (t >> 4);
-    const bool inside = px < a.W && py < a.H;
-    const float pfx = (float)px, pfy = (float)py;
-
-    __shared__ float4 s_a[TILE_PIX];
-    __shared__ float4 s_b[TILE_PIX];
-    __shared__ float4 s_c[TILE_PIX];
-    __shared__ uint32_t s_id[TILE_PIX];
-    __shared__ float s_g[4][TILE_PIX * NGRAD];
-
-    const uint2 range = a.ranges[tile];
-    const int nmax = (int)a.tile_max[tile];  // pairs past this index were blended by no pixel
-    const size_t HW = (size_t)a.H * a.W;
-    const int pix = a.W * py + px;
-
-    const float T_final = inside ? a.final_T[pix] : 0.f;
-    float T = T_final;
-    const int last_contributor = inside ? (int)a.n_contrib[pix] : 0;
-    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
-    if (inside) {
-        dp0 = a.dL_dpix[pix];
-        dp1 = a.dL_dpix[HW + pix];
-        dp2 = a.dL_dpix[2 * HW + pix];
-    }
-    const float bg_dot_dpixel = a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2;
-    float ar0 = 0.f, ar1 = 0.f, ar2 = 0.f;  // accum_rec
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;  // last_color
-    float last_alpha = 0.f;
-    const float ddelx_dx = 0.5f * a.W;
-    const float ddely_dy = 0.5f * a.H;
-
-    for (int base = 0; base < nmax; base += TILE_PIX) {
-        __syncthreads();
-        const int k = base + t;
-        if (k < nmax) {
-            const uint32_t g = a.point_list[range.x + nmax - 1 - k];
-            const Splat s = a.splats[g];
-            s_id[t] = g;
-            s_a[t] = s.a;
-            s_b[t] = s.b;
-            s_c[t] = s.c;
-        }
-        __syncthreads();
-        const int cnt = min(TILE_PIX, nmax - base);
-        for (int j = 0; j < cnt; j++) {
-            const int contributor = nmax - 1 - (base + j);
-            const float4 A = s_a[j];
-            const float4 B = s_b[j];
-            const float dx = A.x - pfx, dy = A.y - pfy;
-            const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-            const float G = __expf(power);
-            const float alpha = fminf(0.99f, B.y * G);
-            const bool act = contributor < last_contributor && power <= 0.0f && alpha >= 1.0f / 255.0f;
-            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
-            if (act) {
-                T = __fdividef(T, 1.f - alpha);
-                const float dchannel_dcolor = alpha * T;
-                const float4 Cc = s_c[j];
-                ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0;
-                ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1;
-                ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2;
-                lc0 = Cc.x;
-                lc1 = Cc.y;
-                lc2 = Cc.z;
-                float dL_dalpha = (Cc.x - ar0) * dp0 + (Cc.y - ar1) * dp1 + (Cc.z - ar2) * dp2;
-                g6 = dchannel_dcolor * dp0;
-                g7 = dchannel_dcolor * dp1;
-                g8 = dchannel_dcolor * dp2;
-                dL_dalpha *= T;
-                last_alpha = alpha;
-                dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
-                const float dL_dG = B.y * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * A.z - gdy * A.w;
-                const float dG_ddely = -gdy * B.x - gdx * A.w;
-                g0 = dL_dG * dG_ddelx * ddelx_dx;
-                g1 = dL_dG * dG_ddely * ddely_dy;
-                g2 = -0.5f * gdx * dx * dL_dG;
-                g3 = -0.5f * gdx * dy * dL_dG;
-                g4 = -0.5f * gdy * dy * dL_dG;
-                g5 = G * dL_dalpha;
-            }
-            float* sg = &s_g[w][j * NGRAD];
-            if (__ballot(act) != 0ull) {
-                g0 = wave_sum_lane63(g0);
-                g1 = wave_sum_lane63(g1);
-                g2 = wave_sum_lane63(g2);
-                g3 = wave_sum_lane63(g3);
-                g4 = wave_sum_lane63(g4);
-                g5 = wave_sum_lane63(g5);
-                g6 = wave_sum_lane63(g6);
-                g7 = wave_sum_lane63(g7);
-                g8 = wave_sum_lane63(g8);
-                if (lane == 63) {
-                    sg[0] = g0; sg[1] = g1; sg[2] = g2; sg[3] = g3; sg[4] = g4;
-                    sg[5] = g5; sg[6] = g6; sg[7] = g7; sg[8] = g8;
-                }
-            } else if (lane == 63) {
-#pragma unroll
-                for (int c = 0; c < NGRAD; c++) sg[c] = 0.f;
-            }
-        }
-        __syncthreads();
-        // one atomic per (pair, component); consecutive lanes hit consecutive components of a pair
-#pragma unroll
-        for (int c = 0; c < NGRAD; c++) {
-            const int e = c * TILE_PIX + t;
-            const int pair = e / NGRAD;
-            if (pair < cnt) {
-                const float v = s_g[0][e] + s_g[1][e] + s_g[2][e] + s_g[3][e];
-                if (v != 0.f) atomicAdd(a.gacc + (size_t)s_id[pair] * GACC_STRIDE + (e - pair * NGRAD), v);
-            }
-        }
-    }
-}
 
 // ---- per-Gaussian backward -------------------------------------------------------------
 
@@ -389,12 +260,6 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         dscale[0] = dscale[1] = dscale[2] = 0.f;
         *drot = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-}
-
-void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
-    const int T = a.gx * a.gy;
-    if (T == 0) return;
-    k_blend_bwd<<<T, TILE_PIX, 0, st>>>(a);
 }
 
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st) {

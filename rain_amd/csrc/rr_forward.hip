@@ -138,87 +138,6 @@ __global__ __launch_bounds__(256) void k_ranges(int L, const K* __restrict__ key
     if (i == L - 1) ranges[cur].y = L;
 }
 
-// One workgroup (4 wave64) per 16x16 tile, one thread per pixel.  Each round stages 256 splat
-// records in LDS (one coalesced id load + one 48-B record gather per thread); the inner loop
-// reads them as LDS broadcasts.  A round starts only if some pixel of the tile is still open
-// (__syncthreads_count, forward.cu:302-304); a wave whose 64 pixels are all saturated leaves the
-// inner loop on its own (divergent loop exit), so early termination is per wave, not per tile.
-__global__ __launch_bounds__(256) void k_blend_fwd(BlendFwdArgs a) {
-    const int tile = blockIdx.x;
-    const int tx = tile % a.gx, ty = tile / a.gx;
-    const int t = threadIdx.x;
-    const int px = tx * TILE_X + (t & 15), py = ty * TILE_Y + (t >> 4);
-    const bool inside = px < a.W && py < a.H;
-    const float pfx = (float)px, pfy = (float)py;
-    bool done = !inside;
-
-    __shared__ float4 s_a[TILE_PIX];
-    __shared__ float4 s_b[TILE_PIX];
-    __shared__ float4 s_c[TILE_PIX];
-    __shared__ uint32_t s_max[4];
-
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-    float T = 1.0f;
-    uint32_t contributor = 0, last_contributor = 0;
-    float C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-
-    for (int base = 0; base < n; base += TILE_PIX) {
-        if (__syncthreads_count(done) == TILE_PIX) break;
-        const int k = base + t;
-        if (k < n) {
-            const uint32_t g = a.point_list[range.x + k];
-            const Splat s = a.splats[g];
-            s_a[t] = s.a;
-            s_b[t] = s.b;
-            s_c[t] = s.c;
-        }
-        __syncthreads();
-        const int cnt = min(TILE_PIX, n - base);
-        for (int j = 0; !done && j < cnt; j++) {
-            contributor++;
-            const float4 A = s_a[j];
-            const float4 B = s_b[j];
-            const float dx = A.x - pfx, dy = A.y - pfy;
-            const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, B.y * __expf(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1 - alpha);
-            if (test_T < 0.0001f) {
-                done = true;
-                continue;
-            }
-            const float4 Cc = s_c[j];
-            C0 += Cc.x * alpha * T;
-            C1 += Cc.y * alpha * T;
-            C2 += Cc.z * alpha * T;
-            Dp += B.z * alpha * T;
-            T = test_T;
-            last_contributor = contributor;
-        }
-    }
-
-    // per-tile max contributor count: lets the backward skip pairs no pixel blended
-    uint32_t m = inside ? last_contributor : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    if ((t & 63) == 0) s_max[t >> 6] = m;
-    __syncthreads();
-    if (t == 0) a.tile_max[tile] = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
-
-    if (inside) {
-        const int pix = a.W * py + px;
-        const size_t HW = (size_t)a.H * a.W;
-        a.final_T[pix] = T;
-        a.n_contrib[pix] = last_contributor;
-        a.out_color[pix] = C0 + T * a.bg[0];
-        a.out_color[HW + pix] = C1 + T * a.bg[1];
-        a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
-        a.out_depth[pix] = Dp;
-    }
-}
-
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
                                                       const float* __restrict__ view, uint8_t* __restrict__ present) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -265,12 +184,6 @@ void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st) {
 }
 template void launch_ranges<uint16_t>(int, const uint16_t*, uint2*, hipStream_t);
 template void launch_ranges<uint32_t>(int, const uint32_t*, uint2*, hipStream_t);
-
-void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
-    const int T = a.gx * a.gy;
-    if (T == 0) return;
-    k_blend_fwd<<<T, TILE_PIX, 0, st>>>(a);
-}
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;
