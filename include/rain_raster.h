@@ -164,6 +164,10 @@ enum rr_stage {
     RR_NUM_STAGES
 };
 int rr_profile_enable(int enable);
+
+/* Tuning knob (diagnostics / A-B tests): wave64s per 16x16 tile used by the forward and backward
+ * blend kernels (1, 2 or 4; 0 restores the default).  Results are identical for every choice. */
+int rr_set_blend_config(int fwd_waves, int bwd_waves);
 int rr_profile_collect(double* ms, int64_t* counts);
 const char* rr_stage_name(int stage);
 

@@ -67,6 +67,9 @@ def lib():
         L.orc_num_rendered.restype = ctypes.c_int
         L.orc_num_rendered.argtypes = [ctypes.c_void_p]
         L.orc_threads.restype = ctypes.c_int
+        L.orc_sh_eval.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
+        L.orc_pixel_blend_list.restype = ctypes.c_int
+        L.orc_pixel_blend_list.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _u32p, ctypes.c_int]
         if hasattr(L, "orc_dist_knn3"):
             L.orc_dist_knn3.restype = ctypes.c_int
             L.orc_dist_knn3.argtypes = [ctypes.c_int, _f32p, _f32p]
@@ -125,6 +128,17 @@ class State:
         if n == 0:
             return np.zeros(0, dtype=dtype)
         return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+    def blend_lists(self, cap: int = 4096):
+        """Per pixel (row-major), the ordered Gaussian ids the forward blended."""
+        L = lib()
+        buf = np.zeros(cap, np.uint32)
+        out = []
+        for py in range(self.H):
+            for px in range(self.W):
+                n = L.orc_pixel_blend_list(self.handle, px, py, _p(buf, _u32p), cap)
+                out.append(buf[:min(n, cap)].copy())
+        return out
 
     @property
     def num_rendered(self):
@@ -216,6 +230,18 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         lib().orc_mark_visible(P, _p(means3D), _p(_f32(viewmatrix).reshape(16)), _p(_f32(projmatrix).reshape(16)),
                                _p(out, _u8p))
     return out.astype(bool)
+
+
+def sh_eval(deg, shs, dirs):
+    """forward.cu:9-60 on unit directions: returns (rgb = max(SH+0.5, 0) [n,3], clamped [n,3] bool).
+    shs is [n, M, 3] (kernel layout, coefficient-major)."""
+    shs = _f32(shs)
+    n, M = shs.shape[0], shs.shape[1]
+    d = _f32(dirs).reshape(n, 3)
+    out = np.zeros((n, 3), np.float32)
+    cl = np.zeros((n, 3), np.uint8)
+    lib().orc_sh_eval(int(deg), M, n, _p(d), _p(shs), _p(out), _p(cl, _u8p))
+    return out, cl.astype(bool)
 
 
 def get_higher_msb(n: int) -> int:

@@ -211,6 +211,19 @@ static f3 color_from_sh(int deg, int max_coeffs, f3 pos, f3 campos, const float*
     return mk3(maxf(result.x, 0.f), maxf(result.y, 0.f), maxf(result.z, 0.f));
 }
 
+/* SH colour for a given unit direction (forward.cu:18-59 after the normalisation at :14-16):
+ * out = max(SH(dir) + 0.5, 0), clamped = (SH(dir) + 0.5 < 0).  Test entry point. */
+void orc_sh_eval(int deg, int max_coeffs, int n, const float* dirs, const float* shs, float* out,
+                 unsigned char* clamped) {
+    for (int i = 0; i < n; i++) {
+        /* campos = 0, pos = dir: color_from_sh re-normalises an (already unit) direction */
+        f3 d = mk3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+        f3 rgb = color_from_sh(deg, max_coeffs, d, mk3(0.f, 0.f, 0.f), shs + (size_t)i * max_coeffs * 3,
+                               clamped + 3 * (size_t)i);
+        out[3 * i] = rgb.x; out[3 * i + 1] = rgb.y; out[3 * i + 2] = rgb.z;
+    }
+}
+
 /* ------------------------------------------------------------------------------------ */
 
 typedef struct orc_state {
@@ -759,6 +772,30 @@ int orc_backward(orc_state* s, const float* bg, const float* means3D, const int*
         }
     }
     return 0;
+}
+
+/* Ordered Gaussian ids actually blended into pixel (px, py) by the forward (the discrete
+ * decisions of forward.cu:318-356 replayed on the stored state).  Returns the count. */
+int orc_pixel_blend_list(const orc_state* s, int px, int py, uint32_t* out_ids, int cap) {
+    int tile = (py / BLOCK_Y) * s->gx + (px / BLOCK_X);
+    uint32_t rs = s->ranges[2 * tile], re = s->ranges[2 * tile + 1];
+    float pfx = (float)px, pfy = (float)py, Tr = 1.0f;
+    int n = 0;
+    for (uint32_t k = rs; k < re; k++) {
+        uint32_t g = s->point_list[k];
+        float dx = s->xy[2 * g] - pfx, dy = s->xy[2 * g + 1] - pfy;
+        const float* co = s->conic_opacity + 4 * (size_t)g;
+        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+        if (power > 0.0f) continue;
+        float alpha = minf(0.99f, co[3] * expf(power));
+        if (alpha < 1.0f / 255.0f) continue;
+        float test_T = Tr * (1 - alpha);
+        if (test_T < 0.0001f) break;
+        if (n < cap) out_ids[n] = g;
+        n++;
+        Tr = test_T;
+    }
+    return n;
 }
 
 /* ---- state accessors for tests ---- */

@@ -57,7 +57,7 @@ class RRDebugViews(ctypes.Structure):
 # every symbol include/rain_raster.h declares (tests check the .so exports all of them)
 RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
                   "rr_forward_geometry", "rr_forward_render", "rr_backward", "rr_mark_visible", "rr_last_error",
-                  "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_profile_enable",
+                  "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config", "rr_profile_enable",
                   "rr_profile_collect", "rr_stage_name"]
 
 _raster = None
@@ -100,6 +100,8 @@ def raster():
         L.rr_read_frame_stats.argtypes = [fp, vp, vp, ctypes.POINTER(RRFrameStats), vp]
         L.rr_debug_get_views.restype = ci
         L.rr_debug_get_views.argtypes = [fp, vp, vp, vp, ci, ctypes.POINTER(RRDebugViews)]
+        L.rr_set_blend_config.restype = ci
+        L.rr_set_blend_config.argtypes = [ci, ci]
         L.rr_profile_enable.restype = ci
         L.rr_profile_enable.argtypes = [ci]
         L.rr_profile_collect.restype = ci

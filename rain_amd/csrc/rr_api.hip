@@ -493,6 +493,13 @@ int rr_debug_get_views(const rr_frame* f, const void* geom_buffer, const void* i
     return RR_OK;
 }
 
+int rr_set_blend_config(int fwd_waves, int bwd_waves) {
+    auto ok = [](int v) { return v == 0 || v == 1 || v == 2 || v == 4; };
+    if (!ok(fwd_waves) || !ok(bwd_waves)) return fail(RR_ERR_ARG, "waves per tile must be 0, 1, 2 or 4");
+    set_blend_config(fwd_waves, bwd_waves);
+    return RR_OK;
+}
+
 int rr_profile_enable(int enable) {
     g_prof = enable != 0;
     return RR_OK;

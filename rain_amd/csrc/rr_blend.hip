@@ -1,49 +1,59 @@
 // rr_blend.hip — per-tile alpha blending, forward and backward (forward.cu:251-369, backward.cu:389-547).
 //
-// CDNA4 mapping: ONE wave64 per 16x16 tile, FOUR pixels per lane (lane l owns column l%16 of rows
-// l/16, l/16+4, l/16+8, l/16+12).  Compared with the reference's 256-thread block per tile:
-//   * the per-pair record (48 B) is staged once in LDS and read as a broadcast by 64 lanes that
-//     each use it for 4 pixels (4x less LDS/VALU overhead per pixel);
-//   * a workgroup is a single wave: no cross-wave barrier cost, no __syncthreads_count; early
-//     termination is a wave vote (`__all`) checked per pair;
-//   * backward: each lane first sums its 4 pixels' contributions in registers, then ONE wave-wide
-//     DPP reduction per (tile, Gaussian) pair (the reference issues 9 atomics per pixel), and the
-//     pair sums are flushed with one coalesced batch of global float atomics per 64 pairs;
-//   * tiles are assigned XCD-contiguously (blockIdx % 8 selects an XCD on MI355X), so tiles that
-//     share Gaussians share an L2.
+// CDNA4 mapping.  A 16x16 tile is processed by NW wave64s (NW = 1, 2 or 4, chosen per kernel at
+// run time, see rr_set_blend_config), each lane owning PPL = 4/NW pixels of one column: thread t
+// (lane l = t%64, wave w = t/64) owns column l%16 of rows l/16 + 4*(w*PPL + q), q < PPL.
+//   * Each round stages 64*NW (tile, Gaussian) records (48 B each, rr_common.hpp Splat) in LDS; the
+//     NEXT round's records are fetched into registers while the current round is blended, so the
+//     dependent id -> record gather latency is hidden behind compute.
+//   * All lanes read a staged record as an LDS broadcast and apply it to their PPL pixels.
+//   * Forward early termination: a round starts only if some pixel of the tile is open
+//     (__syncthreads_count, forward.cu:302-304); inside a round each wave leaves as soon as all its
+//     pixels are saturated (wave vote), pixel groups that are done are skipped by exec mask.
+//   * Backward: each lane sums its PPL pixels' contributions in registers, each wave reduces the 9
+//     gradient components across its 64 lanes with DPP (no LDS), lane 63 parks the wave sums in
+//     LDS, and after each round ONE global float atomic per (tile, Gaussian, component) is issued,
+//     consecutive lanes on consecutive components of a Gaussian's 64-B accumulator line (the
+//     reference issues 9 atomics per contributing PIXEL).  The backward only walks the first
+//     max(n_contrib) pairs of a tile (recorded by the forward).
+//   * Tiles are assigned XCD-contiguously (the dispatcher sends block b to XCD b % 8), so tiles
+//     sharing Gaussians share an L2.
+#include <cstdlib>
+
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
 namespace rr {
 
-constexpr int WPIX = 4;  // pixels per lane
-
-// Bijective block -> tile remap: the blocks the dispatcher sends to one XCD (b % 8) get one
-// contiguous run of tiles (cdna_hip_programming.md §5, "XCD swizzle must be bijective").
+// Bijective block -> tile remap (cdna_hip_programming.md §5, "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_tile(int b, int n) {
     const int q = n >> 3, r = n & 7;
     const int x = b & 7, s = b >> 3;
     return x < r ? x * (q + 1) + s : r * (q + 1) + (x - r) * q + s;
 }
 
-__global__ __launch_bounds__(64) void k_blend_fwd(BlendFwdArgs a) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
+    constexpr int PPL = 4 / NW;
+    constexpr int B = 64 * NW;
     const int ntiles = a.gx * a.gy;
     const int tile = xcd_tile(blockIdx.x, ntiles);
     const int tx = tile % a.gx, ty = tile / a.gx;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
     const int px = tx * TILE_X + (lane & 15);
-    const int py0 = ty * TILE_Y + (lane >> 4);
+    const int py0 = ty * TILE_Y + (lane >> 4) + 4 * w * PPL;
     const float pfx = (float)px;
 
-    __shared__ float4 s_a[64];
-    __shared__ float4 s_b[64];
-    __shared__ float4 s_c[64];
+    __shared__ float4 s_a[B];
+    __shared__ float4 s_b[B];
+    __shared__ float4 s_c[B];
 
-    float T[WPIX], C0[WPIX], C1[WPIX], C2[WPIX], Dp[WPIX];
-    uint32_t contrib[WPIX], last[WPIX];
-    bool done[WPIX];
+    float T[PPL], C0[PPL], C1[PPL], C2[PPL], Dp[PPL];
+    uint32_t contrib[PPL], last[PPL];
+    bool done[PPL];
 #pragma unroll
-    for (int q = 0; q < WPIX; q++) {
+    for (int q = 0; q < PPL; q++) {
         T[q] = 1.0f;
         C0[q] = C1[q] = C2[q] = Dp[q] = 0.f;
         contrib[q] = last[q] = 0;
@@ -52,31 +62,33 @@ __global__ __launch_bounds__(64) void k_blend_fwd(BlendFwdArgs a) {
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
 
-    for (int base = 0; base < n; base += 64) {
-        bool lane_done = done[0] && done[1] && done[2] && done[3];
-        if (__all(lane_done)) break;
-        const int k = base + lane;
-        if (k < n) {
-            const Splat s = a.splats[a.point_list[range.x + k]];
-            s_a[lane] = s.a;
-            s_b[lane] = s.b;
-            s_c[lane] = s.c;
+    Splat nxt;
+    if (t < n) nxt = a.splats[a.point_list[range.x + t]];
+    for (int base = 0; base < n; base += B) {
+        bool my_done = true;
+#pragma unroll
+        for (int q = 0; q < PPL; q++) my_done = my_done && done[q];
+        if (__syncthreads_count(my_done) == B) break;
+        if (base + t < n) {
+            s_a[t] = nxt.a;
+            s_b[t] = nxt.b;
+            s_c[t] = nxt.c;
         }
         __syncthreads();
-        const int cnt = min(64, n - base);
+        if (base + B + t < n) nxt = a.splats[a.point_list[range.x + base + B + t]];  // prefetch next round
+        const int cnt = min(B, n - base);
         for (int j = 0; j < cnt; j++) {
-            lane_done = done[0] && done[1] && done[2] && done[3];
-            if (__all(lane_done)) break;
+            if (__all(my_done)) break;
             const float4 A = s_a[j];
-            const float4 B = s_b[j];
+            const float4 Bv = s_b[j];
 #pragma unroll
-            for (int q = 0; q < WPIX; q++) {
+            for (int q = 0; q < PPL; q++) {
                 if (!done[q]) {
                     contrib[q]++;
                     const float dx = A.x - pfx, dy = A.y - (float)(py0 + 4 * q);
-                    const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
+                    const float power = -0.5f * (A.z * dx * dx + Bv.x * dy * dy) - A.w * dx * dy;
                     if (power <= 0.0f) {
-                        const float alpha = fminf(0.99f, B.y * __expf(power));
+                        const float alpha = fminf(0.99f, Bv.y * __expf(power));
                         if (alpha >= 1.0f / 255.0f) {
                             const float test_T = T[q] * (1 - alpha);
                             if (test_T < 0.0001f) {
@@ -86,7 +98,7 @@ __global__ __launch_bounds__(64) void k_blend_fwd(BlendFwdArgs a) {
                                 C0[q] += Cc.x * alpha * T[q];
                                 C1[q] += Cc.y * alpha * T[q];
                                 C2[q] += Cc.z * alpha * T[q];
-                                Dp[q] += B.z * alpha * T[q];
+                                Dp[q] += Bv.z * alpha * T[q];
                                 T[q] = test_T;
                                 last[q] = contrib[q];
                             }
@@ -94,6 +106,9 @@ __global__ __launch_bounds__(64) void k_blend_fwd(BlendFwdArgs a) {
                     }
                 }
             }
+            my_done = true;
+#pragma unroll
+            for (int q = 0; q < PPL; q++) my_done = my_done && done[q];
         }
         __syncthreads();
     }
@@ -101,7 +116,7 @@ __global__ __launch_bounds__(64) void k_blend_fwd(BlendFwdArgs a) {
     uint32_t m = 0;
     const size_t HW = (size_t)a.H * a.W;
 #pragma unroll
-    for (int q = 0; q < WPIX; q++) {
+    for (int q = 0; q < PPL; q++) {
         const int py = py0 + 4 * q;
         if (px < a.W && py < a.H) {
             m = max(m, last[q]);
@@ -116,33 +131,49 @@ __global__ __launch_bounds__(64) void k_blend_fwd(BlendFwdArgs a) {
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    if (lane == 0) a.tile_max[tile] = m;
+    if (NW == 1) {
+        if (lane == 0) a.tile_max[tile] = m;
+    } else {
+        __shared__ uint32_t s_m[NW];
+        if (lane == 0) s_m[w] = m;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t mm = s_m[0];
+#pragma unroll
+            for (int i = 1; i < NW; i++) mm = max(mm, s_m[i]);
+            a.tile_max[tile] = mm;
+        }
+    }
 }
 
-__global__ __launch_bounds__(64) void k_blend_bwd(BlendBwdArgs a) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
+    constexpr int PPL = 4 / NW;
+    constexpr int B = 64 * NW;
     const int ntiles = a.gx * a.gy;
     const int tile = xcd_tile(blockIdx.x, ntiles);
     const int nmax = (int)a.tile_max[tile];  // pairs past this index were blended by no pixel
     if (nmax == 0) return;
     const int tx = tile % a.gx, ty = tile / a.gx;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
     const int px = tx * TILE_X + (lane & 15);
-    const int py0 = ty * TILE_Y + (lane >> 4);
+    const int py0 = ty * TILE_Y + (lane >> 4) + 4 * w * PPL;
     const float pfx = (float)px;
 
-    __shared__ float4 s_a[64];
-    __shared__ float4 s_b[64];
-    __shared__ float4 s_c[64];
-    __shared__ uint32_t s_id[64];
-    __shared__ float s_g[64 * NGRAD];
+    __shared__ float4 s_a[B];
+    __shared__ float4 s_b[B];
+    __shared__ float4 s_c[B];
+    __shared__ uint32_t s_id[B];
+    __shared__ float s_g[NW][B * NGRAD];
 
     const size_t HW = (size_t)a.H * a.W;
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
-    float T[WPIX], Tf[WPIX], dp0[WPIX], dp1[WPIX], dp2[WPIX], bgd[WPIX];
-    float ar0[WPIX], ar1[WPIX], ar2[WPIX], lc0[WPIX], lc1[WPIX], lc2[WPIX], la[WPIX];
-    int last[WPIX];
+    float T[PPL], Tf[PPL], dp0[PPL], dp1[PPL], dp2[PPL], bgd[PPL];
+    float ar0[PPL], ar1[PPL], ar2[PPL], lc0[PPL], lc1[PPL], lc2[PPL], la[PPL];
+    int last[PPL];
 #pragma unroll
-    for (int q = 0; q < WPIX; q++) {
+    for (int q = 0; q < PPL; q++) {
         const int py = py0 + 4 * q;
         const bool inside = px < a.W && py < a.H;
         const int pix = a.W * py + px;
@@ -159,30 +190,38 @@ __global__ __launch_bounds__(64) void k_blend_bwd(BlendBwdArgs a) {
     const float ddelx_dx = 0.5f * a.W;
     const float ddely_dy = 0.5f * a.H;
 
-    for (int base = 0; base < nmax; base += 64) {
-        const int k = base + lane;
-        if (k < nmax) {
-            const uint32_t g = a.point_list[range.x + nmax - 1 - k];
-            const Splat s = a.splats[g];
-            s_id[lane] = g;
-            s_a[lane] = s.a;
-            s_b[lane] = s.b;
-            s_c[lane] = s.c;
+    uint32_t nid = 0;
+    Splat nxt;
+    if (t < nmax) {
+        nid = a.point_list[range.x + nmax - 1 - t];
+        nxt = a.splats[nid];
+    }
+    for (int base = 0; base < nmax; base += B) {
+        if (base + t < nmax) {
+            s_id[t] = nid;
+            s_a[t] = nxt.a;
+            s_b[t] = nxt.b;
+            s_c[t] = nxt.c;
         }
         __syncthreads();
-        const int cnt = min(64, nmax - base);
+        const int k2 = base + B + t;  // prefetch the next round while this one is blended
+        if (k2 < nmax) {
+            nid = a.point_list[range.x + nmax - 1 - k2];
+            nxt = a.splats[nid];
+        }
+        const int cnt = min(B, nmax - base);
         for (int j = 0; j < cnt; j++) {
             const int contributor = nmax - 1 - (base + j);
             const float4 A = s_a[j];
-            const float4 B = s_b[j];
+            const float4 Bv = s_b[j];
             float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
             bool any = false;
 #pragma unroll
-            for (int q = 0; q < WPIX; q++) {
+            for (int q = 0; q < PPL; q++) {
                 const float dx = A.x - pfx, dy = A.y - (float)(py0 + 4 * q);
-                const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
+                const float power = -0.5f * (A.z * dx * dx + Bv.x * dy * dy) - A.w * dx * dy;
                 const float G = __expf(power);
-                const float alpha = fminf(0.99f, B.y * G);
+                const float alpha = fminf(0.99f, Bv.y * G);
                 const bool act = contributor < last[q] && power <= 0.0f && alpha >= 1.0f / 255.0f;
                 if (act) {
                     any = true;
@@ -203,10 +242,10 @@ __global__ __launch_bounds__(64) void k_blend_bwd(BlendBwdArgs a) {
                     dL_dalpha *= T[q];
                     la[q] = alpha;
                     dL_dalpha += __fdividef(-Tf[q], one_m) * bgd[q];
-                    const float dL_dG = B.y * dL_dalpha;
+                    const float dL_dG = Bv.y * dL_dalpha;
                     const float gdx = G * dx, gdy = G * dy;
                     const float dG_ddelx = -gdx * A.z - gdy * A.w;
-                    const float dG_ddely = -gdy * B.x - gdx * A.w;
+                    const float dG_ddely = -gdy * Bv.x - gdx * A.w;
                     g0 += dL_dG * dG_ddelx * ddelx_dx;
                     g1 += dL_dG * dG_ddely * ddely_dy;
                     g2 += -0.5f * gdx * dx * dL_dG;
@@ -215,7 +254,7 @@ __global__ __launch_bounds__(64) void k_blend_bwd(BlendBwdArgs a) {
                     g5 += G * dL_dalpha;
                 }
             }
-            float* sg = &s_g[j * NGRAD];
+            float* sg = &s_g[w][j * NGRAD];
             if (__ballot(any) != 0ull) {
                 g0 = wave_sum_lane63(g0);
                 g1 = wave_sum_lane63(g1);
@@ -239,10 +278,12 @@ __global__ __launch_bounds__(64) void k_blend_bwd(BlendBwdArgs a) {
         // one atomic per (pair, component); consecutive lanes hit consecutive components of a pair
 #pragma unroll
         for (int c = 0; c < NGRAD; c++) {
-            const int e = c * 64 + lane;
+            const int e = c * B + t;
             const int pair = e / NGRAD;
             if (pair < cnt) {
-                const float v = s_g[e];
+                float v = s_g[0][e];
+#pragma unroll
+                for (int i = 1; i < NW; i++) v += s_g[i][e];
                 if (v != 0.f) atomicAdd(a.gacc + (size_t)s_id[pair] * GACC_STRIDE + (e - pair * NGRAD), v);
             }
         }
@@ -250,16 +291,46 @@ __global__ __launch_bounds__(64) void k_blend_bwd(BlendBwdArgs a) {
     }
 }
 
+namespace {
+int g_fwd_waves = 0;
+int g_bwd_waves = 0;
+int env_waves(const char* name, int dflt) {
+    const char* s = std::getenv(name);
+    if (!s) return dflt;
+    const int v = std::atoi(s);
+    return (v == 1 || v == 2 || v == 4) ? v : dflt;
+}
+}  // namespace
+
+// Defaults: measured on MI355X (profiles/, DESIGN.md §Blend kernels).
+constexpr int kFwdWavesDefault = 4;
+constexpr int kBwdWavesDefault = 1;
+
+void set_blend_config(int fwd_waves, int bwd_waves) {
+    g_fwd_waves = fwd_waves;
+    g_bwd_waves = bwd_waves;
+}
+
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
-    k_blend_fwd<<<T, 64, 0, st>>>(a);
+    const int nw = g_fwd_waves ? g_fwd_waves : env_waves("RAIN_BLEND_FWD_WAVES", kFwdWavesDefault);
+    switch (nw) {
+        case 1: k_blend_fwd<1><<<T, 64, 0, st>>>(a); break;
+        case 2: k_blend_fwd<2><<<T, 128, 0, st>>>(a); break;
+        default: k_blend_fwd<4><<<T, 256, 0, st>>>(a); break;
+    }
 }
 
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
-    k_blend_bwd<<<T, 64, 0, st>>>(a);
+    const int nw = g_bwd_waves ? g_bwd_waves : env_waves("RAIN_BLEND_BWD_WAVES", kBwdWavesDefault);
+    switch (nw) {
+        case 2: k_blend_bwd<2><<<T, 128, 0, st>>>(a); break;
+        case 4: k_blend_bwd<4><<<T, 256, 0, st>>>(a); break;
+        default: k_blend_bwd<1><<<T, 64, 0, st>>>(a); break;
+    }
 }
 
 }  // namespace rr

@@ -87,3 +87,8 @@ void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
 
 }  // namespace rr
+
+namespace rr {
+// Tuning knob: waves per tile (1, 2, 4) of the blend kernels; 0 = default / env override.
+void set_blend_config(int fwd_waves, int bwd_waves);
+}  // namespace rr
