@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
 
     const size_t HW = (size_t)a.H * a.W;
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
-    float T[PPL], Tf[PPL], dp0[PPL], dp1[PPL], dp2[PPL], bgd[PPL];
+    float T[PPL], tfbg[PPL], dp0[PPL], dp1[PPL], dp2[PPL];
     float ar0[PPL], ar1[PPL], ar2[PPL], lc0[PPL], lc1[PPL], lc2[PPL], la[PPL];
     int last[PPL];
 #pragma unroll
@@ -177,13 +177,14 @@ __global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
         const int py = py0 + 4 * q;
         const bool inside = px < a.W && py < a.H;
         const int pix = a.W * py + px;
-        Tf[q] = inside ? a.final_T[pix] : 0.f;
-        T[q] = Tf[q];
+        const float Tf = inside ? a.final_T[pix] : 0.f;
+        T[q] = Tf;
         last[q] = inside ? (int)a.n_contrib[pix] : 0;
         dp0[q] = inside ? a.dL_dpix[pix] : 0.f;
         dp1[q] = inside ? a.dL_dpix[HW + pix] : 0.f;
         dp2[q] = inside ? a.dL_dpix[2 * HW + pix] : 0.f;
-        bgd[q] = bg0 * dp0[q] + bg1 * dp1[q] + bg2 * dp2[q];
+        // -T_final * (bg . dL/dpixel): numerator of the background term (backward.cu:521-524)
+        tfbg[q] = -Tf * (bg0 * dp0[q] + bg1 * dp1[q] + bg2 * dp2[q]);
         ar0[q] = ar1[q] = ar2[q] = lc0[q] = lc1[q] = lc2[q] = la[q] = 0.f;
     }
     const uint2 range = a.ranges[tile];
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
                     g8 += dchannel_dcolor * dp2[q];
                     dL_dalpha *= T[q];
                     la[q] = alpha;
-                    dL_dalpha += __fdividef(-Tf[q], one_m) * bgd[q];
+                    dL_dalpha += __fdividef(tfbg[q], one_m);
                     const float dL_dG = Bv.y * dL_dalpha;
                     const float gdx = G * dx, gdy = G * dy;
                     const float dG_ddelx = -gdx * A.z - gdy * A.w;
@@ -255,24 +256,9 @@ __global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
                 }
             }
             float* sg = &s_g[w][j * NGRAD];
-            if (__ballot(any) != 0ull) {
-                g0 = wave_sum_lane63(g0);
-                g1 = wave_sum_lane63(g1);
-                g2 = wave_sum_lane63(g2);
-                g3 = wave_sum_lane63(g3);
-                g4 = wave_sum_lane63(g4);
-                g5 = wave_sum_lane63(g5);
-                g6 = wave_sum_lane63(g6);
-                g7 = wave_sum_lane63(g7);
-                g8 = wave_sum_lane63(g8);
-                if (lane == 63) {
-                    sg[0] = g0; sg[1] = g1; sg[2] = g2; sg[3] = g3; sg[4] = g4;
-                    sg[5] = g5; sg[6] = g6; sg[7] = g7; sg[8] = g8;
-                }
-            } else if (lane == 63) {
-#pragma unroll
-                for (int c = 0; c < NGRAD; c++) sg[c] = 0.f;
-            }
+            float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+            if (__ballot(any) != 0ull) wave_sum9(g0, g1, g2, g3, g4, g5, g6, g7, g8, t0, t1, t2);
+            red9_store(sg, lane, t0, t1, t2);
         }
         __syncthreads();
         // one atomic per (pair, component); consecutive lanes hit consecutive components of a pair
