@@ -206,16 +206,23 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 // a + b after v_permlane32_swap(a, b): lanes 0-31 get a_lo + a_hi, lanes 32-63 get b_lo + b_hi.
+// NOTE (ROCm 7.2 hipcc): bit-casting the builtin's vector elements directly miscompiles (both
+// results alias the vdst register, see tools/lane_probe.py); going through named unsigned
+// temporaries, as below, generates the intended `v_permlane*_swap v_a, v_b; v_add v_a, v_a, v_b`.
 __device__ __forceinline__ float swap32_add(float a, float b) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
-                                                   false, false);
-    return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+    unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+    const auto r = __builtin_amdgcn_permlane32_swap(ua, ub, false, false);
+    ua = r[0];
+    ub = r[1];
+    return __builtin_bit_cast(float, ua) + __builtin_bit_cast(float, ub);
 }
 // a + b after v_permlane16_swap(a, b): rows (16 lanes) become [a0+a1, b0+b1, a2+a3, b2+b3].
 __device__ __forceinline__ float swap16_add(float a, float b) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
-                                                   false, false);
-    return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+    unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+    const auto r = __builtin_amdgcn_permlane16_swap(ua, ub, false, false);
+    ua = r[0];
+    ub = r[1];
+    return __builtin_bit_cast(float, ua) + __builtin_bit_cast(float, ub);
 }
 
 // Wave64 sums of 9 values in 28 VALU ops (vs 54 for nine independent DPP reductions): two
