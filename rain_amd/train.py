@@ -72,7 +72,7 @@ class StepInfo:
 class Trainer:
     def __init__(self, gaussians: GaussianModel, cameras, gt_images, opt: OptimizationParams | None = None,
                  pipe: PipelineParams | None = None, cfg: TrainConfig | None = None, scene_extent: float = 1.0,
-                 group=None):
+                 group=None, loss_fn=None):
         self.g = gaussians
         self.cams = cameras
         self.gt = gt_images
@@ -81,6 +81,8 @@ class Trainer:
         self.cfg = cfg or TrainConfig()
         self.extent = scene_extent
         self.group = group
+        # loss_fn(image, gt, lambda_dssim) -> scalar; default: the fused HIP L1+SSIM kernels
+        self.loss_fn = loss_fn or (lambda img, gt, lam: fused_l1_ssim_loss(img, gt, lam)[0])
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
         self.sampler = ViewSampler(len(cameras), self.world, self.cfg.seed)
@@ -118,8 +120,8 @@ class Trainer:
         pkg = render(cam, g, self.pipe, self.background, low_pass=self.low_pass)
         image, vsp, vis, radii = pkg["render"], pkg["viewspace_points"], pkg["visibility_filter"], pkg["radii"]
         gt = self.gt[vidx]
-        # (1-λ)·L1 + λ·(1-SSIM) (train.py:113-114) as one fused HIP forward/backward
-        loss, _parts = fused_l1_ssim_loss(image, gt, opt.lambda_dssim)
+        # (1-λ)·L1 + λ·(1-SSIM) (train.py:113-114), by default one fused HIP forward/backward
+        loss = self.loss_fn(image, gt, opt.lambda_dssim)
         loss.backward()
 
         densified = False

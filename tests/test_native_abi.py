@@ -1,0 +1,106 @@
+"""CPU checks of the drop-in boundary: the C-ABI libraries load, export every symbol their headers
+declare, size queries behave, argument validation mirrors the reference's errors, and the product
+path refuses CPU tensors (there is no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from rain_amd import _native as N
+from rain_amd.diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, _C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|size_t|char\s*\*|char)\s*\*?\s*(r[rl]_\w+)\s*\(", src,
+                                 flags=re.M)))
+
+
+@pytest.mark.parametrize("header,lib,listed", [("rain_raster.h", N.RASTER_LIB, N.RASTER_SYMBOLS),
+                                               ("rain_loss.h", N.LOSS_LIB, N.LOSS_SYMBOLS)])
+def test_library_exports_every_declared_symbol(header, lib, listed):
+    names = _declared(header)
+    assert names, header
+    so = ctypes.CDLL(lib)
+    for n in names:
+        assert hasattr(so, n), f"{os.path.basename(lib)} does not export {n}"
+    assert sorted(listed) == names
+
+
+def test_size_queries():
+    L = N.raster()
+    assert L.rr_geometry_bytes(0) > 0
+    assert L.rr_geometry_bytes(1000) < L.rr_geometry_bytes(100000) < L.rr_geometry_bytes(1000000)
+    assert L.rr_image_bytes(1920, 1080) >= 1920 * 1080 * 8
+    assert L.rr_binning_bytes(1000, 256, 256) < L.rr_binning_bytes(10_000_000, 1920, 1080)
+    assert L.rr_backward_workspace_bytes(1000) >= 1000 * 64
+    assert N.loss_lib().rl_workspace_bytes(3, 1080, 1920) >= 3 * 3 * 1080 * 1920 * 4
+    assert L.rr_version().decode().startswith("rain_amd")
+
+
+def test_validation_errors_without_gpu():
+    L = N.raster()
+    f = N.RRFrame(10, 3, 16, 64, 48, 0.5, 0.4, 1.0, 0.3, 0, 0)
+    cam = N.RRCamera(None, None, None, None)
+    g = N.RRGaussians(None, None, None, None, None, None, None)
+    nr = ctypes.c_int(-1)
+    rc = L.rr_forward_geometry(ctypes.byref(f), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
+                               ctypes.byref(nr), None)
+    assert rc == 1 and b"required" in L.rr_last_error()
+    # both SH and colours given -> the reference's message
+    g = N.RRGaussians(1, 1, 1, 1, 1, 1, None)
+    cam = N.RRCamera(1, 1, 1, 1)
+    rc = L.rr_forward_geometry(ctypes.byref(f), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
+                               ctypes.byref(nr), None)
+    assert rc == 1 and b"exactly one of either SHs" in L.rr_last_error().replace(b"excatly", b"exactly")
+    assert L.rr_set_blend_config(3, 1) == 1
+    assert L.rr_set_blend_config(0, 0) == 0
+    # P == 0 is a no-op success (rasterize_points.cu:72)
+    f0 = N.RRFrame(0, 0, 0, 64, 48, 0.5, 0.4, 1.0, 0.3, 0, 0)
+    assert L.rr_forward_geometry(ctypes.byref(f0), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
+                                 ctypes.byref(nr), None) == 0 and nr.value == 0
+
+
+def _settings(device="cpu"):
+    return GaussianRasterizationSettings(
+        image_height=48, image_width=64, tanfovx=0.5, tanfovy=0.4, bg=torch.zeros(3, device=device),
+        scale_modifier=1.0, viewmatrix=torch.eye(4, device=device), projmatrix=torch.eye(4, device=device),
+        sh_degree=0, campos=torch.zeros(3, device=device), prefiltered=False, debug=False, low_pass=0.3)
+
+
+def test_python_surface_validation_messages():
+    r = GaussianRasterizer(_settings())
+    m = torch.zeros(5, 3)
+    with pytest.raises(Exception, match="excatly one of either SHs or precomputed colors"):
+        r(means3D=m, means2D=m, opacities=torch.zeros(5, 1), scales=m, rotations=torch.zeros(5, 4))
+    with pytest.raises(Exception, match="exactly one of either scale/rotation pair or precomputed 3D covariance"):
+        r(means3D=m, means2D=m, opacities=torch.zeros(5, 1), shs=torch.zeros(5, 1, 3))
+    with pytest.raises(Exception, match="exactly one of either scale/rotation pair"):
+        r(means3D=m, means2D=m, opacities=torch.zeros(5, 1), shs=torch.zeros(5, 1, 3), scales=m,
+          rotations=torch.zeros(5, 4), cov3D_precomp=torch.zeros(5, 6))
+
+
+def test_no_cpu_fallback():
+    s = _settings()
+    e = torch.Tensor([])
+    m = torch.zeros(5, 3)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _C.rasterize_gaussians(s.bg, m, e, torch.zeros(5, 1), m, torch.zeros(5, 4), 1.0, e, s.viewmatrix,
+                               s.projmatrix, 0.5, 0.4, 48, 64, e, 0, s.campos, False, False, 0.3)
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        _C.rasterize_gaussians(s.bg, torch.zeros(5, 2), e, torch.zeros(5, 1), m, torch.zeros(5, 4), 1.0, e,
+                               s.viewmatrix, s.projmatrix, 0.5, 0.4, 48, 64, e, 0, s.campos, False, False, 0.3)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _C.mark_visible(m, s.viewmatrix, s.projmatrix)
+
+
+def test_import_shim_is_the_product():
+    import diff_gaussian_rasterization as shim
+
+    assert shim.GaussianRasterizer is GaussianRasterizer
+    assert shim._C is _C
