@@ -46,7 +46,15 @@ typedef struct rr_frame {
     float low_pass;     /* RAIN-GS 2D dilation (forward.cu:99-100); 0.3 in vanilla 3DGS */
     int prefiltered;
     int debug;          /* sync + check after every launch (auxiliary.h:155-162) */
+    int flags;          /* RR_FLAG_* (0 = defaults) */
 } rr_frame;
+
+/* Exact tile culling (default ON): (tile, Gaussian) pairs whose Gaussian provably reaches no
+ * pixel of the tile with alpha >= 1/255 are not emitted.  Every pixel of such a tile skips the pair
+ * in the reference too (forward.cu:329-338, backward.cu:485-491), so images, depth, radii and
+ * gradients are unchanged; only the internal pair list is shorter.  The flag restores the
+ * reference's full bounding-square binning (used by the pair-order parity test). */
+#define RR_FLAG_NO_TILE_CULLING 1
 
 /* Camera / per-frame device arrays (reference args of the same names). */
 typedef struct rr_camera {
@@ -78,21 +86,24 @@ size_t rr_backward_workspace_bytes(int P);
 /*
  * Forward, stage 1 (replaces Rasterizer::forward rasterizer_impl.cu:213-277):
  * preprocess every Gaussian, stable-sort visible Gaussians by depth, prefix-sum their tile
- * counts, and read back the pair count L (the one device->host sync the reference also has,
- * rasterizer_impl.cu:273).  Writes radii[P] (int32) and *num_rendered.
+ * counts, and read back the pair counts (the one device->host sync the reference also has,
+ * rasterizer_impl.cu:273).  Writes radii[P] (int32), *num_rendered = the reference's value (sum
+ * of bounding-square tile counts, returned to Python unchanged) and *num_pairs = the pairs that
+ * will actually be binned (after exact tile culling; size the binning buffer with it).
  */
 int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii,
                         void* geom_buffer, size_t geom_bytes, void* image_buffer, size_t image_bytes,
-                        int* num_rendered, void* stream);
+                        int* num_rendered, int* num_pairs, void* stream);
 
 /*
  * Forward, stage 2 (replaces rasterizer_impl.cu:279-329): expand (tile, Gaussian) pairs in
  * depth order, stable-sort them by tile, find per-tile ranges and alpha-blend every tile.
- * out_color [3,H,W], out_depth [1,H,W] are fully written.
+ * out_color [3,H,W], out_depth [1,H,W] are fully written.  `f` must carry the same flags as in
+ * stage 1.
  */
 int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                       void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
-                      int num_rendered, float* out_color, float* out_depth, void* stream);
+                      int num_pairs, float* out_color, float* out_depth, void* stream);
 
 /* Gradient outputs of _C.rasterize_gaussians_backward (rasterize_points.cu:145-153,190).
  * All arrays are fully written (no pre-zeroing needed). */
@@ -126,10 +137,11 @@ const char* rr_version(void);
 
 /* Per-stage frame statistics of the last forward on this thread (L, visible count, L_eff...). */
 typedef struct rr_frame_stats {
-    int64_t num_rendered;  /* L */
+    int64_t num_rendered;  /* L: the reference's pair count (bounding-square tiles) */
     int64_t num_visible;   /* V */
     int64_t l_eff;         /* sum over tiles of max n_contrib (needs rr_read_frame_stats) */
     int64_t tiles;         /* T */
+    int64_t num_pairs;     /* pairs actually binned (after exact tile culling) */
 } rr_frame_stats;
 int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* image_buffer, rr_frame_stats* out,
                         void* stream);

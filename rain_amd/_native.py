@@ -25,7 +25,10 @@ class RRFrame(ctypes.Structure):
     _fields_ = [("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int), ("width", ctypes.c_int),
                 ("height", ctypes.c_int), ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float),
                 ("scale_modifier", ctypes.c_float), ("low_pass", ctypes.c_float), ("prefiltered", ctypes.c_int),
-                ("debug", ctypes.c_int)]
+                ("debug", ctypes.c_int), ("flags", ctypes.c_int)]
+
+
+RR_FLAG_NO_TILE_CULLING = 1
 
 
 class RRCamera(ctypes.Structure):
@@ -46,7 +49,7 @@ class RRGrads(ctypes.Structure):
 
 class RRFrameStats(ctypes.Structure):
     _fields_ = [("num_rendered", ctypes.c_int64), ("num_visible", ctypes.c_int64), ("l_eff", ctypes.c_int64),
-                ("tiles", ctypes.c_int64)]
+                ("tiles", ctypes.c_int64), ("num_pairs", ctypes.c_int64)]
 
 
 class RRDebugViews(ctypes.Structure):
@@ -87,7 +90,7 @@ def raster():
         L.rr_binning_bytes.argtypes = [ci, ci, ci]
         fp, cp, gp = ctypes.POINTER(RRFrame), ctypes.POINTER(RRCamera), ctypes.POINTER(RRGaussians)
         L.rr_forward_geometry.restype = ci
-        L.rr_forward_geometry.argtypes = [fp, cp, gp, vp, vp, sz, vp, sz, ctypes.POINTER(ci), vp]
+        L.rr_forward_geometry.argtypes = [fp, cp, gp, vp, vp, sz, vp, sz, ctypes.POINTER(ci), ctypes.POINTER(ci), vp]
         L.rr_forward_render.restype = ci
         L.rr_forward_render.argtypes = [fp, cp, gp, vp, vp, vp, vp, sz, ci, vp, vp, vp]
         L.rr_backward.restype = ci

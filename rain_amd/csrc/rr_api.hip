@@ -95,7 +95,7 @@ struct Geom {
     uint32_t* idx_sorted;
     uint32_t* tiles_sorted;
     uint32_t* offsets;
-    uint32_t* counters;  // [0] visible count
+    unsigned long long* counters;  // [0] visible count, [1] sum of rect areas (reference num_rendered)
     void* temp;
     size_t temp_bytes;
     size_t total;
@@ -111,7 +111,7 @@ Geom carve_geom(void* buf, int P) {
     g.idx_sorted = c.take<uint32_t>(n);
     g.tiles_sorted = c.take<uint32_t>(n);
     g.offsets = c.take<uint32_t>(n);
-    g.counters = c.take<uint32_t>(4);
+    g.counters = c.take<unsigned long long>(4);
     g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
@@ -139,10 +139,10 @@ Img carve_img(void* buf, int W, int H) {
 }
 
 struct Bin {
+    uint32_t* point_list;  // FIRST, so the backward finds it without knowing the pair count
     void* keys;
     void* keys_sorted;
     uint32_t* vals;
-    uint32_t* point_list;
     void* temp;
     size_t temp_bytes;
     bool wide;  // 32-bit tile keys (T > 65536)
@@ -156,6 +156,7 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     b.wide = T > 65536;
     b.bits = (int)higher_msb((uint32_t)T);
     const size_t n = (size_t)std::max(L, 1);
+    b.point_list = c.take<uint32_t>(n);
     if (b.wide) {
         b.keys = c.take<uint32_t>(n);
         b.keys_sorted = c.take<uint32_t>(n);
@@ -164,7 +165,6 @@ Bin carve_bin(void* buf, int L, int W, int H) {
         b.keys_sorted = c.take<uint16_t>(n);
     }
     b.vals = c.take<uint32_t>(n);
-    b.point_list = c.take<uint32_t>(n);
     b.temp_bytes = b.wide ? tile_sort_temp<uint32_t>(L, b.bits) : tile_sort_temp<uint16_t>(L, b.bits);
     b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
     b.total = align_up(c.off);
@@ -266,11 +266,13 @@ size_t rr_binning_bytes(int num_rendered, int width, int height) {
 size_t rr_backward_workspace_bytes(int P) { return align_up((size_t)std::max(P, 1) * GACC_STRIDE * sizeof(float)); }
 
 int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii, void* geom_buffer,
-                        size_t geom_bytes, void* image_buffer, size_t image_bytes, int* num_rendered, void* stream) {
+                        size_t geom_bytes, void* image_buffer, size_t image_bytes, int* num_rendered,
+                        int* num_pairs, void* stream) {
     int rc = validate(f, cam, g, true);
     if (rc) return rc;
-    if (!num_rendered) return fail(RR_ERR_ARG, "num_rendered is null");
+    if (!num_rendered || !num_pairs) return fail(RR_ERR_ARG, "num_rendered / num_pairs is null");
     *num_rendered = 0;
+    *num_pairs = 0;
     const int P = f->P, W = f->width, H = f->height;
     if (P == 0) return RR_OK;
     if (!radii || !geom_buffer || !image_buffer) return fail(RR_ERR_ARG, "null output buffer");
@@ -290,9 +292,11 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     a.scales = g->scales; a.rotations = g->rotations; a.cov3D_precomp = g->cov3D_precomp;
     a.view = cam->viewmatrix; a.proj = cam->projmatrix; a.campos = cam->campos;
     a.radii = radii; a.splats = gm.splats; a.tiles = gm.tiles; a.depth_keys = gm.depth_keys;
-    a.num_visible = gm.counters;
+    a.num_visible = reinterpret_cast<uint32_t*>(gm.counters);
+    a.rect_pairs = gm.counters + 1;
+    a.cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
 
-    RR_CHECK(hipMemsetAsync(gm.counters, 0, 4 * sizeof(uint32_t), st), "memset counters");
+    RR_CHECK(hipMemsetAsync(gm.counters, 0, 4 * sizeof(unsigned long long), st), "memset counters");
     {
         StageTimer tm(RR_STAGE_PREPROCESS, st);
         launch_preprocess(a, st);
@@ -316,20 +320,26 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
                  "tile-count scan");
     }
     RR_STAGE_CHECK("scan");
+    // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
+    // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
     uint32_t L = 0;
+    unsigned long long Lref = 0;
     RR_CHECK(hipMemcpyAsync(&L, gm.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, st), "read L");
+    RR_CHECK(hipMemcpyAsync(&Lref, gm.counters + 1, sizeof(Lref), hipMemcpyDeviceToHost, st), "read L");
     RR_CHECK(hipStreamSynchronize(st), "sync L");
-    if (L > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^31 tile/Gaussian pairs");
-    *num_rendered = (int)L;
+    if (L > 0x7fffffffu || Lref > 0x7fffffffull) return fail(RR_ERR_CAPACITY, "more than 2^31 tile/Gaussian pairs");
+    *num_rendered = (int)Lref;
+    *num_pairs = (int)L;
     return RR_OK;
 }
 
 int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                       void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
-                      int num_rendered, float* out_color, float* out_depth, void* stream) {
+                      int num_pairs, float* out_color, float* out_depth, void* stream) {
     int rc = validate(f, cam, g, true);
     if (rc) return rc;
-    const int P = f->P, W = f->width, H = f->height, L = num_rendered;
+    const int P = f->P, W = f->width, H = f->height, L = num_pairs;
+    const int cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
     if (P == 0) return RR_OK;
     if (!out_color || !out_depth || !geom_buffer || !image_buffer || (L > 0 && !binning_buffer))
         return fail(RR_ERR_ARG, "null buffer");
@@ -344,10 +354,10 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
             if (bn.wide)
-                launch_duplicate<uint32_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy,
+                launch_duplicate<uint32_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull,
                                            (uint32_t*)bn.keys, bn.vals, st);
             else
-                launch_duplicate<uint16_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy,
+                launch_duplicate<uint16_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull,
                                            (uint16_t*)bn.keys, bn.vals, st);
         }
         RR_STAGE_CHECK("duplicate");
@@ -404,7 +414,9 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
     if (workspace_bytes < rr_backward_workspace_bytes(P)) return fail(RR_ERR_CAPACITY, "workspace too small");
     const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
     const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
-    const Bin bn = carve_bin(const_cast<void*>(binning_buffer), L, W, H);
+    // point_list sits at the start of the binning buffer, so its position does not depend on the
+    // pair count; tiles whose forward blended nothing (tile_max 0) never read it
+    const Bin bn = carve_bin(const_cast<void*>(binning_buffer), 0, W, H);
     hipStream_t st = (hipStream_t)stream;
     const int gx = grid_x(W), gy = grid_y(H);
     float* gacc = static_cast<float*>(workspace);
@@ -412,7 +424,7 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
         StageTimer tm(RR_STAGE_MEMSET, st);
         RR_CHECK(hipMemsetAsync(gacc, 0, (size_t)P * GACC_STRIDE * sizeof(float), st), "memset accumulators");
     }
-    if (L > 0) {
+    if (L > 0 && binning_buffer) {
         StageTimer tm(RR_STAGE_BLEND_BWD, st);
         BlendBwdArgs b{};
         b.W = W; b.H = H; b.gx = gx; b.gy = gy;
@@ -464,14 +476,16 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
     const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
     hipStream_t st = (hipStream_t)stream;
-    uint32_t vis = 0, L = 0;
+    unsigned long long cnt[2] = {0, 0};
+    uint32_t L = 0;
     std::vector<uint32_t> tm(T);
-    RR_CHECK(hipMemcpyAsync(&vis, gm.counters, 4, hipMemcpyDeviceToHost, st), "stats");
+    RR_CHECK(hipMemcpyAsync(cnt, gm.counters, sizeof(cnt), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(&L, gm.offsets + (P - 1), 4, hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipStreamSynchronize(st), "stats");
-    out->num_visible = vis;
-    out->num_rendered = L;
+    out->num_visible = (int64_t)(cnt[0] & 0xffffffffull);
+    out->num_rendered = (int64_t)cnt[1];
+    out->num_pairs = L;
     int64_t s = 0;
     for (uint32_t v : tm) s += v;
     out->l_eff = s;

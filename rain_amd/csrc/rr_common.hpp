@@ -67,6 +67,45 @@ __device__ __forceinline__ void tile_rect(float px, float py, int r, int gx, int
     y1 = min(gy, max(0, (int)((py + r + TILE_Y - 1) / TILE_Y)));
 }
 
+// ---- exact tile culling ---------------------------------------------------------------
+// The reference emits a (tile, Gaussian) pair for every tile of the 3-sigma bounding square.  A
+// pair whose Gaussian reaches no pixel of the tile with alpha >= 1/255 is skipped by every pixel
+// in both blend kernels (forward.cu:329-338, backward.cu:485-491) and so changes no output.  Such
+// pairs are dropped here with a conservative test: q(d) = d^T conic d is minimised over the
+// continuous rectangle spanned by the tile's pixel centres (a lower bound of the discrete
+// minimum) and compared with 2 ln(255 o) plus a margin that covers fp32 / fast-exp rounding
+// in the blend.  Non positive-definite conics are never culled.
+__device__ __forceinline__ float cull_qmax(float opacity) {
+    // alpha = o*exp(-q/2) >= 1/255  <=>  q <= 2 ln(255 o); +0.02 absolute / +1e-4 relative margin
+    const float t = 2.0f * (logf(255.0f * opacity) + 0.01f);
+    return t + 1e-4f * fabsf(t);
+}
+__device__ __forceinline__ bool tile_may_touch(float mx, float my, float ca, float cb, float cc, float qmax, int tx,
+                                               int ty) {
+    // the count pass (preprocess) and the emit pass (duplicate) must take identical decisions:
+    // no FMA contraction, so both inlined copies round identically
+#pragma clang fp contract(off)
+    if (!(ca > 0.f && cc > 0.f && ca * cc - cb * cb > 0.f)) return true;
+    const float x0 = (float)(tx * TILE_X) - mx, x1 = x0 + (float)(TILE_X - 1);
+    const float y0 = (float)(ty * TILE_Y) - my, y1 = y0 + (float)(TILE_Y - 1);
+    if (x0 <= 0.f && x1 >= 0.f && y0 <= 0.f && y1 >= 0.f) return true;
+    float qmin = 3.0e38f;
+    const float xs[2] = {x0, x1}, ys[2] = {y0, y1};
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const float x = xs[i];
+        const float y = fminf(fmaxf(-cb * x / cc, y0), y1);
+        qmin = fminf(qmin, ca * x * x + 2.f * cb * x * y + cc * y * y);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const float y = ys[i];
+        const float x = fminf(fmaxf(-cb * y / ca, x0), x1);
+        qmin = fminf(qmin, ca * x * x + 2.f * cb * x * y + cc * y * y);
+    }
+    return qmin <= qmax;
+}
+
 // Column-major 4x4 transforms (auxiliary.h:47-86).  Matrices live in device memory and are
 // indexed with wave-uniform offsets, so the compiler keeps them in SGPRs (s_load).
 __device__ __forceinline__ v3 xform_point_4x3(v3 p, const float* m) {

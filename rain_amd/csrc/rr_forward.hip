@@ -85,9 +85,17 @@ __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     s.c = rgb;
     a.splats[idx] = s;
     a.radii[idx] = radius;
-    a.tiles[idx] = (uint32_t)area;
+    uint32_t n = (uint32_t)area;
+    if (a.cull) {
+        const float qmax = cull_qmax(opacity);
+        n = 0;
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) n += tile_may_touch(px, py, cx, cy, cz, qmax, x, y) ? 1u : 0u;
+    }
+    a.tiles[idx] = n;
     a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
     atomicAdd(a.num_visible, 1u);
+    atomicAdd(a.rect_pairs, (unsigned long long)area);
 }
 
 __global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __restrict__ idx_sorted,
@@ -102,7 +110,7 @@ template <typename K>
 __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __restrict__ idx_sorted,
                                                    const uint32_t* __restrict__ offsets,
                                                    const Splat* __restrict__ splats, const int* __restrict__ radii,
-                                                   int gx, int gy, K* __restrict__ keys,
+                                                   int gx, int gy, int cull, K* __restrict__ keys,
                                                    uint32_t* __restrict__ vals) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P) return;
@@ -110,15 +118,29 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     const int r = radii[g];
     if (r <= 0) return;
     uint32_t off = s == 0 ? 0u : offsets[s - 1];
+    const uint32_t end = offsets[s];
+    if (off == end) return;
     const float4 A = splats[g].a;
     int x0, y0, x1, y1;
     tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
-    for (int y = y0; y < y1; y++)
-        for (int x = x0; x < x1; x++) {
-            keys[off] = (K)(y * gx + x);
-            vals[off] = g;
-            off++;
-        }
+    if (cull) {
+        const float4 B = splats[g].b;
+        const float qmax = cull_qmax(B.y);  // identical inputs -> identical decisions to the count pass
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++)
+                if (off < end && tile_may_touch(A.x, A.y, A.z, A.w, B.x, qmax, x, y)) {
+                    keys[off] = (K)(y * gx + x);
+                    vals[off] = g;
+                    off++;
+                }
+    } else {
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) {
+                keys[off] = (K)(y * gx + x);
+                vals[off] = g;
+                off++;
+            }
+    }
 }
 
 template <typename K>
@@ -168,14 +190,14 @@ void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint32_t* tile
 
 template <typename K>
 void launch_duplicate(int P, const uint32_t* idx_sorted, const uint32_t* offsets, const Splat* splats,
-                      const int* radii, int gx, int gy, K* keys, uint32_t* vals, hipStream_t st) {
+                      const int* radii, int gx, int gy, int cull, K* keys, uint32_t* vals, hipStream_t st) {
     if (P == 0) return;
-    k_duplicate<K><<<blocks_for(P), 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, keys, vals);
+    k_duplicate<K><<<blocks_for(P), 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, cull, keys, vals);
 }
 template void launch_duplicate<uint16_t>(int, const uint32_t*, const uint32_t*, const Splat*, const int*, int, int,
-                                         uint16_t*, uint32_t*, hipStream_t);
+                                         int, uint16_t*, uint32_t*, hipStream_t);
 template void launch_duplicate<uint32_t>(int, const uint32_t*, const uint32_t*, const Splat*, const int*, int, int,
-                                         uint32_t*, uint32_t*, hipStream_t);
+                                         int, uint32_t*, uint32_t*, hipStream_t);
 
 template <typename K>
 void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st) {

@@ -19,9 +19,11 @@ struct PreArgs {
     const float* campos;
     int* radii;
     Splat* splats;
-    uint32_t* tiles;
+    uint32_t* tiles;             // pairs this Gaussian emits (culled tile count, or rect area)
     uint32_t* depth_keys;
     uint32_t* num_visible;
+    unsigned long long* rect_pairs;  // sum of rect areas = the reference's num_rendered
+    int cull;                    // exact tile culling on/off
 };
 
 struct BlendFwdArgs {
@@ -77,7 +79,7 @@ void launch_preprocess(const PreArgs& a, hipStream_t st);
 void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint32_t* tiles, uint32_t* out, hipStream_t st);
 template <typename K>
 void launch_duplicate(int P, const uint32_t* idx_sorted, const uint32_t* offsets, const Splat* splats,
-                      const int* radii, int gx, int gy, K* keys, uint32_t* vals, hipStream_t st);
+                      const int* radii, int gx, int gy, int cull, K* keys, uint32_t* vals, hipStream_t st);
 template <typename K>
 void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);

@@ -15,12 +15,17 @@ reference uses the current device and the legacy default stream).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from .. import _native as N
 
 NUM_CHANNELS = 3
+
+# Exact tile culling (include/rain_raster.h RR_FLAG_NO_TILE_CULLING): identical outputs, fewer
+# (tile, Gaussian) pairs.  RAIN_TILE_CULLING=0 restores the reference's bounding-square binning.
+TILE_CULLING = os.environ.get("RAIN_TILE_CULLING", "1") != "0"
 
 
 def _ptr(t):
@@ -47,8 +52,9 @@ def _require_device(means3D):
 
 
 def _frame(P, degree, M, W, H, tan_fovx, tan_fovy, scale_modifier, low_pass, prefiltered, debug):
+    flags = 0 if TILE_CULLING else N.RR_FLAG_NO_TILE_CULLING
     return N.RRFrame(int(P), int(degree), int(M), int(W), int(H), float(tan_fovx), float(tan_fovy),
-                     float(scale_modifier), float(low_pass), int(bool(prefiltered)), int(bool(debug)))
+                     float(scale_modifier), float(low_pass), int(bool(prefiltered)), int(bool(debug)), flags)
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
@@ -85,15 +91,18 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     img = torch.empty((L.rr_image_bytes(W, H),), **u8)
     stream = N.stream_of(means3D)
     nr = ctypes.c_int(0)
+    npairs = ctypes.c_int(0)
     N.check(L.rr_forward_geometry(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _ptr(radii),
-                                  _ptr(geom), geom.numel(), _ptr(img), img.numel(), ctypes.byref(nr), stream),
+                                  _ptr(geom), geom.numel(), _ptr(img), img.numel(), ctypes.byref(nr),
+                                  ctypes.byref(npairs), stream),
             "rasterize_gaussians")
-    num_rendered = nr.value
-    binning = torch.empty((L.rr_binning_bytes(num_rendered, W, H) if num_rendered > 0 else 0,), **u8)
+    num_rendered, num_pairs = nr.value, npairs.value
+    binning = torch.empty((L.rr_binning_bytes(num_pairs, W, H) if num_pairs > 0 else 0,), **u8)
     N.check(L.rr_forward_render(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _ptr(radii), _ptr(geom),
-                                _ptr(img), _ptr(binning), binning.numel(), num_rendered, _ptr(out_color),
+                                _ptr(img), _ptr(binning), binning.numel(), num_pairs, _ptr(out_color),
                                 _ptr(out_depth), stream),
             "rasterize_gaussians")
+    # num_rendered is the reference's value (sum of bounding-square tile counts)
     return num_rendered, out_color, radii, out_depth, geom, binning, img
 
 
@@ -151,9 +160,10 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 
 
 def debug_views(geomBuffer, binningBuffer, imageBuffer, num_rendered, P, W, H):
-    """Copies of the forward's private binning/image state (tests only): point_list [L],
+    """Copies of the forward's private binning/image state (tests only): point_list [num_pairs],
     ranges [T,2], tile_max [T], final_T [H,W], n_contrib [H,W], splats [P,12]."""
     f = _frame(P, 0, 0, W, H, 1.0, 1.0, 1.0, 0.3, False, False)
+    num_rendered = frame_stats(geomBuffer, imageBuffer, P, W, H)["num_pairs"]
     v = N.RRDebugViews()
     N.check(N.raster().rr_debug_get_views(ctypes.byref(f), _ptr(geomBuffer), _ptr(imageBuffer), _ptr(binningBuffer),
                                           int(num_rendered), ctypes.byref(v)), "debug_views")
@@ -187,4 +197,5 @@ def frame_stats(geomBuffer, imageBuffer, P, W, H):
     st = N.RRFrameStats()
     N.check(N.raster().rr_read_frame_stats(ctypes.byref(f), _ptr(geomBuffer), _ptr(imageBuffer), ctypes.byref(st),
                                            N.stream_of(geomBuffer)), "frame_stats")
-    return dict(num_rendered=st.num_rendered, num_visible=st.num_visible, l_eff=st.l_eff, tiles=st.tiles)
+    return dict(num_rendered=st.num_rendered, num_visible=st.num_visible, l_eff=st.l_eff, tiles=st.tiles,
+                num_pairs=st.num_pairs)

@@ -75,11 +75,12 @@ def test_forward_backward_parity(oracle, gpu, case):
     _check_grads(ref, got)
 
 
-def test_pair_order_and_image_state(oracle, gpu):
-    """Per-tile lists must hold the same Gaussians in the same (depth, index) order as the
-    reference's 64-bit-key stable sort; n_contrib / final_T must match."""
+def test_pair_order_and_image_state(oracle, gpu, monkeypatch):
+    """With tile culling off, per-tile lists must hold the same Gaussians in the same
+    (depth, index) order as the reference's 64-bit-key stable sort; n_contrib / final_T match."""
     from rain_amd.diff_gaussian_rasterization import _C
 
+    monkeypatch.setattr(_C, "TILE_CULLING", False)
     inp, st = make_scene(P=3000, W=128, H=96, sh_degree=3)
     ref = oracle_run(oracle, inp, st)
     got = gpu_run(inp, st, gpu)
@@ -101,6 +102,47 @@ def test_pair_order_and_image_state(oracle, gpu):
     pad[:H, :W] = nc
     tmax = pad.reshape(gy, 16, gx, 16).max(axis=(1, 3)).reshape(-1)
     np.testing.assert_array_equal(v["tile_max"].cpu().numpy(), tmax)
+
+
+@pytest.mark.parametrize("low_pass,scale_mult", [(0.3, 1.0), (0.3, 3.0), (50.0, 1.0)])
+def test_tile_culling_drops_only_invisible_pairs(oracle, gpu, low_pass, scale_mult):
+    """With exact tile culling (default) each tile's list is an order-preserving subsequence of the
+    reference's, every dropped pair has alpha < 1/255 (or power > 0) at every pixel of its tile
+    (evaluated exactly like forward.cu:325-338), and the reference's num_rendered is returned."""
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    inp, st = make_scene(P=2500, W=128, H=96, sh_degree=3, low_pass=low_pass, scale_mult=scale_mult)
+    ref = oracle_run(oracle, inp, st)
+    got = gpu_run(inp, st, gpu)
+    assert got["num_rendered"] == ref["num_rendered"]
+    geom, binning, img = got["buffers"]
+    P = inp["means3D"].shape[0]
+    W, H = st["image_width"], st["image_height"]
+    v = _C.debug_views(geom, binning, img, got["num_rendered"], P, W, H)
+    ri = ref["state"].internals()
+    pl, rg = v["point_list"].cpu().numpy().astype(np.int64), v["ranges"].cpu().numpy().astype(np.int64)
+    rpl, rrg = ri["point_list"].astype(np.int64), ri["ranges"].astype(np.int64)
+    assert len(pl) < len(rpl)  # the scene has culled pairs
+    xy, co = ri["xy"], ri["conic_opacity"]
+    gx = (W + 15) // 16
+    for tile in range(rrg.shape[0]):
+        mine = list(pl[rg[tile, 0]:rg[tile, 1]])
+        full = list(rpl[rrg[tile, 0]:rrg[tile, 1]])
+        it = iter(full)
+        assert all(g in it for g in mine), f"tile {tile}: not an ordered subsequence"
+        dropped = np.array(sorted(set(full) - set(mine)), dtype=np.int64)
+        if dropped.size == 0:
+            continue
+        tx, ty = tile % gx, tile // gx
+        px, py = np.meshgrid(np.arange(tx * 16, min(tx * 16 + 16, W), dtype=np.float32),
+                             np.arange(ty * 16, min(ty * 16 + 16, H), dtype=np.float32))
+        dx = xy[dropped, 0][:, None, None] - px[None]
+        dy = xy[dropped, 1][:, None, None] - py[None]
+        c = co[dropped]
+        power = (np.float32(-0.5) * (c[:, 0, None, None] * dx * dx + c[:, 2, None, None] * dy * dy)
+                 - c[:, 1, None, None] * dx * dy)
+        alpha = np.minimum(np.float32(0.99), c[:, 3, None, None] * np.exp(power))
+        assert np.all((power > 0) | (alpha < 1.0 / 255.0)), f"tile {tile}: a visible pair was culled"
 
 
 def test_forward_deterministic(gpu):

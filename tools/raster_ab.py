@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="4:1,1:1,2:2,4:4")
+    ap.add_argument("--configs", default="4:1:1,4:1:0", help="fwd_waves:bwd_waves[:tile_culling]")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--views", type=int, default=4)
     ap.add_argument("--points", type=int, default=1_000_000)
@@ -37,12 +37,15 @@ def main():
     act = synthetic.activated(params)
     cams = [c.to(dev) for c in fibonacci_cameras(200, args.width, args.height)][:args.views]
     L = _native.raster()
-    cfgs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    cfgs = [tuple(int(x) for x in (c.split(":") + ["1"])[:3]) for c in args.configs.split(",")]
     times = {c: {} for c in cfgs}
     outs = {}
     for r in range(args.rounds):
         for c in cfgs:
             L.rr_set_blend_config(c[0], c[1])
+            _C.TILE_CULLING = bool(c[2])
             L.rr_profile_enable(1)
             _native.Profiler.collect()
             for vi, cam in enumerate(cams):
@@ -69,7 +72,7 @@ def main():
         o = outs[c]
         same_img = bool(torch.equal(o[0], base[0]))
         rel = lambda a, b: float((a - b).abs().sum() / b.abs().sum().clamp_min(1e-30))  # noqa: E731
-        res[f"{c[0]}:{c[1]}"] = {"stages_ms": {k: round(statistics.median(v), 4) for k, v in times[c].items()},
+        res[f"{c[0]}:{c[1]}:{c[2]}"] = {"stages_ms": {k: round(statistics.median(v), 4) for k, v in times[c].items()},
                                  "image_bitwise_equal": same_img, "dmeans3D_relL1": rel(o[1], base[1]),
                                  "dsh_relL1": rel(o[2], base[2])}
     print(json.dumps(res, indent=1))
