@@ -17,10 +17,17 @@
 
 namespace rr {
 
+// Wave-aggregated 64-bit counter add (one atomic per wave instead of one per lane).
+__device__ __forceinline__ void wave_add_u64(unsigned long long* p, unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (__lane_id() == 0 && v) atomicAdd(p, v);
+}
+
+// Returns the Gaussian's bounding-rect tile count (0 if culled) — the reference's contribution to
+// num_rendered (rasterizer_impl.cu:269-273).
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
+__device__ __forceinline__ unsigned long long preprocess_one(const PreArgs& a, int idx) {
     a.radii[idx] = 0;
     a.tiles[idx] = 0;
     a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
@@ -30,7 +37,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     const v3 p_view = xform_point_4x3(p, a.view);
     if (p_view.z <= 0.2f) {
         if (a.prefiltered) __builtin_trap();
-        return;
+        return 0;
     }
     const float4 p_hom = xform_point_4x4(p, a.proj);
     const float p_w = 1.0f / (p_hom.w + 0.0000001f);
@@ -52,7 +59,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     cc += a.low_pass;
 
     const float det = ca * cc - cb * cb;
-    if (det == 0.0f) return;
+    if (det == 0.0f) return 0;
     const float det_inv = 1.f / det;
     const float cx = cc * det_inv, cy = -cb * det_inv, cz = ca * det_inv;
     const float mid = 0.5f * (ca + cc);
@@ -64,7 +71,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     int x0, y0, x1, y1;
     tile_rect(px, py, radius, a.gx, a.gy, x0, y0, x1, y1);
     const int area = (x1 - x0) * (y1 - y0);
-    if (area == 0) return;
+    if (area == 0) return 0;
 
     float4 rgb;
     if (a.colors_precomp) {
@@ -95,7 +102,15 @@ __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     a.tiles[idx] = n;
     a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
     atomicAdd(a.num_visible, 1u);
-    atomicAdd(a.rect_pairs, (unsigned long long)area);
+    return (unsigned long long)area;
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long rect_area = 0;
+    if (idx < a.P) rect_area = preprocess_one<DEG>(a, idx);
+    wave_add_u64(a.rect_pairs, rect_area);  // all lanes of the wave take part
 }
 
 __global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __restrict__ idx_sorted,

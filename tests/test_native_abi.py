@@ -50,20 +50,20 @@ def test_validation_errors_without_gpu():
     g = N.RRGaussians(None, None, None, None, None, None, None)
     nr = ctypes.c_int(-1)
     rc = L.rr_forward_geometry(ctypes.byref(f), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
-                               ctypes.byref(nr), None)
+                               ctypes.byref(nr), ctypes.byref(nr), None)
     assert rc == 1 and b"required" in L.rr_last_error()
     # both SH and colours given -> the reference's message
     g = N.RRGaussians(1, 1, 1, 1, 1, 1, None)
     cam = N.RRCamera(1, 1, 1, 1)
     rc = L.rr_forward_geometry(ctypes.byref(f), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
-                               ctypes.byref(nr), None)
+                               ctypes.byref(nr), ctypes.byref(nr), None)
     assert rc == 1 and b"exactly one of either SHs" in L.rr_last_error().replace(b"excatly", b"exactly")
     assert L.rr_set_blend_config(3, 1) == 1
     assert L.rr_set_blend_config(0, 0) == 0
     # P == 0 is a no-op success (rasterize_points.cu:72)
     f0 = N.RRFrame(0, 0, 0, 64, 48, 0.5, 0.4, 1.0, 0.3, 0, 0)
     assert L.rr_forward_geometry(ctypes.byref(f0), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
-                                 ctypes.byref(nr), None) == 0 and nr.value == 0
+                                 ctypes.byref(nr), ctypes.byref(nr), None) == 0 and nr.value == 0
 
 
 def _settings(device="cpu"):
