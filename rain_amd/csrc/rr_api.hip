@@ -70,11 +70,19 @@ size_t depth_sort_temp(int P) {
                                         32, (hipStream_t)0);
     return bytes;
 }
+// Component-wise saturating sum of {pairs, rect area}: associative on non-negative counts, and a
+// saturated total (>= 2^32) is caught by the 2^31 capacity check instead of wrapping silently.
+struct SatAdd2 {
+    __host__ __device__ uint2 operator()(const uint2& a, const uint2& b) const {
+        const uint32_t x = a.x + b.x, y = a.y + b.y;
+        return make_uint2(x < a.x ? 0xffffffffu : x, y < a.y ? 0xffffffffu : y);
+    }
+};
 size_t scan_temp(int P) {
     size_t bytes = 0;
     if (P > 0)
-        (void)rocprim::inclusive_scan(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)P,
-                                      rocprim::plus<uint32_t>(), (hipStream_t)0);
+        (void)rocprim::inclusive_scan(nullptr, bytes, (const uint2*)nullptr, (uint2*)nullptr, (size_t)P, SatAdd2(),
+                                      (hipStream_t)0);
     return bytes;
 }
 template <typename K>
@@ -89,13 +97,12 @@ size_t tile_sort_temp(int L, int bits) {
 // ---- scratch layouts ----
 struct Geom {
     Splat* splats;
-    uint32_t* tiles;
+    uint2* tiles;         // per Gaussian {pairs emitted, bounding-rect tiles}
     uint32_t* depth_keys;
     uint32_t* depth_keys_sorted;
     uint32_t* idx_sorted;
-    uint32_t* tiles_sorted;
-    uint32_t* offsets;
-    unsigned long long* counters;  // [0] visible count, [1] sum of rect areas (reference num_rendered)
+    uint2* tiles_sorted;  // tiles[] in depth order
+    uint2* offsets;       // inclusive prefix sum of tiles_sorted; .y of the last = reference num_rendered
     void* temp;
     size_t temp_bytes;
     size_t total;
@@ -105,13 +112,12 @@ Geom carve_geom(void* buf, int P) {
     Geom g;
     const size_t n = (size_t)std::max(P, 1);
     g.splats = c.take<Splat>(n);
-    g.tiles = c.take<uint32_t>(n);
+    g.tiles = c.take<uint2>(n);
     g.depth_keys = c.take<uint32_t>(n);
     g.depth_keys_sorted = c.take<uint32_t>(n);
     g.idx_sorted = c.take<uint32_t>(n);
-    g.tiles_sorted = c.take<uint32_t>(n);
-    g.offsets = c.take<uint32_t>(n);
-    g.counters = c.take<unsigned long long>(4);
+    g.tiles_sorted = c.take<uint2>(n);
+    g.offsets = c.take<uint2>(n);
     g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
@@ -292,11 +298,8 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     a.scales = g->scales; a.rotations = g->rotations; a.cov3D_precomp = g->cov3D_precomp;
     a.view = cam->viewmatrix; a.proj = cam->projmatrix; a.campos = cam->campos;
     a.radii = radii; a.splats = gm.splats; a.tiles = gm.tiles; a.depth_keys = gm.depth_keys;
-    a.num_visible = reinterpret_cast<uint32_t*>(gm.counters);
-    a.rect_pairs = gm.counters + 1;
     a.cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
 
-    RR_CHECK(hipMemsetAsync(gm.counters, 0, 4 * sizeof(unsigned long long), st), "memset counters");
     {
         StageTimer tm(RR_STAGE_PREPROCESS, st);
         launch_preprocess(a, st);
@@ -316,20 +319,18 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
         launch_gather_tiles(P, gm.idx_sorted, gm.tiles, gm.tiles_sorted, st);
         size_t tb = gm.temp_bytes;
         RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, gm.tiles_sorted, gm.offsets, (size_t)P,
-                                         rocprim::plus<uint32_t>(), st),
+                                         SatAdd2(), st),
                  "tile-count scan");
     }
     RR_STAGE_CHECK("scan");
     // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
     // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
-    uint32_t L = 0;
-    unsigned long long Lref = 0;
-    RR_CHECK(hipMemcpyAsync(&L, gm.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, st), "read L");
-    RR_CHECK(hipMemcpyAsync(&Lref, gm.counters + 1, sizeof(Lref), hipMemcpyDeviceToHost, st), "read L");
+    uint2 tot = make_uint2(0u, 0u);
+    RR_CHECK(hipMemcpyAsync(&tot, gm.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, st), "read L");
     RR_CHECK(hipStreamSynchronize(st), "sync L");
-    if (L > 0x7fffffffu || Lref > 0x7fffffffull) return fail(RR_ERR_CAPACITY, "more than 2^31 tile/Gaussian pairs");
-    *num_rendered = (int)Lref;
-    *num_pairs = (int)L;
+    if (tot.x > 0x7fffffffu || tot.y > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^31 tile/Gaussian pairs");
+    *num_rendered = (int)tot.y;
+    *num_pairs = (int)tot.x;
     return RR_OK;
 }
 
@@ -476,16 +477,18 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
     const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
     hipStream_t st = (hipStream_t)stream;
-    unsigned long long cnt[2] = {0, 0};
-    uint32_t L = 0;
+    uint2 tot = make_uint2(0u, 0u);
     std::vector<uint32_t> tm(T);
-    RR_CHECK(hipMemcpyAsync(cnt, gm.counters, sizeof(cnt), hipMemcpyDeviceToHost, st), "stats");
-    RR_CHECK(hipMemcpyAsync(&L, gm.offsets + (P - 1), 4, hipMemcpyDeviceToHost, st), "stats");
+    std::vector<uint2> per((size_t)P);
+    RR_CHECK(hipMemcpyAsync(&tot, gm.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
+    RR_CHECK(hipMemcpyAsync(per.data(), gm.tiles, (size_t)P * sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipStreamSynchronize(st), "stats");
-    out->num_visible = (int64_t)(cnt[0] & 0xffffffffull);
-    out->num_rendered = (int64_t)cnt[1];
-    out->num_pairs = L;
+    int64_t vis = 0;
+    for (const uint2& v : per) vis += v.y > 0;  // a Gaussian is visible iff its rect is non-empty (radii > 0)
+    out->num_visible = vis;
+    out->num_rendered = tot.y;
+    out->num_pairs = tot.x;
     int64_t s = 0;
     for (uint32_t v : tm) s += v;
     out->l_eff = s;

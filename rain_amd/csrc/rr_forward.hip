@@ -17,19 +17,12 @@
 
 namespace rr {
 
-// Wave-aggregated 64-bit counter add (one atomic per wave instead of one per lane).
-__device__ __forceinline__ void wave_add_u64(unsigned long long* p, unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (__lane_id() == 0 && v) atomicAdd(p, v);
-}
-
-// Returns the Gaussian's bounding-rect tile count (0 if culled) — the reference's contribution to
-// num_rendered (rasterizer_impl.cu:269-273).
+// No global atomics here: per-Gaussian counts go to tiles[idx] = {pairs, rect area} and are
+// prefix-summed in depth order (the rect-area sum is the reference's num_rendered).
 template <int DEG>
-__device__ __forceinline__ unsigned long long preprocess_one(const PreArgs& a, int idx) {
+__device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     a.radii[idx] = 0;
-    a.tiles[idx] = 0;
+    a.tiles[idx] = make_uint2(0u, 0u);
     a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
 
     const v3 p = load3(a.means3D + 3 * (size_t)idx);
@@ -37,7 +30,7 @@ __device__ __forceinline__ unsigned long long preprocess_one(const PreArgs& a, i
     const v3 p_view = xform_point_4x3(p, a.view);
     if (p_view.z <= 0.2f) {
         if (a.prefiltered) __builtin_trap();
-        return 0;
+        return;
     }
     const float4 p_hom = xform_point_4x4(p, a.proj);
     const float p_w = 1.0f / (p_hom.w + 0.0000001f);
@@ -59,7 +52,7 @@ __device__ __forceinline__ unsigned long long preprocess_one(const PreArgs& a, i
     cc += a.low_pass;
 
     const float det = ca * cc - cb * cb;
-    if (det == 0.0f) return 0;
+    if (det == 0.0f) return;
     const float det_inv = 1.f / det;
     const float cx = cc * det_inv, cy = -cb * det_inv, cz = ca * det_inv;
     const float mid = 0.5f * (ca + cc);
@@ -71,7 +64,7 @@ __device__ __forceinline__ unsigned long long preprocess_one(const PreArgs& a, i
     int x0, y0, x1, y1;
     tile_rect(px, py, radius, a.gx, a.gy, x0, y0, x1, y1);
     const int area = (x1 - x0) * (y1 - y0);
-    if (area == 0) return 0;
+    if (area == 0) return;
 
     float4 rgb;
     if (a.colors_precomp) {
@@ -99,23 +92,19 @@ __device__ __forceinline__ unsigned long long preprocess_one(const PreArgs& a, i
         for (int y = y0; y < y1; y++)
             for (int x = x0; x < x1; x++) n += tile_may_touch(px, py, cx, cy, cz, qmax, x, y) ? 1u : 0u;
     }
-    a.tiles[idx] = n;
+    a.tiles[idx] = make_uint2(n, (uint32_t)area);
     a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
-    atomicAdd(a.num_visible, 1u);
-    return (unsigned long long)area;
 }
 
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long rect_area = 0;
-    if (idx < a.P) rect_area = preprocess_one<DEG>(a, idx);
-    wave_add_u64(a.rect_pairs, rect_area);  // all lanes of the wave take part
+    if (idx < a.P) preprocess_one<DEG>(a, idx);
 }
 
 __global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __restrict__ idx_sorted,
-                                                      const uint32_t* __restrict__ tiles,
-                                                      uint32_t* __restrict__ tiles_sorted) {
+                                                      const uint2* __restrict__ tiles,
+                                                      uint2* __restrict__ tiles_sorted) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P) return;
     tiles_sorted[s] = tiles[idx_sorted[s]];
@@ -123,7 +112,7 @@ __global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __r
 
 template <typename K>
 __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __restrict__ idx_sorted,
-                                                   const uint32_t* __restrict__ offsets,
+                                                   const uint2* __restrict__ offsets,
                                                    const Splat* __restrict__ splats, const int* __restrict__ radii,
                                                    int gx, int gy, int cull, K* __restrict__ keys,
                                                    uint32_t* __restrict__ vals) {
@@ -132,8 +121,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     const uint32_t g = idx_sorted[s];
     const int r = radii[g];
     if (r <= 0) return;
-    uint32_t off = s == 0 ? 0u : offsets[s - 1];
-    const uint32_t end = offsets[s];
+    uint32_t off = s == 0 ? 0u : offsets[s - 1].x;
+    const uint32_t end = offsets[s].x;
     if (off == end) return;
     const float4 A = splats[g].a;
     int x0, y0, x1, y1;
@@ -198,20 +187,20 @@ void launch_preprocess(const PreArgs& a, hipStream_t st) {
     }
 }
 
-void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint32_t* tiles, uint32_t* out, hipStream_t st) {
+void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint2* tiles, uint2* out, hipStream_t st) {
     if (P == 0) return;
     k_gather_tiles<<<blocks_for(P), 256, 0, st>>>(P, idx_sorted, tiles, out);
 }
 
 template <typename K>
-void launch_duplicate(int P, const uint32_t* idx_sorted, const uint32_t* offsets, const Splat* splats,
+void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats,
                       const int* radii, int gx, int gy, int cull, K* keys, uint32_t* vals, hipStream_t st) {
     if (P == 0) return;
     k_duplicate<K><<<blocks_for(P), 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, cull, keys, vals);
 }
-template void launch_duplicate<uint16_t>(int, const uint32_t*, const uint32_t*, const Splat*, const int*, int, int,
+template void launch_duplicate<uint16_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int,
                                          int, uint16_t*, uint32_t*, hipStream_t);
-template void launch_duplicate<uint32_t>(int, const uint32_t*, const uint32_t*, const Splat*, const int*, int, int,
+template void launch_duplicate<uint32_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int,
                                          int, uint32_t*, uint32_t*, hipStream_t);
 
 template <typename K>

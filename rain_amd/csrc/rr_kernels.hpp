@@ -19,10 +19,8 @@ struct PreArgs {
     const float* campos;
     int* radii;
     Splat* splats;
-    uint32_t* tiles;             // pairs this Gaussian emits (culled tile count, or rect area)
+    uint2* tiles;                // {pairs this Gaussian emits (after culling), bounding-rect tile count}
     uint32_t* depth_keys;
-    uint32_t* num_visible;
-    unsigned long long* rect_pairs;  // sum of rect areas = the reference's num_rendered
     int cull;                    // exact tile culling on/off
 };
 
@@ -76,9 +74,9 @@ struct GaussBwdArgs {
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);
-void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint32_t* tiles, uint32_t* out, hipStream_t st);
+void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint2* tiles, uint2* out, hipStream_t st);
 template <typename K>
-void launch_duplicate(int P, const uint32_t* idx_sorted, const uint32_t* offsets, const Splat* splats,
+void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats,
                       const int* radii, int gx, int gy, int cull, K* keys, uint32_t* vals, hipStream_t st);
 template <typename K>
 void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st);
