@@ -71,39 +71,63 @@ __device__ __forceinline__ void tile_rect(float px, float py, int r, int gx, int
 // The reference emits a (tile, Gaussian) pair for every tile of the 3-sigma bounding square.  A
 // pair whose Gaussian reaches no pixel of the tile with alpha >= 1/255 is skipped by every pixel
 // in both blend kernels (forward.cu:329-338, backward.cu:485-491) and so changes no output.  Such
-// pairs are dropped here with a conservative test: q(d) = d^T conic d is minimised over the
-// continuous rectangle spanned by the tile's pixel centres (a lower bound of the discrete
-// minimum) and compared with 2 ln(255 o) plus a margin that covers fp32 / fast-exp rounding
+// pairs are dropped here with a conservative test: a tile is kept iff the ellipse
+// {d : d^T conic d <= 2 ln(255 o) + margin} meets the continuous rectangle spanned by the tile's
+// pixel centres (a superset of the discrete pixels); the margin covers fp32 / fast-exp rounding
 // in the blend.  Non positive-definite conics are never culled.
 __device__ __forceinline__ float cull_qmax(float opacity) {
     // alpha = o*exp(-q/2) >= 1/255  <=>  q <= 2 ln(255 o); +0.02 absolute / +1e-4 relative margin
     const float t = 2.0f * (logf(255.0f * opacity) + 0.01f);
     return t + 1e-4f * fabsf(t);
 }
-__device__ __forceinline__ bool tile_may_touch(float mx, float my, float ca, float cb, float cc, float qmax, int tx,
-                                               int ty) {
-    // the count pass (preprocess) and the emit pass (duplicate) must take identical decisions:
-    // no FMA contraction, so both inlined copies round identically
+// Evaluated per tile row, O(rows) instead of O(tiles): the set {q <= qmax} is an
+// ellipse, its intersection with tile row ty's pixel-centre band [y0, y1] is convex, so its
+// x-projection is one interval [xl, xr] and the row's touched tiles are the contiguous columns
+// whose pixel-centre span [16 tx, 16 tx + 15] meets it.  xr over the band is the concave
+// x_right(y) = (-cb y + sqrt(ca qmax - D y^2)) / ca maximised at y clamped to the ellipse's
+// rightmost point y* = -cb xmax / cc (mirror for xl).  Returns the column range [*lo, *hi)
+// clipped to the bounding rect [x0, x1); empty rows give lo >= hi.  Slack of 1e-3 px + 1e-5
+// relative keeps it conservative against rounding (the q margin of cull_qmax covers the blend).
+__device__ __forceinline__ void cull_row_span(float mx, float my, float ca, float cb, float cc, float qmax, int ty,
+                                              int x0, int x1, int* lo, int* hi) {
 #pragma clang fp contract(off)
-    if (!(ca > 0.f && cc > 0.f && ca * cc - cb * cb > 0.f)) return true;
-    const float x0 = (float)(tx * TILE_X) - mx, x1 = x0 + (float)(TILE_X - 1);
-    const float y0 = (float)(ty * TILE_Y) - my, y1 = y0 + (float)(TILE_Y - 1);
-    if (x0 <= 0.f && x1 >= 0.f && y0 <= 0.f && y1 >= 0.f) return true;
-    float qmin = 3.0e38f;
-    const float xs[2] = {x0, x1}, ys[2] = {y0, y1};
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const float x = xs[i];
-        const float y = fminf(fmaxf(-cb * x / cc, y0), y1);
-        qmin = fminf(qmin, ca * x * x + 2.f * cb * x * y + cc * y * y);
+    const float D = ca * cc - cb * cb;
+    if (!(ca > 0.f && cc > 0.f && D > 0.f)) {  // not a proper ellipse: keep the whole rect row
+        *lo = x0;
+        *hi = x1;
+        return;
     }
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const float y = ys[i];
-        const float x = fminf(fmaxf(-cb * y / ca, x0), x1);
-        qmin = fminf(qmin, ca * x * x + 2.f * cb * x * y + cc * y * y);
+    if (!(qmax > 0.f)) {  // opacity below 1/255 everywhere: the blend skips every pixel
+        *lo = x1;
+        *hi = x1;
+        return;
     }
-    return qmin <= qmax;
+    const float yext = sqrtf(ca * qmax / D);
+    const float by0 = (float)(ty * TILE_Y) - my, by1 = by0 + (float)(TILE_Y - 1);
+    const float slack_y = 1e-3f + 1e-5f * yext;
+    const float ya = fmaxf(by0, -yext), yb = fminf(by1, yext);
+    if (ya > yb + slack_y) {
+        *lo = x1;
+        *hi = x1;
+        return;
+    }
+    const float xmax = sqrtf(cc * qmax / D);
+    const float ystar = -cb * xmax / cc;               // rightmost point; leftmost is at -ystar
+    const float yr = fminf(fmaxf(ystar, ya), yb);
+    const float yl = fminf(fmaxf(-ystar, ya), yb);
+    const float xr = (-cb * yr + sqrtf(fmaxf(ca * qmax - D * yr * yr, 0.f))) / ca;
+    const float xl = (-cb * yl - sqrtf(fmaxf(ca * qmax - D * yl * yl, 0.f))) / ca;
+    if (!(xr >= xl) || !(xr - xl < 3.0e38f)) {  // non-finite arithmetic: stay conservative
+        *lo = x0;
+        *hi = x1;
+        return;
+    }
+    const float slack_x = 1e-3f + 1e-5f * xmax;
+    // tile tx is touched iff 16 tx - mx <= xr and 16 tx + 15 - mx >= xl
+    const float vl = (xl - slack_x + mx - (float)(TILE_X - 1)) / (float)TILE_X;
+    const float vh = (xr + slack_x + mx) / (float)TILE_X;
+    *lo = (int)ceilf(fminf(fmaxf(vl, (float)x0), (float)x1));
+    *hi = (int)floorf(fminf(fmaxf(vh, (float)x0 - 1.f), (float)x1 - 1.f)) + 1;
 }
 
 // Column-major 4x4 transforms (auxiliary.h:47-86).  Matrices live in device memory and are

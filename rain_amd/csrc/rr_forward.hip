@@ -89,8 +89,11 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     if (a.cull) {
         const float qmax = cull_qmax(opacity);
         n = 0;
-        for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) n += tile_may_touch(px, py, cx, cy, cz, qmax, x, y) ? 1u : 0u;
+        for (int y = y0; y < y1; y++) {
+            int lo, hi;
+            cull_row_span(px, py, cx, cy, cz, qmax, y, x0, x1, &lo, &hi);
+            n += hi > lo ? (uint32_t)(hi - lo) : 0u;
+        }
     }
     a.tiles[idx] = make_uint2(n, (uint32_t)area);
     a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
@@ -130,13 +133,15 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     if (cull) {
         const float4 B = splats[g].b;
         const float qmax = cull_qmax(B.y);  // identical inputs -> identical decisions to the count pass
-        for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++)
-                if (off < end && tile_may_touch(A.x, A.y, A.z, A.w, B.x, qmax, x, y)) {
-                    keys[off] = (K)(y * gx + x);
-                    vals[off] = g;
-                    off++;
-                }
+        for (int y = y0; y < y1; y++) {
+            int lo, hi;
+            cull_row_span(A.x, A.y, A.z, A.w, B.x, qmax, y, x0, x1, &lo, &hi);
+            for (int x = lo; x < hi && off < end; x++) {
+                keys[off] = (K)(y * gx + x);
+                vals[off] = g;
+                off++;
+            }
+        }
     } else {
         for (int y = y0; y < y1; y++)
             for (int x = x0; x < x1; x++) {
