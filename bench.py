@@ -53,16 +53,19 @@ def parse():
 
 
 def algorithmic_bytes(stage, st, P, W, H, K):
-    """SURVEY §8(d) per-launch algorithmic bytes."""
-    L, V, Le, T, N = st["num_rendered"], st["num_visible"], st["l_eff"], st["tiles"], W * H
+    """SURVEY §8(d) per-launch algorithmic bytes.  L is the number of (tile, Gaussian) pairs this
+    implementation actually bins (num_pairs, after exact tile culling), not the reference's larger
+    num_rendered, so binning stages are not credited for pairs they never touch.  The tile sort is
+    priced at its minimum: read + write each u16 key and u32 value once."""
+    L, V, Le, T, N = st["num_pairs"], st["num_visible"], st["l_eff"], st["tiles"], W * H
     M = K
-    kb = 32 + math.ceil(math.log2(max(T, 2)))
+    kw = 2 if T <= 65536 else 4
     return {
         "preprocess": 20 * P + V * (99 + 12 * K),
         "scan": 8 * P,
-        "duplicate": 4 * P + 16 * V + 12 * L,
-        "tile_sort": 24 * L * math.ceil(kb / 8),
-        "ranges": 8 * L + 16 * T,
+        "duplicate": 4 * P + 16 * V + (kw + 4) * L,
+        "tile_sort": 2 * (kw + 4) * L,
+        "ranges": kw * L + 8 * T,
         "blend_fwd": 8 * T + 44 * Le + 24 * N,
         "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
         "gauss_bwd": 4 * P * (27 + 3 * M) + 4 * P + 88 * V + 4 * P + V * (143 + 24 * K),

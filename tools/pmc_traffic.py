@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Turn two rocprofv3 counter passes (FETCH_SIZE, WRITE_SIZE; separate runs because the TCC slots
+cannot hold both) over tools/pmc_workload.py into profiles/pmc_traffic.json.
+
+HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE, both in KiB as rocprofv3 reports them
+(MI355X_MICROARCH.md, HBM section: on gfx950 FETCH_SIZE reports half the bytes of wide coalesced
+reads; WRITE_SIZE is exact for 16-B stores and dword atomics).  Infinity-Cache hits are counted,
+so this is memory-side fabric traffic, an upper bound of HBM bytes.
+
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [--out profiles/pmc_traffic.json]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+import statistics
+
+STAGES = [  # kernel-name pattern -> bench.py stage name
+    (r"k_blend_bwd", "blend_bwd"),
+    (r"k_blend_fwd", "blend_fwd"),
+    (r"k_preprocess", "preprocess"),
+    (r"k_gauss_bwd", "gauss_bwd"),
+    (r"k_duplicate", "duplicate"),
+    (r"k_ranges", "ranges"),
+    (r"k_gather_tiles", "gather_tiles"),
+]
+
+
+def _stage(name):
+    for pat, st in STAGES:
+        if re.search(pat, name):
+            return st
+    return None
+
+
+def _read(dirname, counter):
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {dirname}")
+    per = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                st = _stage(row.get("Kernel_Name", ""))
+                if st is None:
+                    continue
+                key = (fn, row.get("Dispatch_Id"))
+                per.setdefault(st, {}).setdefault(key, 0.0)
+                per[st][key] += float(row["Counter_Value"])  # summed over XCD / instance rows
+    return {st: list(d.values()) for st, d in per.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    fetch = _read(a.fetch_dir, "FETCH_SIZE")
+    write = _read(a.write_dir, "WRITE_SIZE")
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE over tools/pmc_workload.py "
+                     "(1M Gaussians, SH 3, 1920x1080, fwd+bwd); hbm = 2*FETCH + WRITE (gfx950 correction)",
+           "unit": "bytes per launch (median over launches)", "kernels": {}}
+    for st in sorted(set(fetch) | set(write)):
+        f = statistics.median(fetch[st]) * 1024.0 if st in fetch else None
+        w = statistics.median(write[st]) * 1024.0 if st in write else None
+        out["kernels"][st] = {
+            "launches": len(fetch.get(st, [])),
+            "fetch_bytes_raw": f, "write_bytes": w,
+            "hbm_bytes_per_launch": (2 * f + w) if (f is not None and w is not None) else None,
+        }
+    with open(a.out, "w") as fo:
+        json.dump(out, fo, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
