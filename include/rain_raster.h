@@ -56,6 +56,16 @@ typedef struct rr_frame {
  * reference's full bounding-square binning (used by the pair-order parity test). */
 #define RR_FLAG_NO_TILE_CULLING 1
 
+/* Raw-parameter (training) mode: the Gaussian inputs are GaussianModel's pre-activation
+ * parameters (scene/gaussian_model.py:131-136) and the rasterizer applies the getters itself
+ * (gaussian_model.py:85-105): scales = exp(scales), rotations = rotations / max(|rotations|, 1e-12),
+ * opacities = sigmoid(opacities), SH = cat(shs [P,1,3], shs_rest [P,M-1,3]).  The backward then
+ * writes gradients w.r.t. those raw parameters (chain rule through the getters fused into the
+ * per-Gaussian kernel), splitting dL/dSH into dL_dsh [P,1,3] and dL_dsh_rest [P,M-1,3], and can
+ * fold the densification statistics (train.py:132-134, gaussian_model.py:419-421) into the same
+ * pass.  Requires shs and scales/rotations (no precomputed colours or covariances). */
+#define RR_FLAG_RAW_PARAMS 2
+
 /* Camera / per-frame device arrays (reference args of the same names). */
 typedef struct rr_camera {
     const float* background; /* [3] */
@@ -74,6 +84,7 @@ typedef struct rr_gaussians {
     const float* scales;
     const float* rotations;
     const float* cov3D_precomp;
+    const float* shs_rest;  /* RR_FLAG_RAW_PARAMS only: f_rest [P,M-1,3] (shs is then f_dc [P,1,3]) */
 } rr_gaussians;
 
 /* ---- scratch sizing (replaces GeometryState/ImageState/BinningState::fromChunk,
@@ -116,6 +127,16 @@ typedef struct rr_grads {
     float* dL_dsh;        /* [P,M,3] (may be NULL when M == 0) */
     float* dL_dscales;    /* [P,3] */
     float* dL_drotations; /* [P,4] */
+    /* RR_FLAG_RAW_PARAMS only (all optional; dL_dmeans2D / dL_dcolors / dL_dcov3D may then be NULL):
+     * dL_dsh -> f_dc grad [P,1,3], dL_dsh_rest -> f_rest grad [P,M-1,3]; dL_dopacity, dL_dscales,
+     * dL_drotations are w.r.t. the raw logit / log-scale / unnormalised quaternion.
+     * Densification statistics, updated in place for radii > 0 (gaussian_model.py:419-421,
+     * train.py:133): grad_accum[i] += |dL/dmean2D[i].xy|, denom[i] += 1,
+     * max_radii2D[i] = max(max_radii2D[i], radii[i]). */
+    float* dL_dsh_rest;
+    float* grad_accum;    /* [P] */
+    float* denom;         /* [P] */
+    float* max_radii2D;   /* [P] */
 } rr_grads;
 
 /*

@@ -27,6 +27,7 @@ LIBS = {
     "librain_raster.so": ["rr_forward.hip", "rr_blend.hip", "rr_backward.hip", "rr_api.hip"],
     "librain_loss.so": ["loss.hip"],
     "librain_knn.so": ["knn.hip"],
+    "librain_train.so": ["train.hip"],
 }
 
 

@@ -29,6 +29,7 @@ class RRFrame(ctypes.Structure):
 
 
 RR_FLAG_NO_TILE_CULLING = 1
+RR_FLAG_RAW_PARAMS = 2
 
 
 class RRCamera(ctypes.Structure):
@@ -39,12 +40,13 @@ class RRCamera(ctypes.Structure):
 class RRGaussians(ctypes.Structure):
     _fields_ = [("means3D", ctypes.c_void_p), ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
                 ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p), ("rotations", ctypes.c_void_p),
-                ("cov3D_precomp", ctypes.c_void_p)]
+                ("cov3D_precomp", ctypes.c_void_p), ("shs_rest", ctypes.c_void_p)]
 
 
 class RRGrads(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D",
-                                                "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")]
+                                                "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations",
+                                                "dL_dsh_rest", "grad_accum", "denom", "max_radii2D")]
 
 
 class RRFrameStats(ctypes.Structure):
@@ -134,6 +136,30 @@ def loss_lib():
         L.rl_last_error.restype = ctypes.c_char_p
         _loss = L
     return _loss
+
+
+TRAIN_LIB = os.path.join(LIB_DIR, "librain_train.so")
+TRAIN_SYMBOLS = ["rt_adam_step", "rt_last_error"]
+RT_MAX_GROUPS = 8
+_train = None
+
+
+class RTAdamGroup(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64), ("lr", ctypes.c_double),
+                ("bias_correction1", ctypes.c_float), ("bias_correction2_sqrt", ctypes.c_float)]
+
+
+def train_lib():
+    global _train
+    if _train is None:
+        L = _load(TRAIN_LIB)
+        L.rt_adam_step.restype = ctypes.c_int
+        L.rt_adam_step.argtypes = [ctypes.POINTER(RTAdamGroup), ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                   ctypes.c_double, ctypes.c_void_p]
+        L.rt_last_error.restype = ctypes.c_char_p
+        _train = L
+    return _train
 
 
 def knn():

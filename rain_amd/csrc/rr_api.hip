@@ -254,6 +254,11 @@ int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, boo
                     "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
     if (g->shs && (f->D < 0 || f->D > 3 || f->M < (f->D + 1) * (f->D + 1)))
         return fail(RR_ERR_ARG, "sh_degree must be 0..3 and sh.size(1) >= (degree+1)^2");
+    if (f->flags & RR_FLAG_RAW_PARAMS) {
+        if (!g->shs || !sr || !g->opacities)
+            return fail(RR_ERR_ARG, "raw-parameter mode needs SH, scales/rotations and opacities");
+        if (f->M > 1 && !g->shs_rest) return fail(RR_ERR_ARG, "raw-parameter mode needs shs_rest when M > 1");
+    }
     return RR_OK;
 }
 
@@ -299,6 +304,8 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     a.view = cam->viewmatrix; a.proj = cam->projmatrix; a.campos = cam->campos;
     a.radii = radii; a.splats = gm.splats; a.tiles = gm.tiles; a.depth_keys = gm.depth_keys;
     a.cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
+    a.raw = (f->flags & RR_FLAG_RAW_PARAMS) ? 1 : 0;
+    a.shs_rest = g->shs_rest;
 
     {
         StageTimer tm(RR_STAGE_PREPROCESS, st);
@@ -409,9 +416,14 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
     if (P == 0) return RR_OK;
     if (!out || !dL_dpix || !radii || !geom_buffer || !image_buffer || !workspace)
         return fail(RR_ERR_ARG, "null buffer");
-    if (!out->dL_dmeans2D || !out->dL_dcolors || !out->dL_dopacity || !out->dL_dmeans3D || !out->dL_dcov3D ||
-        !out->dL_dscales || !out->dL_drotations || (f->M > 0 && !out->dL_dsh))
+    const bool raw = (f->flags & RR_FLAG_RAW_PARAMS) != 0;
+    if (!out->dL_dopacity || !out->dL_dmeans3D || !out->dL_dscales || !out->dL_drotations ||
+        (f->M > 0 && !out->dL_dsh) ||
+        (!raw && (!out->dL_dmeans2D || !out->dL_dcolors || !out->dL_dcov3D)) ||
+        (raw && f->M > 1 && !out->dL_dsh_rest))
         return fail(RR_ERR_ARG, "null gradient output");
+    if (out->grad_accum && (!raw || !out->denom || !out->max_radii2D))
+        return fail(RR_ERR_ARG, "densification statistics need raw mode and grad_accum, denom, max_radii2D");
     if (workspace_bytes < rr_backward_workspace_bytes(P)) return fail(RR_ERR_CAPACITY, "workspace too small");
     const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
     const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
@@ -449,6 +461,9 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
         a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
         a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = f->M > 0 ? out->dL_dsh : nullptr;
         a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
+        a.raw = raw ? 1 : 0; a.opacities = g->opacities; a.shs_rest = g->shs_rest;
+        a.dL_dsh_rest = out->dL_dsh_rest;
+        a.grad_accum = out->grad_accum; a.denom = out->denom; a.max_radii2D = out->max_radii2D;
         launch_gauss_bwd(a, st);
     }
     RR_STAGE_CHECK("gaussian backward");

@@ -14,22 +14,23 @@ namespace rr {
 
 // SH backward (backward.cu:9-128): writes dL_dsh[0..K) and returns dL/d(dir) via dRGBd{x,y,z}.
 template <int DEG>
-__device__ __forceinline__ v3 sh_backward(v3 dir, const float* sh, v3 dL_dRGB, float* dsh) {
+__device__ __forceinline__ v3 sh_backward(v3 dir, const float* rest, v3 dL_dRGB, float* dsh_dc, float* dsh_rest) {
     const float x = dir.x, y = dir.y, z = dir.z;
     v3 dRGBdx = mk(0, 0, 0), dRGBdy = mk(0, 0, 0), dRGBdz = mk(0, 0, 0);
     auto W = [&](int k, float s) {
-        dsh[3 * k + 0] = s * dL_dRGB.x;
-        dsh[3 * k + 1] = s * dL_dRGB.y;
-        dsh[3 * k + 2] = s * dL_dRGB.z;
+        float* d = k == 0 ? dsh_dc : dsh_rest + 3 * (k - 1);
+        d[0] = s * dL_dRGB.x;
+        d[1] = s * dL_dRGB.y;
+        d[2] = s * dL_dRGB.z;
     };
     W(0, RR_SH_C0);
     if (DEG > 0) {
         W(1, -RR_SH_C1 * y);
         W(2, RR_SH_C1 * z);
         W(3, -RR_SH_C1 * x);
-        dRGBdx = -RR_SH_C1 * load3(sh + 9);
-        dRGBdy = -RR_SH_C1 * load3(sh + 3);
-        dRGBdz = RR_SH_C1 * load3(sh + 6);
+        dRGBdx = -RR_SH_C1 * load3(rest + 6);
+        dRGBdy = -RR_SH_C1 * load3(rest + 0);
+        dRGBdz = RR_SH_C1 * load3(rest + 3);
         if (DEG > 1) {
             const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
             W(4, RR_SH_C2_0 * xy);
@@ -37,8 +38,8 @@ __device__ __forceinline__ v3 sh_backward(v3 dir, const float* sh, v3 dL_dRGB, f
             W(6, RR_SH_C2_2 * (2.f * zz - xx - yy));
             W(7, RR_SH_C2_3 * xz);
             W(8, RR_SH_C2_4 * (xx - yy));
-            const v3 s4 = load3(sh + 12), s5 = load3(sh + 15), s6 = load3(sh + 18), s7 = load3(sh + 21),
-                     s8 = load3(sh + 24);
+            const v3 s4 = load3(rest + 9), s5 = load3(rest + 12), s6 = load3(rest + 15), s7 = load3(rest + 18),
+                     s8 = load3(rest + 21);
             dRGBdx = dRGBdx + ((RR_SH_C2_0 * y) * s4 + (RR_SH_C2_2 * 2.f * -x) * s6 + (RR_SH_C2_3 * z) * s7 +
                                (RR_SH_C2_4 * 2.f * x) * s8);
             dRGBdy = dRGBdy + ((RR_SH_C2_0 * x) * s4 + (RR_SH_C2_1 * z) * s5 + (RR_SH_C2_2 * 2.f * -y) * s6 +
@@ -52,8 +53,8 @@ __device__ __forceinline__ v3 sh_backward(v3 dir, const float* sh, v3 dL_dRGB, f
                 W(13, RR_SH_C3_4 * x * (4.f * zz - xx - yy));
                 W(14, RR_SH_C3_5 * z * (xx - yy));
                 W(15, RR_SH_C3_6 * x * (xx - 3.f * yy));
-                const v3 s9 = load3(sh + 27), s10 = load3(sh + 30), s11 = load3(sh + 33), s12 = load3(sh + 36),
-                         s13 = load3(sh + 39), s14 = load3(sh + 42), s15 = load3(sh + 45);
+                const v3 s9 = load3(rest + 24), s10 = load3(rest + 27), s11 = load3(rest + 30), s12 = load3(rest + 33),
+                         s13 = load3(rest + 36), s14 = load3(rest + 39), s15 = load3(rest + 42);
                 dRGBdx = dRGBdx + ((RR_SH_C3_0 * 3.f * 2.f * xy) * s9 + (RR_SH_C3_1 * yz) * s10 +
                                    (RR_SH_C3_2 * -2.f * xy) * s11 + (RR_SH_C3_3 * -3.f * 2.f * xz) * s12 +
                                    (RR_SH_C3_4 * (-3.f * xx + 4.f * zz - yy)) * s13 + (RR_SH_C3_5 * 2.f * xz) * s14 +
@@ -76,23 +77,35 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
     const int M = a.M;
-    float* dsh = a.dL_dsh ? a.dL_dsh + (size_t)idx * M * 3 : nullptr;
-    float* dmean2 = a.dL_dmeans2D + 3 * (size_t)idx;
-    float* dcol = a.dL_dcolors + 3 * (size_t)idx;
+    // SH gradient destinations: one [M,3] block, or (raw mode) f_dc [1,3] + f_rest [M-1,3]
+    float* dsh_dc = nullptr;
+    float* dsh_rest = nullptr;
+    int n_rest = 0;  // floats in dsh_rest
+    if (a.dL_dsh) {
+        dsh_dc = a.raw ? a.dL_dsh + 3 * (size_t)idx : a.dL_dsh + (size_t)idx * M * 3;
+        dsh_rest = a.raw ? a.dL_dsh_rest + (size_t)idx * (M - 1) * 3 : dsh_dc + 3;
+        n_rest = 3 * (M - 1);
+    }
+    float* dmean2 = a.dL_dmeans2D ? a.dL_dmeans2D + 3 * (size_t)idx : nullptr;
+    float* dcol = a.dL_dcolors ? a.dL_dcolors + 3 * (size_t)idx : nullptr;
     float* dmean3 = a.dL_dmeans3D + 3 * (size_t)idx;
-    float* dcov = a.dL_dcov3D + 6 * (size_t)idx;
+    float* dcov = a.dL_dcov3D ? a.dL_dcov3D + 6 * (size_t)idx : nullptr;
     float* dscale = a.dL_dscales + 3 * (size_t)idx;
     float4* drot = reinterpret_cast<float4*>(a.dL_drot) + idx;
 
-    if (!(a.radii[idx] > 0)) {  // untouched Gaussians: exact zeros (backward.cu:146,357)
-        dmean2[0] = dmean2[1] = dmean2[2] = 0.f;
-        dcol[0] = dcol[1] = dcol[2] = 0.f;
+    const int radius = a.radii[idx];
+    if (!(radius > 0)) {  // untouched Gaussians: exact zeros (backward.cu:146,357)
+        if (dmean2) dmean2[0] = dmean2[1] = dmean2[2] = 0.f;
+        if (dcol) dcol[0] = dcol[1] = dcol[2] = 0.f;
         a.dL_dopacity[idx] = 0.f;
         dmean3[0] = dmean3[1] = dmean3[2] = 0.f;
+        if (dcov)
 #pragma unroll
-        for (int i = 0; i < 6; i++) dcov[i] = 0.f;
-        if (dsh)
-            for (int i = 0; i < 3 * M; i++) dsh[i] = 0.f;
+            for (int i = 0; i < 6; i++) dcov[i] = 0.f;
+        if (dsh_dc) {
+            dsh_dc[0] = dsh_dc[1] = dsh_dc[2] = 0.f;
+            for (int i = 0; i < n_rest; i++) dsh_rest[i] = 0.f;
+        }
         dscale[0] = dscale[1] = dscale[2] = 0.f;
         *drot = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
@@ -104,25 +117,43 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
     const float g8 = gp[8];
     const float dm2x = ga.x, dm2y = ga.y;
     const float dcx = ga.z, dcy = ga.w, dcz = gb.x;
-    dmean2[0] = dm2x;
-    dmean2[1] = dm2y;
-    dmean2[2] = 0.f;
-    dcol[0] = gb.z;
-    dcol[1] = gb.w;
-    dcol[2] = g8;
-    a.dL_dopacity[idx] = gb.y;
+    if (dmean2) {
+        dmean2[0] = dm2x;
+        dmean2[1] = dm2y;
+        dmean2[2] = 0.f;
+    }
+    if (dcol) {
+        dcol[0] = gb.z;
+        dcol[1] = gb.w;
+        dcol[2] = g8;
+    }
+    if (a.raw) {  // sigmoid backward (torch: grad * (1 - y) * y)
+        const float o = act_opacity(a.opacities[idx]);
+        a.dL_dopacity[idx] = gb.y * (1.0f - o) * o;
+    } else {
+        a.dL_dopacity[idx] = gb.y;
+    }
+    if (a.grad_accum) {  // densification statistics (gaussian_model.py:419-421, train.py:133)
+        a.grad_accum[idx] += sqrtf(dm2x * dm2x + dm2y * dm2y);
+        a.denom[idx] += 1.0f;
+        a.max_radii2D[idx] = fmaxf(a.max_radii2D[idx], (float)radius);
+    }
 
     const v3 mean = load3(a.means3D + 3 * (size_t)idx);
     float cov[6];
-    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f), q_raw = q;
     v3 scale = mk(0.f, 0.f, 0.f);
     if (a.cov3D_precomp) {
         const float* c = a.cov3D_precomp + 6 * (size_t)idx;
 #pragma unroll
         for (int i = 0; i < 6; i++) cov[i] = c[i];
     } else {
-        q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        q = q_raw = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
         scale = load3(a.scales + 3 * (size_t)idx);
+        if (a.raw) {
+            q = act_rot(q_raw);
+            scale = act_scale(scale);
+        }
         cov3d_from_scale_rot(scale, a.scale_modifier, q, cov);  // identical to the forward's value
     }
 
@@ -153,8 +184,9 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         dc[4] = 2 * T[0][2] * T[0][1] * dL_da + (T[0][1] * T[1][2] + T[0][2] * T[1][1]) * dL_db +
                 2 * T[1][1] * T[1][2] * dL_dc;
     }
+    if (dcov)
 #pragma unroll
-    for (int i = 0; i < 6; i++) dcov[i] = dc[i];
+        for (int i = 0; i < 6; i++) dcov[i] = dc[i];
     const float V[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
     const float dL_dT00 = 2 * (T[0][0] * V[0][0] + T[0][1] * V[0][1] + T[0][2] * V[0][2]) * dL_da +
                           (T[1][0] * V[0][0] + T[1][1] * V[0][1] + T[1][2] * V[0][2]) * dL_db;
@@ -193,19 +225,20 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
 
     // ---- SH bwd (backward.cu:9-128); the clamp mask is recomputed from the forward SH value ----
     if (a.shs) {
-        const float* sh = a.shs + (size_t)idx * M * 3;
+        const float* dc = a.raw ? a.shs + 3 * (size_t)idx : a.shs + (size_t)idx * M * 3;
+        const float* rest = a.raw ? a.shs_rest + (size_t)idx * (M - 1) * 3 : dc + 3;
         const v3 cp = load3(a.campos);
         const v3 dir_orig = mean - cp;
         const float len = sqrtf(dot(dir_orig, dir_orig));
         const v3 dir = mk(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
-        const v3 rgb = sh_eval<DEG>(dir, sh);
+        const v3 rgb = sh_eval<DEG>(dir, dc, rest);
         v3 dL_dRGB = mk(gb.z, gb.w, g8);
         dL_dRGB.x *= rgb.x < 0 ? 0.f : 1.f;
         dL_dRGB.y *= rgb.y < 0 ? 0.f : 1.f;
         dL_dRGB.z *= rgb.z < 0 ? 0.f : 1.f;
-        const v3 dL_ddir = sh_backward<DEG>(dir, sh, dL_dRGB, dsh);
+        const v3 dL_ddir = sh_backward<DEG>(dir, rest, dL_dRGB, dsh_dc, dsh_rest);
         constexpr int K = (DEG + 1) * (DEG + 1);
-        for (int i = 3 * K; i < 3 * M; i++) dsh[i] = 0.f;
+        for (int i = 3 * (K - 1); i < n_rest; i++) dsh_rest[i] = 0.f;
         // dnormvdv (auxiliary.h:96-106)
         const v3 v = dir_orig;
         const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
@@ -213,8 +246,9 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         dmean.x += ((+sum2 - v.x * v.x) * dL_ddir.x - v.y * v.x * dL_ddir.y - v.z * v.x * dL_ddir.z) * invsum32;
         dmean.y += (-v.x * v.y * dL_ddir.x + (sum2 - v.y * v.y) * dL_ddir.y - v.z * v.y * dL_ddir.z) * invsum32;
         dmean.z += (-v.x * v.z * dL_ddir.x - v.y * v.z * dL_ddir.y + (sum2 - v.z * v.z) * dL_ddir.z) * invsum32;
-    } else if (dsh) {
-        for (int i = 0; i < 3 * M; i++) dsh[i] = 0.f;
+    } else if (dsh_dc) {
+        dsh_dc[0] = dsh_dc[1] = dsh_dc[2] = 0.f;
+        for (int i = 0; i < n_rest; i++) dsh_rest[i] = 0.f;
     }
     dmean3[0] = dmean.x;
     dmean3[1] = dmean.y;
@@ -240,8 +274,13 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
 #pragma unroll
             for (int j = 0; j < 3; j++)
                 dM[i][j] = 2.0f * Mm[i][0] * dS[0][j] + 2.0f * Mm[i][1] * dS[1][j] + 2.0f * Mm[i][2] * dS[2][j];
+        float ds[3];
 #pragma unroll
-        for (int i = 0; i < 3; i++) dscale[i] = R[0][i] * dM[i][0] + R[1][i] * dM[i][1] + R[2][i] * dM[i][2];
+        for (int i = 0; i < 3; i++) ds[i] = R[0][i] * dM[i][0] + R[1][i] * dM[i][1] + R[2][i] * dM[i][2];
+        // raw mode: exp backward (torch: grad * result)
+        dscale[0] = a.raw ? ds[0] * scale.x : ds[0];
+        dscale[1] = a.raw ? ds[1] * scale.y : ds[1];
+        dscale[2] = a.raw ? ds[2] * scale.z : ds[2];
         float Gm[3][3];
 #pragma unroll
         for (int i = 0; i < 3; i++)
@@ -255,6 +294,15 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
                4 * y * (Gm[2][2] + Gm[0][0]);
         dq.w = 2 * r * (Gm[0][1] - Gm[1][0]) + 2 * x * (Gm[2][0] + Gm[0][2]) + 2 * y * (Gm[1][2] + Gm[2][1]) -
                4 * z * (Gm[1][1] + Gm[0][0]);
+        if (a.raw) {
+            // F.normalize backward: x / clamp_min(n, eps) -> g / n' - x (g.x) / n'^2 / n  (n >= eps)
+            const float4 x = q_raw;
+            const float n = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+            const float nd = fmaxf(n, 1e-12f);
+            const float gx = dq.x * x.x + dq.y * x.y + dq.z * x.z + dq.w * x.w;
+            const float c = n >= 1e-12f ? -gx / (nd * nd) / n : 0.f;
+            dq = make_float4(dq.x / nd + x.x * c, dq.y / nd + x.y * c, dq.z / nd + x.z * c, dq.w / nd + x.w * c);
+        }
         *drot = dq;
     } else {
         dscale[0] = dscale[1] = dscale[2] = 0.f;

@@ -145,6 +145,15 @@ __device__ __forceinline__ v3 xform_vec_4x3_T(v3 p, const float* m) {
               m[8] * p.x + m[9] * p.y + m[10] * p.z);
 }
 
+// GaussianModel getters (gaussian_model.py:85-105) for raw-parameter mode, written as torch
+// evaluates them: exp, x / clamp_min(|x|_2, 1e-12) (F.normalize), 1 / (1 + exp(-x)).
+__device__ __forceinline__ v3 act_scale(v3 s) { return mk(expf(s.x), expf(s.y), expf(s.z)); }
+__device__ __forceinline__ float4 act_rot(float4 q) {
+    const float n = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+    return make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
+}
+__device__ __forceinline__ float act_opacity(float o) { return 1.0f / (1.0f + expf(-o)); }
+
 // Quaternion (r,x,y,z) -> row-major rotation (forward.cu:116-127 builds its transpose in glm).
 __device__ __forceinline__ void quat_rot(float4 q, float R[3][3]) {
     const float r = q.x, x = q.y, y = q.z, z = q.w;
@@ -213,27 +222,29 @@ __device__ __forceinline__ void ewa_cov2d(const Proj2D& p, const float cov[6], f
 }
 
 // SH -> RGB (forward.cu:9-60), degree known at compile time.  Returns the pre-clamp value.
+// Coefficient 0 is dc[0..3), coefficient k >= 1 is rest[3(k-1)..): one contiguous [M,3] block
+// (dc = sh, rest = sh + 3) or the model's separate f_dc / f_rest tensors (raw-parameter mode).
 template <int DEG>
-__device__ __forceinline__ v3 sh_eval(v3 dir, const float* sh) {
-    v3 r = RR_SH_C0 * load3(sh);
+__device__ __forceinline__ v3 sh_eval(v3 dir, const float* dc, const float* rest) {
+    v3 r = RR_SH_C0 * load3(dc);
     if (DEG > 0) {
         const float x = dir.x, y = dir.y, z = dir.z;
-        r = r - (RR_SH_C1 * y) * load3(sh + 3) + (RR_SH_C1 * z) * load3(sh + 6) - (RR_SH_C1 * x) * load3(sh + 9);
+        r = r - (RR_SH_C1 * y) * load3(rest + 0) + (RR_SH_C1 * z) * load3(rest + 3) - (RR_SH_C1 * x) * load3(rest + 6);
         if (DEG > 1) {
             const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            r = r + (RR_SH_C2_0 * xy) * load3(sh + 12);
-            r = r + (RR_SH_C2_1 * yz) * load3(sh + 15);
-            r = r + (RR_SH_C2_2 * (2.0f * zz - xx - yy)) * load3(sh + 18);
-            r = r + (RR_SH_C2_3 * xz) * load3(sh + 21);
-            r = r + (RR_SH_C2_4 * (xx - yy)) * load3(sh + 24);
+            r = r + (RR_SH_C2_0 * xy) * load3(rest + 9);
+            r = r + (RR_SH_C2_1 * yz) * load3(rest + 12);
+            r = r + (RR_SH_C2_2 * (2.0f * zz - xx - yy)) * load3(rest + 15);
+            r = r + (RR_SH_C2_3 * xz) * load3(rest + 18);
+            r = r + (RR_SH_C2_4 * (xx - yy)) * load3(rest + 21);
             if (DEG > 2) {
-                r = r + (RR_SH_C3_0 * y * (3.0f * xx - yy)) * load3(sh + 27);
-                r = r + (RR_SH_C3_1 * xy * z) * load3(sh + 30);
-                r = r + (RR_SH_C3_2 * y * (4.0f * zz - xx - yy)) * load3(sh + 33);
-                r = r + (RR_SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * load3(sh + 36);
-                r = r + (RR_SH_C3_4 * x * (4.0f * zz - xx - yy)) * load3(sh + 39);
-                r = r + (RR_SH_C3_5 * z * (xx - yy)) * load3(sh + 42);
-                r = r + (RR_SH_C3_6 * x * (xx - 3.0f * yy)) * load3(sh + 45);
+                r = r + (RR_SH_C3_0 * y * (3.0f * xx - yy)) * load3(rest + 24);
+                r = r + (RR_SH_C3_1 * xy * z) * load3(rest + 27);
+                r = r + (RR_SH_C3_2 * y * (4.0f * zz - xx - yy)) * load3(rest + 30);
+                r = r + (RR_SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * load3(rest + 33);
+                r = r + (RR_SH_C3_4 * x * (4.0f * zz - xx - yy)) * load3(rest + 36);
+                r = r + (RR_SH_C3_5 * z * (xx - yy)) * load3(rest + 39);
+                r = r + (RR_SH_C3_6 * x * (xx - 3.0f * yy)) * load3(rest + 42);
             }
         }
     }

@@ -42,8 +42,13 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
 #pragma unroll
         for (int i = 0; i < 6; i++) cov[i] = c[i];
     } else {
-        const float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
-        cov3d_from_scale_rot(load3(a.scales + 3 * (size_t)idx), a.scale_modifier, q, cov);
+        float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        v3 sc = load3(a.scales + 3 * (size_t)idx);
+        if (a.raw) {
+            q = act_rot(q);
+            sc = act_scale(sc);
+        }
+        cov3d_from_scale_rot(sc, a.scale_modifier, q, cov);
     }
     const Proj2D pr = ewa_setup(p, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view);
     float ca, cb, cc;
@@ -75,10 +80,12 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
         v3 dir = p - cp;
         const float len = sqrtf(dot(dir, dir));
         dir = mk(dir.x / len, dir.y / len, dir.z / len);
-        const v3 c = sh_eval<DEG>(dir, a.shs + (size_t)idx * a.M * 3);
+        const float* dc = a.raw ? a.shs + 3 * (size_t)idx : a.shs + (size_t)idx * a.M * 3;
+        const float* rest = a.raw ? a.shs_rest + (size_t)idx * (a.M - 1) * 3 : dc + 3;
+        const v3 c = sh_eval<DEG>(dir, dc, rest);
         rgb = make_float4(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f), 0.f);
     }
-    const float opacity = a.opacities[idx];
+    const float opacity = a.raw ? act_opacity(a.opacities[idx]) : a.opacities[idx];
     Splat s;
     s.a = make_float4(px, py, cx, cy);
     s.b = make_float4(cz, opacity, p_view.z, 0.f);

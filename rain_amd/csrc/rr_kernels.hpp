@@ -22,6 +22,8 @@ struct PreArgs {
     uint2* tiles;                // {pairs this Gaussian emits (after culling), bounding-rect tile count}
     uint32_t* depth_keys;
     int cull;                    // exact tile culling on/off
+    int raw;                     // RR_FLAG_RAW_PARAMS: apply the GaussianModel getters in-kernel
+    const float* shs_rest;       // raw mode: f_rest [P,M-1,3] (shs = f_dc [P,1,3])
 };
 
 struct BlendFwdArgs {
@@ -71,6 +73,13 @@ struct GaussBwdArgs {
     float* dL_dsh;
     float* dL_dscales;
     float* dL_drot;
+    int raw;
+    const float* opacities;  // raw mode: logits (sigmoid backward)
+    const float* shs_rest;
+    float* dL_dsh_rest;
+    float* grad_accum;
+    float* denom;
+    float* max_radii2D;
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);

@@ -204,8 +204,12 @@ class GaussianModel:
             {'params': [self._scaling], 'lr': training_args.scaling_lr, "name": "scaling"},
             {'params': [self._rotation], 'lr': training_args.rotation_lr, "name": "rotation"},
         ]
-        fused = self.device.type == "cuda"
-        self.optimizer = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=fused)
+        if self.device.type == "cuda":
+            # one HIP launch for all six groups (include/rain_train.h); same state layout as torch Adam
+            from .optim import FusedAdam
+            self.optimizer = FusedAdam(groups, lr=0.0, eps=1e-15)
+        else:
+            self.optimizer = torch.optim.Adam(groups, lr=0.0, eps=1e-15)
         self.xyz_scheduler_args = get_expon_lr_func(
             lr_init=training_args.position_lr_init * self.spatial_lr_scale,
             lr_final=training_args.position_lr_final * self.spatial_lr_scale,
@@ -223,19 +227,26 @@ class GaussianModel:
     def params(self):
         return [self._xyz, self._features_dc, self._features_rest, self._opacity, self._scaling, self._rotation]
 
-    def bind_flat_grad(self, extra: int = 0):
-        """Make every parameter's .grad a view into one zeroed fp32 buffer (plus `extra` trailing
-        floats for densification statistics) and return the buffer."""
+    FLAT_ALIGN = 64  # floats: every parameter's gradient view starts on a 256-B boundary
+
+    def bind_flat_grad(self, extra: int = 0, zero: bool = True):
+        """Make every parameter's .grad a view into one fp32 buffer (segments padded to 256 B, plus
+        `extra` trailing floats for densification statistics) and return the buffer.  The whole
+        buffer is zeroed if `zero`, otherwise only the trailing `extra` floats (for writers that
+        overwrite every gradient, e.g. the fused raw-parameter backward)."""
         ps = self.params()
-        n = sum(p.numel() for p in ps)
+        a = self.FLAT_ALIGN
+        n = sum((p.numel() + a - 1) // a * a for p in ps)
         if self.flat_grad is None or self.flat_grad.numel() != n + extra:
             self.flat_grad = torch.zeros(n + extra, device=self.device)
-        else:
+        elif zero:
             self.flat_grad.zero_()
+        elif extra:
+            self.flat_grad[n:].zero_()
         off = 0
         for p in ps:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
-            off += p.numel()
+            off += (p.numel() + a - 1) // a * a
         return self.flat_grad
 
     # ---- densification (gaussian_model.py:200-421) ----

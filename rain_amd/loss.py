@@ -72,26 +72,52 @@ def _window_host():
     return _WINDOW
 
 
+def l1_ssim_forward(img, gt, lambda_dssim):
+    """Fused forward (include/rain_loss.h).  Returns (loss scalar, parts [3], workspace); the
+    workspace carries the per-pixel SSIM derivative maps the backward needs."""
+    from . import _native as N
+
+    L = N.loss_lib()
+    img = img.contiguous()
+    gt = gt.contiguous()
+    C, H, W = img.shape[-3:]
+    ws = torch.empty((L.rl_workspace_bytes(C, H, W),), dtype=torch.uint8, device=img.device)
+    loss = torch.empty((), dtype=torch.float32, device=img.device)
+    parts = torch.empty((3,), dtype=torch.float32, device=img.device)
+    rc = L.rl_l1_ssim_forward(img.data_ptr(), gt.data_ptr(), C, H, W, float(lambda_dssim), _window_host(),
+                              ws.data_ptr(), ws.numel(), loss.data_ptr(), parts.data_ptr(), N.stream_of(img))
+    if rc:
+        raise RuntimeError(L.rl_last_error().decode())
+    return loss, parts, ws
+
+
+def l1_ssim_backward(img, gt, lambda_dssim, ws, grad_loss=None):
+    """dLoss/dimg scaled by grad_loss (a device scalar; None = 1)."""
+    from . import _native as N
+
+    L = N.loss_lib()
+    img = img.contiguous()
+    gt = gt.contiguous()
+    C, H, W = img.shape[-3:]
+    dimg = torch.empty_like(img)
+    if grad_loss is None:
+        grad_loss = torch.ones((1,), dtype=torch.float32, device=img.device)
+    g = grad_loss.reshape(1).contiguous().float()
+    rc = L.rl_l1_ssim_backward(img.data_ptr(), gt.data_ptr(), C, H, W, float(lambda_dssim), _window_host(),
+                               ws.data_ptr(), g.data_ptr(), dimg.data_ptr(), N.stream_of(img))
+    if rc:
+        raise RuntimeError(L.rl_last_error().decode())
+    return dimg
+
+
 class _FusedL1SSIM(torch.autograd.Function):
     """(1-λ)·L1 + λ·(1-SSIM) in two HIP kernels (rain_amd/csrc/loss.hip, include/rain_loss.h)."""
 
     @staticmethod
     def forward(ctx, img, gt, lambda_dssim):
-        import ctypes
-
-        from . import _native as N
-
-        L = N.loss_lib()
         img = img.contiguous()
         gt = gt.contiguous()
-        C, H, W = img.shape[-3:]
-        ws = torch.empty((L.rl_workspace_bytes(C, H, W),), dtype=torch.uint8, device=img.device)
-        loss = torch.empty((), dtype=torch.float32, device=img.device)
-        parts = torch.empty((3,), dtype=torch.float32, device=img.device)
-        rc = L.rl_l1_ssim_forward(img.data_ptr(), gt.data_ptr(), C, H, W, float(lambda_dssim), _window_host(),
-                                  ws.data_ptr(), ws.numel(), loss.data_ptr(), parts.data_ptr(), N.stream_of(img))
-        if rc:
-            raise RuntimeError(L.rl_last_error().decode())
+        loss, parts, ws = l1_ssim_forward(img, gt, lambda_dssim)
         ctx.save_for_backward(img, gt, ws)
         ctx.lam = float(lambda_dssim)
         ctx.mark_non_differentiable(parts)
@@ -99,18 +125,8 @@ class _FusedL1SSIM(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_loss, _grad_parts):
-        from . import _native as N
-
         img, gt, ws = ctx.saved_tensors
-        L = N.loss_lib()
-        C, H, W = img.shape[-3:]
-        dimg = torch.empty_like(img)
-        g = grad_loss.reshape(1).contiguous().float()
-        rc = L.rl_l1_ssim_backward(img.data_ptr(), gt.data_ptr(), C, H, W, ctx.lam, _window_host(), ws.data_ptr(),
-                                   g.data_ptr(), dimg.data_ptr(), N.stream_of(img))
-        if rc:
-            raise RuntimeError(L.rl_last_error().decode())
-        return dimg, None, None
+        return l1_ssim_backward(img, gt, ctx.lam, ws, grad_loss), None, None
 
 
 def fused_l1_ssim_loss(img, gt, lambda_dssim=0.2):

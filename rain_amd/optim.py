@@ -1,0 +1,70 @@
+"""Fused Adam for the Gaussian parameter groups (include/rain_train.h).
+
+Drop-in for the reference's ``torch.optim.Adam(l, lr=0.0, eps=1e-15)``
+(scene/gaussian_model.py:153): same constructor, param_groups (with their "name" keys, which the
+densification surgery relies on, gaussian_model.py:200-291), per-parameter state
+{"step", "exp_avg", "exp_avg_sq"} and state_dict layout — but every group is updated by ONE HIP
+launch per step instead of torch's per-group multi-tensor launches.  Arithmetic follows torch's
+fused Adam (see rain_train.h).  Parameters whose .grad is None are skipped, as in torch.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _native as N
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        if weight_decay != 0.0:
+            raise ValueError("rain_amd FusedAdam: weight_decay is not supported (the reference uses none)")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0, amsgrad=False, maximize=False)
+        super().__init__(params, defaults)
+        N.train_lib()  # fail loudly now if the native library is missing
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        batches = {}  # (beta1, beta2, eps, device) -> [RTAdamGroup]
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.device.type != "cuda" or p.dtype != torch.float32 or not p.is_contiguous():
+                    raise RuntimeError("rain_amd FusedAdam: parameters must be contiguous float32 HIP tensors")
+                g = p.grad
+                if g.is_sparse or not g.is_contiguous() or g.dtype != torch.float32:
+                    raise RuntimeError("rain_amd FusedAdam: gradients must be dense contiguous float32")
+                state = self.state[p]
+                if len(state) == 0:
+                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                stp = state["step"]
+                if stp.device.type != "cpu":  # e.g. loaded from a torch fused/capturable Adam
+                    stp = state["step"] = stp.detach().to("cpu", torch.float32)
+                stp += 1.0
+                k = float(stp.item())
+                bc1 = 1.0 - math.pow(b1, k)
+                bc2s = math.sqrt(1.0 - math.pow(b2, k))
+                m, v = state["exp_avg"], state["exp_avg_sq"]
+                batches.setdefault((float(b1), float(b2), float(group["eps"]), p.device), []).append(
+                    (N.RTAdamGroup(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                                   float(group["lr"]), bc1, bc2s), p))
+        L = N.train_lib()
+        for (b1, b2, eps, dev), items in batches.items():
+            stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            for i in range(0, len(items), N.RT_MAX_GROUPS):
+                chunk = items[i:i + N.RT_MAX_GROUPS]
+                arr = (N.RTAdamGroup * len(chunk))(*[c[0] for c in chunk])
+                rc = L.rt_adam_step(arr, len(chunk), b1, b2, eps, stream)
+                if rc != 0:
+                    raise RuntimeError(f"rt_adam_step: {L.rt_last_error().decode(errors='replace')}")
+        return loss

@@ -72,7 +72,7 @@ class StepInfo:
 class Trainer:
     def __init__(self, gaussians: GaussianModel, cameras, gt_images, opt: OptimizationParams | None = None,
                  pipe: PipelineParams | None = None, cfg: TrainConfig | None = None, scene_extent: float = 1.0,
-                 group=None, loss_fn=None):
+                 group=None, loss_fn=None, fused: bool | None = None):
         self.g = gaussians
         self.cams = cameras
         self.gt = gt_images
@@ -93,8 +93,16 @@ class Trainer:
         self.densify_gen = torch.Generator(device=dev).manual_seed(self.cfg.seed + 12345)
         if self.cfg.warmup_iter > 0:
             self.opt.densify_until_iter += self.cfg.warmup_iter
+        # Fused step (rain_amd.fused): getters + their backward inside the rasterizer, gradients
+        # written straight into the flat buffer, densification statistics folded into the backward
+        # kernel, no autograd graph.  Needs the default loss and the SH / scale-rotation path.
+        plain_pipe = not (self.pipe.convert_SHs_python or self.pipe.compute_cov3D_python)
+        auto = dev.type == "cuda" and loss_fn is None and plain_pipe
+        self.fused = auto if fused is None else bool(fused)
+        if self.fused and not (dev.type == "cuda" and loss_fn is None and plain_pipe):
+            raise ValueError("fused step needs a HIP device, the default loss and the default pipeline")
 
-    def step(self, iteration: int, sync_loss: bool = False) -> StepInfo:
+    def _low_pass_and_view(self, iteration):
         g, opt, cfg = self.g, self.opt, self.cfg
         g.update_learning_rate(iteration)
         if cfg.ours:
@@ -102,7 +110,6 @@ class Trainer:
                 g.oneupSHdegree()
         elif iteration % 1000 == 0:
             g.oneupSHdegree()
-
         views = self.sampler.next_group()
         vidx = views[self.rank]
         cam = self.cams[vidx]
@@ -112,7 +119,76 @@ class Trainer:
                                                   cfg.c2f_max_lowpass)
         else:
             self.low_pass = 0.3
+        return vidx, cam
 
+    def _densify_and_adam(self, iteration):
+        g, opt, cfg = self.g, self.opt, self.cfg
+        densified = False
+        if iteration < opt.densify_until_iter:
+            if cfg.densify and iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0:
+                size_threshold = 20 if iteration > opt.opacity_reset_interval else None
+                abe_split = iteration <= cfg.warmup_iter
+                g.densify_and_prune(opt.densify_grad_threshold, 0.005, self.extent, size_threshold, N=2,
+                                    abe_split=abe_split, generator=self.densify_gen)
+                densified = True
+            if iteration % opt.opacity_reset_interval == 0 or (cfg.white_background and
+                                                               iteration == opt.densify_from_iter):
+                g.reset_opacity()
+        if iteration < opt.iterations:
+            # after densify_and_prune the parameters are new tensors with grad None, so this step
+            # skips them, exactly as the reference's optimizer.step() does (train.py:145-147)
+            g.optimizer.step()
+            g.optimizer.zero_grad(set_to_none=True)
+        return densified
+
+    def step(self, iteration: int, sync_loss: bool = False) -> StepInfo:
+        if self.fused:
+            return self._step_fused(iteration, sync_loss)
+        return self._step_autograd(iteration, sync_loss)
+
+    def _step_fused(self, iteration: int, sync_loss: bool) -> StepInfo:
+        from . import fused
+        from .loss import l1_ssim_backward, l1_ssim_forward
+
+        g, opt = self.g, self.opt
+        vidx, cam = self._low_pass_and_view(iteration)
+        P = g.get_xyz.shape[0]
+        densify_phase = iteration < opt.densify_until_iter
+        extra = 2 * P if (self.world > 1 and densify_phase) else 0
+        flat = g.bind_flat_grad(extra=extra, zero=False)  # the backward overwrites every gradient
+        with torch.no_grad():
+            image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass)
+            gt = self.gt[vidx]
+            loss, _parts, lws = l1_ssim_forward(image, gt, opt.lambda_dssim)
+            dimg = l1_ssim_backward(image, gt, opt.lambda_dssim, lws)
+            grads = dict(xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad,
+                         opacity=g._opacity.grad, scaling=g._scaling.grad, rotation=g._rotation.grad)
+            nparam = flat.numel() - extra
+            stats = None
+            local_max = None
+            if densify_phase:
+                if self.world > 1:
+                    local_max = g.max_radii2D.clone()
+                    stats = (flat[nparam:nparam + P], flat[nparam + P:], local_max)
+                else:
+                    stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D)
+            fused.backward(st, dimg, grads, stats)
+            if self.world > 1:
+                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+                flat[:nparam].mul_(1.0 / self.world)
+                if densify_phase:
+                    dist.all_reduce(local_max, op=dist.ReduceOp.MAX, group=self.group)
+                    g.max_radii2D = local_max
+                    g.xyz_gradient_accum += flat[nparam:nparam + P].unsqueeze(1)
+                    g.denom += flat[nparam + P:].unsqueeze(1)
+            densified = self._densify_and_adam(iteration)
+        return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
+                        view=vidx, low_pass=self.low_pass, densified=densified)
+
+    def _step_autograd(self, iteration: int, sync_loss: bool = False) -> StepInfo:
+        """The reference-API step: render() through GaussianRasterizer + autograd (train.py:109-147)."""
+        g, opt = self.g, self.opt
+        vidx, cam = self._low_pass_and_view(iteration)
         P = g.get_xyz.shape[0]
         densify_phase = iteration < opt.densify_until_iter
         flat = g.bind_flat_grad(extra=2 * P if (self.world > 1 and densify_phase) else 0)
@@ -124,7 +200,6 @@ class Trainer:
         loss = self.loss_fn(image, gt, opt.lambda_dssim)
         loss.backward()
 
-        densified = False
         with torch.no_grad():
             nparam = flat.numel() - (2 * P if (self.world > 1 and densify_phase) else 0)
             if self.world > 1:
@@ -146,19 +221,6 @@ class Trainer:
                 else:
                     g.max_radii2D[vis] = torch.max(g.max_radii2D[vis], radii[vis].float())
                     g.add_densification_stats(vsp, vis)
-                if cfg.densify and iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0:
-                    size_threshold = 20 if iteration > opt.opacity_reset_interval else None
-                    abe_split = iteration <= cfg.warmup_iter
-                    g.densify_and_prune(opt.densify_grad_threshold, 0.005, self.extent, size_threshold, N=2,
-                                        abe_split=abe_split, generator=self.densify_gen)
-                    densified = True
-                if iteration % opt.opacity_reset_interval == 0 or (cfg.white_background and
-                                                                   iteration == opt.densify_from_iter):
-                    g.reset_opacity()
-            if iteration < opt.iterations:
-                # after densify_and_prune the parameters are new tensors with grad None, so this step
-                # skips them, exactly as the reference's optimizer.step() does (train.py:145-147)
-                g.optimizer.step()
-                g.optimizer.zero_grad(set_to_none=True)
+            densified = self._densify_and_adam(iteration)
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
                         view=vidx, low_pass=self.low_pass, densified=densified)

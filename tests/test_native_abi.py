@@ -17,12 +17,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared(header):
     src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|size_t|char\s*\*|char)\s*\*?\s*(r[rl]_\w+)\s*\(", src,
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|size_t|char\s*\*|char)\s*\*?\s*(r[rlt]_\w+)\s*\(", src,
                                  flags=re.M)))
 
 
 @pytest.mark.parametrize("header,lib,listed", [("rain_raster.h", N.RASTER_LIB, N.RASTER_SYMBOLS),
-                                               ("rain_loss.h", N.LOSS_LIB, N.LOSS_SYMBOLS)])
+                                               ("rain_loss.h", N.LOSS_LIB, N.LOSS_SYMBOLS),
+                                               ("rain_train.h", N.TRAIN_LIB, N.TRAIN_SYMBOLS)])
 def test_library_exports_every_declared_symbol(header, lib, listed):
     names = _declared(header)
     assert names, header
