@@ -70,9 +70,8 @@ def lib():
         L.orc_sh_eval.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
         L.orc_pixel_blend_list.restype = ctypes.c_int
         L.orc_pixel_blend_list.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _u32p, ctypes.c_int]
-        if hasattr(L, "orc_dist_knn3"):
-            L.orc_dist_knn3.restype = ctypes.c_int
-            L.orc_dist_knn3.argtypes = [ctypes.c_int, _f32p, _f32p]
+        L.orc_dist_knn3.restype = None
+        L.orc_dist_knn3.argtypes = [ctypes.c_int, _f32p, _f32p, ctypes.POINTER(ctypes.c_uint32), _f32p]
         _lib = L
     return _lib
 
@@ -248,10 +247,16 @@ def get_higher_msb(n: int) -> int:
     return int(lib().orc_get_higher_msb(n))
 
 
-def dist_knn3(points):
-    """≙ simple_knn distCUDA2: mean squared distance to the 3 nearest neighbours."""
-    pts = _f32(points).reshape(-1, 3)
-    out = np.zeros(pts.shape[0], np.float32)
-    if pts.shape[0]:
-        lib().orc_dist_knn3(pts.shape[0], _p(pts), _p(out))
-    return out
+def dist_knn3(points, details=False):
+    """≙ simple_knn distCUDA2 (simple_knn.cu:164-207): mean squared distance to the 3 nearest
+    neighbours.  With details=True also returns the Morton-sorted order and the bbox (origin
+    included, simple_knn.cu:172-181)."""
+    pts = _f32(points)
+    pts = np.zeros((0, 3), np.float32) if pts is None else pts.reshape(-1, 3)
+    P = pts.shape[0]
+    out = np.zeros(P, np.float32)
+    order = np.zeros(P, np.uint32)
+    bbox = np.zeros(6, np.float32)
+    if P:
+        lib().orc_dist_knn3(P, _p(pts), _p(out), order.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _p(bbox))
+    return (out, order, bbox) if details else out

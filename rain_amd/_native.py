@@ -16,6 +16,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_PKG, "lib")
 RASTER_LIB = os.path.join(LIB_DIR, "librain_raster.so")
 KNN_LIB = os.path.join(LIB_DIR, "librain_knn.so")
+KNN_SYMBOLS = ["sk_workspace_bytes", "sk_dist_cuda2", "sk_last_error"]
 
 STAGES = ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd", "blend_bwd",
           "gauss_bwd", "memset"]

@@ -42,16 +42,12 @@ def knn3_mean_sq_dist_cpu(points: np.ndarray) -> np.ndarray:
 
 def init_scales(points: torch.Tensor) -> torch.Tensor:
     """scales = log(sqrt(clamp_min(distCUDA2(points), 1e-7))) repeated x3 (gaussian_model.py:124-125)."""
-    d2 = None
-    if points.is_cuda:
-        try:
-            from .simple_knn import distCUDA2
+    if points.is_cuda:  # the HIP simple-knn (include/rain_knn.h); raises if the library is missing
+        from .simple_knn import distCUDA2
 
-            d2 = distCUDA2(points)
-        except ImportError:
-            d2 = None
-    if d2 is None:
-        d2 = torch.from_numpy(knn3_mean_sq_dist_cpu(points.detach().cpu().numpy())).to(points.device)
+        d2 = distCUDA2(points)
+    else:  # CPU-only test scenes
+        d2 = torch.from_numpy(knn3_mean_sq_dist_cpu(points.detach().cpu().numpy()))
     d2 = torch.clamp_min(d2, 0.0000001)
     return torch.log(torch.sqrt(d2))[..., None].repeat(1, 3)
 

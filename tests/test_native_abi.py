@@ -17,13 +17,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared(header):
     src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|size_t|char\s*\*|char)\s*\*?\s*(r[rlt]_\w+)\s*\(", src,
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|size_t|char\s*\*|char)\s*\*?\s*(r[rlt]_\w+|sk_\w+)\s*\(", src,
                                  flags=re.M)))
 
 
 @pytest.mark.parametrize("header,lib,listed", [("rain_raster.h", N.RASTER_LIB, N.RASTER_SYMBOLS),
                                                ("rain_loss.h", N.LOSS_LIB, N.LOSS_SYMBOLS),
-                                               ("rain_train.h", N.TRAIN_LIB, N.TRAIN_SYMBOLS)])
+                                               ("rain_train.h", N.TRAIN_LIB, N.TRAIN_SYMBOLS),
+                                               ("rain_knn.h", N.KNN_LIB, N.KNN_SYMBOLS)])
 def test_library_exports_every_declared_symbol(header, lib, listed):
     names = _declared(header)
     assert names, header
@@ -105,3 +106,20 @@ def test_import_shim_is_the_product():
 
     assert shim.GaussianRasterizer is GaussianRasterizer
     assert shim._C is _C
+
+
+def test_simple_knn_shim_and_no_cpu_fallback():
+    import simple_knn
+    from simple_knn._C import distCUDA2
+
+    from rain_amd.simple_knn import distCUDA2 as native
+
+    assert distCUDA2 is native and simple_knn.distCUDA2 is native
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        distCUDA2(torch.zeros(10, 3))
+    with pytest.raises(RuntimeError, match="num_points, 3"):
+        distCUDA2(torch.zeros(10, 2))
+    L = N.knn()
+    assert L.sk_workspace_bytes(1000) < L.sk_workspace_bytes(1_000_000)
+    assert L.sk_dist_cuda2(-1, None, None, None, 0, None) != 0 and b"P" in L.sk_last_error()
+    assert L.sk_dist_cuda2(0, None, None, None, 0, None) == 0
