@@ -135,6 +135,57 @@ class GaussianModel:
         self.denom = denom
         self.optimizer.load_state_dict(opt_dict)
 
+    # ---- PLY (gaussian_model.py:167-246), via rain_amd.ply instead of plyfile ----
+    def construct_list_of_attributes(self):
+        names = ["x", "y", "z", "nx", "ny", "nz"]
+        names += [f"f_dc_{i}" for i in range(self._features_dc.shape[1] * self._features_dc.shape[2])]
+        names += [f"f_rest_{i}" for i in range(self._features_rest.shape[1] * self._features_rest.shape[2])]
+        names.append("opacity")
+        names += [f"scale_{i}" for i in range(self._scaling.shape[1])]
+        names += [f"rot_{i}" for i in range(self._rotation.shape[1])]
+        return names
+
+    def save_ply(self, path):
+        """Pre-activation values; SH stored channel-major ([P,3,K] flattened, gaussian_model.py:184-185)."""
+        from .ply import write_vertices
+
+        xyz = self._xyz.detach().cpu().numpy()
+        f_dc = self._features_dc.detach().transpose(1, 2).flatten(start_dim=1).contiguous().cpu().numpy()
+        f_rest = self._features_rest.detach().transpose(1, 2).flatten(start_dim=1).contiguous().cpu().numpy()
+        cols = np.concatenate((xyz, np.zeros_like(xyz), f_dc, f_rest, self._opacity.detach().cpu().numpy(),
+                               self._scaling.detach().cpu().numpy(), self._rotation.detach().cpu().numpy()), axis=1)
+        names = self.construct_list_of_attributes()
+        write_vertices(path, {n: cols[:, i] for i, n in enumerate(names)})
+
+    def load_ply(self, path):
+        from .ply import read_elements
+
+        v = read_elements(path)["vertex"]
+        names = v.dtype.names
+
+        def group(prefix):
+            ks = sorted((n for n in names if n.startswith(prefix)), key=lambda x: int(x.split("_")[-1]))
+            return np.stack([np.asarray(v[k], dtype=np.float64) for k in ks], axis=1) if ks else \
+                np.zeros((len(v), 0))
+
+        xyz = np.stack([np.asarray(v[k], dtype=np.float64) for k in ("x", "y", "z")], axis=1)
+        opacities = np.asarray(v["opacity"], dtype=np.float64)[..., None]
+        f_dc = np.stack([np.asarray(v[f"f_dc_{i}"], dtype=np.float64) for i in range(3)], axis=1)[..., None]
+        extra = group("f_rest_")
+        K1 = (self.max_sh_degree + 1) ** 2 - 1
+        assert extra.shape[1] == 3 * K1, f"{path}: {extra.shape[1]} f_rest columns, expected {3 * K1}"
+        extra = extra.reshape(len(v), 3, K1)
+        dev = self.device
+        t = lambda a: torch.tensor(a, dtype=torch.float, device=dev)  # noqa: E731
+        self._xyz = nn.Parameter(t(xyz).requires_grad_(True))
+        self._features_dc = nn.Parameter(t(f_dc).transpose(1, 2).contiguous().requires_grad_(True))
+        self._features_rest = nn.Parameter(t(extra).transpose(1, 2).contiguous().requires_grad_(True))
+        self._opacity = nn.Parameter(t(opacities).requires_grad_(True))
+        self._scaling = nn.Parameter(t(group("scale_")).requires_grad_(True))
+        self._rotation = nn.Parameter(t(group("rot")).requires_grad_(True))
+        self.max_radii2D = torch.zeros((self._xyz.shape[0]), device=dev)
+        self.active_sh_degree = self.max_sh_degree
+
     # ---- getters (gaussian_model.py:85-108) ----
     @property
     def get_scaling(self):
