@@ -527,7 +527,9 @@ int rr_debug_get_views(const rr_frame* f, const void* geom_buffer, const void* i
 
 int rr_set_blend_config(int fwd_waves, int bwd_waves) {
     auto ok = [](int v) { return v == 0 || v == 1 || v == 2 || v == 4; };
-    if (!ok(fwd_waves) || !ok(bwd_waves)) return fail(RR_ERR_ARG, "waves per tile must be 0, 1, 2 or 4");
+    // bwd 3 = one wave per tile without the 4-waves/SIMD register cap (A/B tuning variant)
+    if (!ok(fwd_waves) || !(ok(bwd_waves) || bwd_waves == 3))
+        return fail(RR_ERR_ARG, "waves per tile must be 0, 1, 2 or 4");
     set_blend_config(fwd_waves, bwd_waves);
     return RR_OK;
 }

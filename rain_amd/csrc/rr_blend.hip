@@ -25,6 +25,22 @@
 
 namespace rr {
 
+// Prefetch of one Splat record into three float4 registers.  Plain float4 variables: keeping
+// the prefetched record in a struct made hipcc place it in scratch (private memory).
+__device__ __forceinline__ void load_splat(const Splat* __restrict__ s, uint32_t i, float4& a, float4& b, float4& c) {
+    const float4* p = reinterpret_cast<const float4*>(s + i);
+    a = p[0];
+    b = p[1];
+    c = p[2];
+}
+
+// 1/x from v_rcp_f32 (1 ulp) refined by one Newton step (~0.5 ulp): 4 VALU ops instead of the
+// ~10-op IEEE division sequence hipcc emits for '/' and __fdividef.  x = 1 - alpha is in [0.01, 1).
+__device__ __forceinline__ float rcp_nr(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.0f), r);
+}
+
 // Bijective block -> tile remap (cdna_hip_programming.md §5, "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_tile(int b, int n) {
     const int q = n >> 3, r = n & 7;
@@ -62,20 +78,20 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
 
-    Splat nxt;
-    if (t < n) nxt = a.splats[a.point_list[range.x + t]];
+    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
+    if (t < n) load_splat(a.splats, a.point_list[range.x + t], na, nb, nc);
     for (int base = 0; base < n; base += B) {
         bool my_done = true;
 #pragma unroll
         for (int q = 0; q < PPL; q++) my_done = my_done && done[q];
         if (__syncthreads_count(my_done) == B) break;
         if (base + t < n) {
-            s_a[t] = nxt.a;
-            s_b[t] = nxt.b;
-            s_c[t] = nxt.c;
+            s_a[t] = na;
+            s_b[t] = nb;
+            s_c[t] = nc;
         }
         __syncthreads();
-        if (base + B + t < n) nxt = a.splats[a.point_list[range.x + base + B + t]];  // prefetch next round
+        if (base + B + t < n) load_splat(a.splats, a.point_list[range.x + base + B + t], na, nb, nc);  // next round
         const int cnt = min(B, n - base);
         for (int j = 0; j < cnt; j++) {
             if (__all(my_done)) break;
@@ -146,8 +162,10 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
     }
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
+// OCC: minimum waves per SIMD requested from the register allocator (4 caps k_blend_bwd<1> at
+// 128 VGPRs, a few spills in the per-round flush; 1 = compiler's choice, 132 VGPRs / 3 waves).
+template <int NW, int OCC>
+__global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
     constexpr int PPL = 4 / NW;
     constexpr int B = 64 * NW;
     const int ntiles = a.gx * a.gy;
@@ -192,23 +210,23 @@ __global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
     const float ddely_dy = 0.5f * a.H;
 
     uint32_t nid = 0;
-    Splat nxt;
+    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
     if (t < nmax) {
         nid = a.point_list[range.x + nmax - 1 - t];
-        nxt = a.splats[nid];
+        load_splat(a.splats, nid, na, nb, nc);
     }
     for (int base = 0; base < nmax; base += B) {
         if (base + t < nmax) {
             s_id[t] = nid;
-            s_a[t] = nxt.a;
-            s_b[t] = nxt.b;
-            s_c[t] = nxt.c;
+            s_a[t] = na;
+            s_b[t] = nb;
+            s_c[t] = nc;
         }
         __syncthreads();
         const int k2 = base + B + t;  // prefetch the next round while this one is blended
         if (k2 < nmax) {
             nid = a.point_list[range.x + nmax - 1 - k2];
-            nxt = a.splats[nid];
+            load_splat(a.splats, nid, na, nb, nc);
         }
         const int cnt = min(B, nmax - base);
         for (int j = 0; j < cnt; j++) {
@@ -227,7 +245,8 @@ __global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
                 if (act) {
                     any = true;
                     const float one_m = 1.f - alpha;
-                    T[q] = __fdividef(T[q], one_m);
+                    const float inv = rcp_nr(one_m);  // both divisions by (1 - alpha) share one reciprocal
+                    T[q] = T[q] * inv;
                     const float dchannel_dcolor = alpha * T[q];
                     const float4 Cc = s_c[j];
                     ar0[q] = la[q] * lc0[q] + (1.f - la[q]) * ar0[q];
@@ -242,7 +261,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_bwd(BlendBwdArgs a) {
                     g8 += dchannel_dcolor * dp2[q];
                     dL_dalpha *= T[q];
                     la[q] = alpha;
-                    dL_dalpha += __fdividef(tfbg[q], one_m);
+                    dL_dalpha += tfbg[q] * inv;
                     const float dL_dG = Bv.y * dL_dalpha;
                     const float gdx = G * dx, gdy = G * dy;
                     const float dG_ddelx = -gdx * A.z - gdy * A.w;
@@ -284,7 +303,7 @@ int env_waves(const char* name, int dflt) {
     const char* s = std::getenv(name);
     if (!s) return dflt;
     const int v = std::atoi(s);
-    return (v == 1 || v == 2 || v == 4) ? v : dflt;
+    return (v >= 1 && v <= 4) ? v : dflt;
 }
 }  // namespace
 
@@ -313,9 +332,10 @@ void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
     if (T == 0) return;
     const int nw = g_bwd_waves ? g_bwd_waves : env_waves("RAIN_BLEND_BWD_WAVES", kBwdWavesDefault);
     switch (nw) {
-        case 2: k_blend_bwd<2><<<T, 128, 0, st>>>(a); break;
-        case 4: k_blend_bwd<4><<<T, 256, 0, st>>>(a); break;
-        default: k_blend_bwd<1><<<T, 64, 0, st>>>(a); break;
+        case 2: k_blend_bwd<2, 1><<<T, 128, 0, st>>>(a); break;
+        case 3: k_blend_bwd<1, 1><<<T, 64, 0, st>>>(a); break;  // A/B variant: 1 wave, no occupancy cap
+        case 4: k_blend_bwd<4, 1><<<T, 256, 0, st>>>(a); break;
+        default: k_blend_bwd<1, 4><<<T, 64, 0, st>>>(a); break;
     }
 }
 
