@@ -23,6 +23,10 @@
 
 namespace {
 
+// Onesweep radix sort at every size (rocPRIM's default merge-sorts below 2^20 items)
+using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
+
 thread_local std::string g_err;
 int fail(const std::string& m) {
     g_err = m;
@@ -232,7 +236,7 @@ Ws carve(void* buf, int P) {
     w.boxes = c.take<Box>((size_t)(nb > 0 ? nb : 1));
     w.temp_bytes = 0;
     if (P > 0)
-        (void)rocprim::radix_sort_pairs(nullptr, w.temp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+        (void)rocprim::radix_sort_pairs<OnesweepSort>(nullptr, w.temp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                         rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)P, 0, 30,
                                         (hipStream_t)0);
     w.temp = c.take<char>(w.temp_bytes > 0 ? w.temp_bytes : 1);
@@ -263,7 +267,7 @@ int sk_dist_cuda2(int P, const float* points, float* mean_dists, void* workspace
     k_bbox_final<<<1, kThreads, 0, st>>>(npart, w.part, w.bbox);
     k_morton<<<nblk, kThreads, 0, st>>>(P, points, w.bbox, w.codes);
     size_t tb = w.temp_bytes;
-    if (rocprim::radix_sort_pairs(w.temp, tb, w.codes, w.codes_sorted, rocprim::counting_iterator<uint32_t>(0), w.idx,
+    if (rocprim::radix_sort_pairs<OnesweepSort>(w.temp, tb, w.codes, w.codes_sorted, rocprim::counting_iterator<uint32_t>(0), w.idx,
                                   (size_t)P, 0, 30, st) != hipSuccess)
         return fail("morton sort failed");
     k_gather<<<nblk, kThreads, 0, st>>>(P, points, w.idx, w.sorted);

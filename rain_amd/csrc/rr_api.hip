@@ -3,9 +3,7 @@
 //
 // Replaces CudaRasterizer::Rasterizer::{forward,backward,markVisible}
 // (rasterizer_impl.cu:130-142,187-430) and the pybind wrappers (rasterize_points.cu:24-212).
-#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -61,15 +59,7 @@ uint32_t higher_msb(uint32_t n) {
 inline int grid_x(int W) { return (W + TILE_X - 1) / TILE_X; }
 inline int grid_y(int H) { return (H + TILE_Y - 1) / TILE_Y; }
 
-// ---- temp-storage queries (rocPRIM two-phase API) ----
-size_t depth_sort_temp(int P) {
-    size_t bytes = 0;
-    if (P > 0)
-        (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                        rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)P, 0,
-                                        32, (hipStream_t)0);
-    return bytes;
-}
+// ---- temp-storage queries ----
 // Component-wise saturating sum of {pairs, rect area}: associative on non-negative counts, and a
 // saturated total (>= 2^32) is caught by the 2^31 capacity check instead of wrapping silently.
 struct SatAdd2 {
@@ -78,6 +68,7 @@ struct SatAdd2 {
         return make_uint2(x < a.x ? 0xffffffffu : x, y < a.y ? 0xffffffffu : y);
     }
 };
+size_t depth_sort_temp(int P) { return P > 0 ? radix_sort_temp_bytes<uint32_t>((size_t)P, 32) : 0; }
 size_t scan_temp(int P) {
     size_t bytes = 0;
     if (P > 0)
@@ -87,11 +78,7 @@ size_t scan_temp(int P) {
 }
 template <typename K>
 size_t tile_sort_temp(int L, int bits) {
-    size_t bytes = 0;
-    if (L > 0)
-        (void)rocprim::radix_sort_pairs(nullptr, bytes, (const K*)nullptr, (K*)nullptr, (const uint32_t*)nullptr,
-                                        (uint32_t*)nullptr, (size_t)L, 0, bits, (hipStream_t)0);
-    return bytes;
+    return L > 0 ? radix_sort_temp_bytes<K>((size_t)L, bits) : 0;
 }
 
 // ---- scratch layouts ----
@@ -315,9 +302,8 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     {
         StageTimer tm(RR_STAGE_DEPTH_SORT, st);
         size_t tb = gm.temp_bytes;
-        RR_CHECK(rocprim::radix_sort_pairs(gm.temp, tb, gm.depth_keys, gm.depth_keys_sorted,
-                                           rocprim::counting_iterator<uint32_t>(0), gm.idx_sorted, (size_t)P, 0, 32,
-                                           st),
+        RR_CHECK(radix_sort_pairs<uint32_t>(gm.temp, tb, gm.depth_keys, gm.depth_keys_sorted, nullptr, gm.idx_sorted,
+                                            (size_t)P, 0, 32, st),
                  "depth sort");
     }
     RR_STAGE_CHECK("depth sort");
@@ -373,14 +359,12 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
             StageTimer tm(RR_STAGE_TILE_SORT, st);
             size_t tb = bn.temp_bytes;
             if (bn.wide)
-                RR_CHECK(rocprim::radix_sort_pairs(bn.temp, tb, (const uint32_t*)bn.keys, (uint32_t*)bn.keys_sorted,
-                                                   (const uint32_t*)bn.vals, bn.point_list, (size_t)L, 0, bn.bits,
-                                                   st),
+                RR_CHECK(radix_sort_pairs<uint32_t>(bn.temp, tb, (const uint32_t*)bn.keys, (uint32_t*)bn.keys_sorted,
+                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st),
                          "tile sort");
             else
-                RR_CHECK(rocprim::radix_sort_pairs(bn.temp, tb, (const uint16_t*)bn.keys, (uint16_t*)bn.keys_sorted,
-                                                   (const uint32_t*)bn.vals, bn.point_list, (size_t)L, 0, bn.bits,
-                                                   st),
+                RR_CHECK(radix_sort_pairs<uint16_t>(bn.temp, tb, (const uint16_t*)bn.keys, (uint16_t*)bn.keys_sorted,
+                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st),
                          "tile sort");
         }
         RR_STAGE_CHECK("tile sort");

@@ -93,6 +93,14 @@ void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);
+
+// rr_sort.hip: stable LSD radix sort of (K key, u32 value) pairs on bits [begin_bit, end_bit).
+// vals_in == nullptr means values = input index.  keys_out may be nullptr only for a single pass.
+template <typename K>
+size_t radix_sort_temp_bytes(size_t n, int bits);
+template <typename K>
+hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
+                            uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
 
 }  // namespace rr
