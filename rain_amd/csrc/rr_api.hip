@@ -241,6 +241,7 @@ int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, boo
                     "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
     if (g->shs && (f->D < 0 || f->D > 3 || f->M < (f->D + 1) * (f->D + 1)))
         return fail(RR_ERR_ARG, "sh_degree must be 0..3 and sh.size(1) >= (degree+1)^2");
+    if (f->M > 16) return fail(RR_ERR_ARG, "sh.size(1) > 16 is not supported (SH degree <= 3, forward.cu:9-60)");
     if (f->flags & RR_FLAG_RAW_PARAMS) {
         if (!g->shs || !sr || !g->opacities)
             return fail(RR_ERR_ARG, "raw-parameter mode needs SH, scales/rotations and opacities");

@@ -12,32 +12,20 @@ namespace rr {
 
 // ---- per-Gaussian backward -------------------------------------------------------------
 
-// SH backward (backward.cu:9-128): writes dL_dsh[0..K) and returns dL/d(dir) via dRGBd{x,y,z}.
+// SH backward (backward.cu:9-128), split in two so that the coefficient gradients can overwrite
+// the staged coefficients in LDS: sh_dir_grad only reads the coefficients (rest[3(k-1)..] holds
+// coefficient k >= 1) and returns dL/d(dir); sh_coeff_grads only writes dL/dsh_k = Y_k(dir) dL/dRGB
+// into row[3k..3k+2] for k < K and zeros for K <= k < M.
 template <int DEG>
-__device__ __forceinline__ v3 sh_backward(v3 dir, const float* rest, v3 dL_dRGB, float* dsh_dc, float* dsh_rest) {
+__device__ __forceinline__ v3 sh_dir_grad(v3 dir, const float* rest, v3 dL_dRGB) {
     const float x = dir.x, y = dir.y, z = dir.z;
     v3 dRGBdx = mk(0, 0, 0), dRGBdy = mk(0, 0, 0), dRGBdz = mk(0, 0, 0);
-    auto W = [&](int k, float s) {
-        float* d = k == 0 ? dsh_dc : dsh_rest + 3 * (k - 1);
-        d[0] = s * dL_dRGB.x;
-        d[1] = s * dL_dRGB.y;
-        d[2] = s * dL_dRGB.z;
-    };
-    W(0, RR_SH_C0);
     if (DEG > 0) {
-        W(1, -RR_SH_C1 * y);
-        W(2, RR_SH_C1 * z);
-        W(3, -RR_SH_C1 * x);
         dRGBdx = -RR_SH_C1 * load3(rest + 6);
         dRGBdy = -RR_SH_C1 * load3(rest + 0);
         dRGBdz = RR_SH_C1 * load3(rest + 3);
         if (DEG > 1) {
             const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            W(4, RR_SH_C2_0 * xy);
-            W(5, RR_SH_C2_1 * yz);
-            W(6, RR_SH_C2_2 * (2.f * zz - xx - yy));
-            W(7, RR_SH_C2_3 * xz);
-            W(8, RR_SH_C2_4 * (xx - yy));
             const v3 s4 = load3(rest + 9), s5 = load3(rest + 12), s6 = load3(rest + 15), s7 = load3(rest + 18),
                      s8 = load3(rest + 21);
             dRGBdx = dRGBdx + ((RR_SH_C2_0 * y) * s4 + (RR_SH_C2_2 * 2.f * -x) * s6 + (RR_SH_C2_3 * z) * s7 +
@@ -46,13 +34,6 @@ __device__ __forceinline__ v3 sh_backward(v3 dir, const float* rest, v3 dL_dRGB,
                                (RR_SH_C2_4 * 2.f * -y) * s8);
             dRGBdz = dRGBdz + ((RR_SH_C2_1 * y) * s5 + (RR_SH_C2_2 * 2.f * 2.f * z) * s6 + (RR_SH_C2_3 * x) * s7);
             if (DEG > 2) {
-                W(9, RR_SH_C3_0 * y * (3.f * xx - yy));
-                W(10, RR_SH_C3_1 * xy * z);
-                W(11, RR_SH_C3_2 * y * (4.f * zz - xx - yy));
-                W(12, RR_SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy));
-                W(13, RR_SH_C3_4 * x * (4.f * zz - xx - yy));
-                W(14, RR_SH_C3_5 * z * (xx - yy));
-                W(15, RR_SH_C3_6 * x * (xx - 3.f * yy));
                 const v3 s9 = load3(rest + 24), s10 = load3(rest + 27), s11 = load3(rest + 30), s12 = load3(rest + 33),
                          s13 = load3(rest + 36), s14 = load3(rest + 39), s15 = load3(rest + 42);
                 dRGBdx = dRGBdx + ((RR_SH_C3_0 * 3.f * 2.f * xy) * s9 + (RR_SH_C3_1 * yz) * s10 +
@@ -73,19 +54,46 @@ __device__ __forceinline__ v3 sh_backward(v3 dir, const float* rest, v3 dL_dRGB,
 }
 
 template <int DEG>
-__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
-    const int M = a.M;
-    // SH gradient destinations: one [M,3] block, or (raw mode) f_dc [1,3] + f_rest [M-1,3]
-    float* dsh_dc = nullptr;
-    float* dsh_rest = nullptr;
-    int n_rest = 0;  // floats in dsh_rest
-    if (a.dL_dsh) {
-        dsh_dc = a.raw ? a.dL_dsh + 3 * (size_t)idx : a.dL_dsh + (size_t)idx * M * 3;
-        dsh_rest = a.raw ? a.dL_dsh_rest + (size_t)idx * (M - 1) * 3 : dsh_dc + 3;
-        n_rest = 3 * (M - 1);
+__device__ __forceinline__ void sh_coeff_grads(v3 dir, v3 dL_dRGB, float* row, int M) {
+    const float x = dir.x, y = dir.y, z = dir.z;
+    auto W = [&](int k, float s) {
+        row[3 * k + 0] = s * dL_dRGB.x;
+        row[3 * k + 1] = s * dL_dRGB.y;
+        row[3 * k + 2] = s * dL_dRGB.z;
+    };
+    W(0, RR_SH_C0);
+    if (DEG > 0) {
+        W(1, -RR_SH_C1 * y);
+        W(2, RR_SH_C1 * z);
+        W(3, -RR_SH_C1 * x);
+        if (DEG > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            W(4, RR_SH_C2_0 * xy);
+            W(5, RR_SH_C2_1 * yz);
+            W(6, RR_SH_C2_2 * (2.f * zz - xx - yy));
+            W(7, RR_SH_C2_3 * xz);
+            W(8, RR_SH_C2_4 * (xx - yy));
+            if (DEG > 2) {
+                W(9, RR_SH_C3_0 * y * (3.f * xx - yy));
+                W(10, RR_SH_C3_1 * xy * z);
+                W(11, RR_SH_C3_2 * y * (4.f * zz - xx - yy));
+                W(12, RR_SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy));
+                W(13, RR_SH_C3_4 * x * (4.f * zz - xx - yy));
+                W(14, RR_SH_C3_5 * z * (xx - yy));
+                W(15, RR_SH_C3_6 * x * (xx - 3.f * yy));
+            }
+        }
     }
+    constexpr int K = (DEG + 1) * (DEG + 1);
+    for (int i = 3 * K; i < 3 * M; i++) row[i] = 0.f;
+}
+
+// One Gaussian.  `row` is this thread's LDS row holding its SH coefficients (staged by the
+// kernel; coefficient k at row[3k..3k+2]) and receiving its SH gradients in the same layout; it is
+// nullptr when there are neither SH inputs nor SH gradients.
+template <int DEG>
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* row) {
+    const int M = a.M;
     float* dmean2 = a.dL_dmeans2D ? a.dL_dmeans2D + 3 * (size_t)idx : nullptr;
     float* dcol = a.dL_dcolors ? a.dL_dcolors + 3 * (size_t)idx : nullptr;
     float* dmean3 = a.dL_dmeans3D + 3 * (size_t)idx;
@@ -102,10 +110,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         if (dcov)
 #pragma unroll
             for (int i = 0; i < 6; i++) dcov[i] = 0.f;
-        if (dsh_dc) {
-            dsh_dc[0] = dsh_dc[1] = dsh_dc[2] = 0.f;
-            for (int i = 0; i < n_rest; i++) dsh_rest[i] = 0.f;
-        }
+        if (row)
+            for (int i = 0; i < 3 * M; i++) row[i] = 0.f;
         dscale[0] = dscale[1] = dscale[2] = 0.f;
         *drot = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
@@ -225,8 +231,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
 
     // ---- SH bwd (backward.cu:9-128); the clamp mask is recomputed from the forward SH value ----
     if (a.shs) {
-        const float* dc = a.raw ? a.shs + 3 * (size_t)idx : a.shs + (size_t)idx * M * 3;
-        const float* rest = a.raw ? a.shs_rest + (size_t)idx * (M - 1) * 3 : dc + 3;
+        const float* dc = row;  // staged coefficients (same values as shs / f_dc + f_rest)
+        const float* rest = row + 3;
         const v3 cp = load3(a.campos);
         const v3 dir_orig = mean - cp;
         const float len = sqrtf(dot(dir_orig, dir_orig));
@@ -236,9 +242,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         dL_dRGB.x *= rgb.x < 0 ? 0.f : 1.f;
         dL_dRGB.y *= rgb.y < 0 ? 0.f : 1.f;
         dL_dRGB.z *= rgb.z < 0 ? 0.f : 1.f;
-        const v3 dL_ddir = sh_backward<DEG>(dir, rest, dL_dRGB, dsh_dc, dsh_rest);
-        constexpr int K = (DEG + 1) * (DEG + 1);
-        for (int i = 3 * (K - 1); i < n_rest; i++) dsh_rest[i] = 0.f;
+        const v3 dL_ddir = sh_dir_grad<DEG>(dir, rest, dL_dRGB);  // last read of the staged coefficients
+        sh_coeff_grads<DEG>(dir, dL_dRGB, row, M);                // overwrite them with dL/dsh
         // dnormvdv (auxiliary.h:96-106)
         const v3 v = dir_orig;
         const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
@@ -246,9 +251,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         dmean.x += ((+sum2 - v.x * v.x) * dL_ddir.x - v.y * v.x * dL_ddir.y - v.z * v.x * dL_ddir.z) * invsum32;
         dmean.y += (-v.x * v.y * dL_ddir.x + (sum2 - v.y * v.y) * dL_ddir.y - v.z * v.y * dL_ddir.z) * invsum32;
         dmean.z += (-v.x * v.z * dL_ddir.x - v.y * v.z * dL_ddir.y + (sum2 - v.z * v.z) * dL_ddir.z) * invsum32;
-    } else if (dsh_dc) {
-        dsh_dc[0] = dsh_dc[1] = dsh_dc[2] = 0.f;
-        for (int i = 0; i < n_rest; i++) dsh_rest[i] = 0.f;
+    } else if (row) {
+        for (int i = 0; i < 3 * M; i++) row[i] = 0.f;
     }
     dmean3[0] = dmean.x;
     dmean3[1] = dmean.y;
@@ -310,14 +314,79 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
     }
 }
 
+// Workgroup of kGB Gaussians.  The SH coefficients (the bulk of the per-Gaussian bytes: 192 B at
+// M = 16) are staged into LDS one Gaussian row per wave instruction (coalesced 192-B reads instead
+// of 64 lanes each walking its own 192-B record), and dL/dsh leaves the same way.  Row stride
+// kShStride is odd, so the per-thread row accesses are LDS-bank-conflict free.
+constexpr int kGB = 128;
+constexpr int kShStride = 49;
+
+template <int DEG>
+__global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
+    __shared__ float s_sh[kGB * kShStride];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int i0 = blockIdx.x * kGB;
+    const int nvalid = min(kGB, a.P - i0);
+    const int M = a.M, nf = 3 * M;  // floats per Gaussian
+    const bool stage = M > 0 && (a.shs != nullptr || a.dL_dsh != nullptr);
+    if (stage && a.shs) {
+        // flat, coalesced loads of the block's coefficient region(s), all in flight at once, then
+        // scattered into the padded LDS rows; j = e / w via a float reciprocal (exact: e < 2^13)
+        auto stage_in = [&](const float* src, int w, int koff) {
+            const int total = nvalid * w;
+            const float inv = 1.0f / (float)w;
+            float buf[48];
+#pragma unroll
+            for (int q = 0; q < 48; q++) {
+                const int e = t + q * kGB;
+                buf[q] = e < total ? src[(size_t)i0 * w + e] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < 48; q++) {
+                const int e = t + q * kGB;
+                if (e < total) {
+                    const int j = (int)(((float)e + 0.5f) * inv);
+                    s_sh[j * kShStride + koff + (e - j * w)] = buf[q];
+                }
+            }
+        };
+        if (!a.raw) {
+            stage_in(a.shs, nf, 0);
+        } else {
+            stage_in(a.shs, 3, 0);
+            if (nf > 3) stage_in(a.shs_rest, nf - 3, 3);
+        }
+    }
+    __syncthreads();
+    if (t < nvalid) gauss_bwd_one<DEG>(a, i0 + t, stage ? s_sh + t * kShStride : nullptr);
+    __syncthreads();
+    if (stage && a.dL_dsh) {
+        auto stage_out = [&](float* dst, int w, int koff) {
+            const int total = nvalid * w;
+            const float inv = 1.0f / (float)w;
+            for (int e = t; e < total; e += kGB) {
+                const int j = (int)(((float)e + 0.5f) * inv);
+                dst[(size_t)i0 * w + e] = s_sh[j * kShStride + koff + (e - j * w)];
+            }
+        };
+        if (!a.raw) {
+            stage_out(a.dL_dsh, nf, 0);
+        } else {
+            stage_out(a.dL_dsh, 3, 0);
+            if (nf > 3) stage_out(a.dL_dsh_rest, nf - 3, 3);
+        }
+    }
+}
+
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st) {
     if (a.P == 0) return;
-    const int nb = (a.P + 255) / 256;
+    // a.M <= 16 is validated by the API: the LDS row holds at most 16 coefficients
+    const int nb = (a.P + kGB - 1) / kGB;
     switch (a.shs ? a.D : 0) {
-        case 0: k_gauss_bwd<0><<<nb, 256, 0, st>>>(a); break;
-        case 1: k_gauss_bwd<1><<<nb, 256, 0, st>>>(a); break;
-        case 2: k_gauss_bwd<2><<<nb, 256, 0, st>>>(a); break;
-        default: k_gauss_bwd<3><<<nb, 256, 0, st>>>(a); break;
+        case 0: k_gauss_bwd<0><<<nb, kGB, 0, st>>>(a); break;
+        case 1: k_gauss_bwd<1><<<nb, kGB, 0, st>>>(a); break;
+        case 2: k_gauss_bwd<2><<<nb, kGB, 0, st>>>(a); break;
+        default: k_gauss_bwd<3><<<nb, kGB, 0, st>>>(a); break;
     }
 }
 
