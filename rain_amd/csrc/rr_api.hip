@@ -136,6 +136,7 @@ struct Bin {
     void* keys;
     void* keys_sorted;
     uint32_t* vals;
+    uint32_t* first;  // first Gaussian of every duplicate window (= sort unit)
     void* temp;
     size_t temp_bytes;
     bool wide;  // 32-bit tile keys (T > 65536)
@@ -147,7 +148,7 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     Bin b;
     const int T = grid_x(W) * grid_y(H);
     b.wide = T > 65536;
-    b.bits = (int)higher_msb((uint32_t)T);
+    b.bits = std::max(1, (int)higher_msb((uint32_t)T));  // >= 1: the duplicate windows are sort units
     const size_t n = (size_t)std::max(L, 1);
     b.point_list = c.take<uint32_t>(n);
     if (b.wide) {
@@ -158,6 +159,9 @@ Bin carve_bin(void* buf, int L, int W, int H) {
         b.keys_sorted = c.take<uint16_t>(n);
     }
     b.vals = c.take<uint32_t>(n);
+    const RadixPlan pl = b.wide ? radix_sort_plan<uint32_t>(nullptr, (size_t)L, 0, b.bits)
+                                : radix_sort_plan<uint16_t>(nullptr, (size_t)L, 0, b.bits);
+    b.first = c.take<uint32_t>((size_t)std::max(pl.units, 1));
     b.temp_bytes = b.wide ? tile_sort_temp<uint32_t>(L, b.bits) : tile_sort_temp<uint16_t>(L, b.bits);
     b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
     b.total = align_up(c.off);
@@ -348,12 +352,19 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
     if (L > 0) {
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
-            if (bn.wide)
-                launch_duplicate<uint32_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull,
-                                           (uint32_t*)bn.keys, bn.vals, st);
-            else
-                launch_duplicate<uint16_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull,
-                                           (uint16_t*)bn.keys, bn.vals, st);
+            // windows of the duplicate kernel == units of the tile sort; it also writes the sort's
+            // first-pass digit counts
+            if (bn.wide) {
+                const RadixPlan pl = radix_sort_plan<uint32_t>(bn.temp, (size_t)L, 0, bn.bits);
+                launch_duplicate<uint32_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull, bn.first,
+                                           (uint32_t)pl.unit_items, pl.units, (uint32_t)L, (uint32_t*)bn.keys,
+                                           bn.vals, pl.dbits0, pl.counts, st);
+            } else {
+                const RadixPlan pl = radix_sort_plan<uint16_t>(bn.temp, (size_t)L, 0, bn.bits);
+                launch_duplicate<uint16_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull, bn.first,
+                                           (uint32_t)pl.unit_items, pl.units, (uint32_t)L, (uint16_t*)bn.keys,
+                                           bn.vals, pl.dbits0, pl.counts, st);
+            }
         }
         RR_STAGE_CHECK("duplicate");
         {
@@ -361,11 +372,11 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
             size_t tb = bn.temp_bytes;
             if (bn.wide)
                 RR_CHECK(radix_sort_pairs<uint32_t>(bn.temp, tb, (const uint32_t*)bn.keys, (uint32_t*)bn.keys_sorted,
-                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st),
+                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st, true),
                          "tile sort");
             else
                 RR_CHECK(radix_sort_pairs<uint16_t>(bn.temp, tb, (const uint16_t*)bn.keys, (uint16_t*)bn.keys_sorted,
-                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st),
+                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st, true),
                          "tile sort");
         }
         RR_STAGE_CHECK("tile sort");

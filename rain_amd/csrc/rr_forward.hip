@@ -2,7 +2,7 @@
 //
 //   k_preprocess<DEG>  one thread per Gaussian (forward.cu:144-246 semantics)
 //   k_gather_tiles     tile counts in depth order (input of the prefix sum)
-//   k_duplicate<K>     (tile, Gaussian) pairs in depth order, key = tile id only
+//   k_duplicate<K>     (tile, Gaussian) pairs in depth order, key = tile id only (LDS windows)
 //   k_ranges<K>        per-tile [start, end) in the tile-sorted list (rasterizer_impl.cu:105-127)
 //   k_blend_fwd        per-tile front-to-back alpha blend (forward.cu:251-369)
 //   k_mark_visible     frustum test (rasterizer_impl.cu:43-55)
@@ -120,43 +120,82 @@ __global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __r
     tiles_sorted[s] = tiles[idx_sorted[s]];
 }
 
+// First Gaussian (depth rank) of every window of `win` consecutive pairs: window k starts inside
+// the pair range [a, b) of exactly one Gaussian.
+__global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __restrict__ offsets, uint32_t win,
+                                                       int nwin, uint32_t* __restrict__ first) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P) return;
+    const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
+    if (a == b) return;
+    for (uint32_t k = (a + win - 1) / win; k <= (b - 1) / win && k < (uint32_t)nwin; k++) first[k] = (uint32_t)s;
+}
+
+// duplicateWithKeys (rasterizer_impl.cu:59-100), output-driven: workgroup k produces exactly the
+// pairs [k*win, (k+1)*win) of the depth-ordered pair list.  Its Gaussians (from first[k] on) emit
+// into an LDS window, which then leaves with coalesced stores — the per-Gaussian form scatters
+// every pair to its own cache line — and the window's histogram of the lowest `dbits` key bits is
+// written as the tile sort's first-pass digit counts (rr_sort.hip units == windows).
 template <typename K>
 __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __restrict__ idx_sorted,
                                                    const uint2* __restrict__ offsets,
                                                    const Splat* __restrict__ splats, const int* __restrict__ radii,
-                                                   int gx, int gy, int cull, K* __restrict__ keys,
-                                                   uint32_t* __restrict__ vals) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P) return;
-    const uint32_t g = idx_sorted[s];
-    const int r = radii[g];
-    if (r <= 0) return;
-    uint32_t off = s == 0 ? 0u : offsets[s - 1].x;
-    const uint32_t end = offsets[s].x;
-    if (off == end) return;
-    const float4 A = splats[g].a;
-    int x0, y0, x1, y1;
-    tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
-    if (cull) {
-        const float4 B = splats[g].b;
-        const float qmax = cull_qmax(B.y);  // identical inputs -> identical decisions to the count pass
-        for (int y = y0; y < y1; y++) {
-            int lo, hi;
-            cull_row_span(A.x, A.y, A.z, A.w, B.x, qmax, y, x0, x1, &lo, &hi);
-            for (int x = lo; x < hi && off < end; x++) {
-                keys[off] = (K)(y * gx + x);
-                vals[off] = g;
-                off++;
+                                                   int gx, int gy, int cull, const uint32_t* __restrict__ first,
+                                                   uint32_t win, uint32_t L, K* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals, int dbits,
+                                                   uint32_t* __restrict__ counts, int units) {
+    __shared__ K s_key[4096];
+    __shared__ uint32_t s_val[4096];
+    __shared__ uint32_t hist[256];
+    const int t = threadIdx.x;
+    const int ndig = 1 << dbits;
+    for (int d = t; d < ndig; d += 256) hist[d] = 0;
+    const uint32_t w0 = blockIdx.x * win, w1 = min(w0 + win, L);
+    const int s0 = (int)first[blockIdx.x];
+    for (int base = s0;; base += 256) {
+        const int s = base + t;
+        if (s < P) {
+            const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
+            const uint32_t lo = max(a, w0), hi = min(b, w1);
+            if (lo < hi) {
+                const uint32_t g = idx_sorted[s];
+                const int r = radii[g];
+                const float4 A = splats[g].a;
+                int x0, y0, x1, y1;
+                tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
+                const float qmax = cull ? cull_qmax(splats[g].b.y) : 0.f;
+                const float cz = cull ? splats[g].b.x : 0.f;
+                uint32_t pos = a;
+                for (int y = y0; y < y1 && pos < hi; y++) {
+                    int l = x0, h = x1;
+                    if (cull) cull_row_span(A.x, A.y, A.z, A.w, cz, qmax, y, x0, x1, &l, &h);
+                    const uint32_t c = h > l ? (uint32_t)(h - l) : 0u;
+                    if (pos + c <= lo) {  // row entirely before the window
+                        pos += c;
+                        continue;
+                    }
+                    for (int x = l; x < h && pos < hi; x++, pos++)
+                        if (pos >= lo) {
+                            s_key[pos - w0] = (K)(y * gx + x);
+                            s_val[pos - w0] = g;
+                        }
+                }
             }
         }
-    } else {
-        for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) {
-                keys[off] = (K)(y * gx + x);
-                vals[off] = g;
-                off++;
-            }
+        // another round only if this round's last Gaussian ends before the window does
+        const int last = min(base + 255, P - 1);
+        if (last >= P - 1 || offsets[last].x >= w1) break;
     }
+    __syncthreads();
+    const uint32_t mask = (uint32_t)ndig - 1u;
+    for (uint32_t j = t; j < w1 - w0; j += 256) {
+        const K k = s_key[j];
+        keys[w0 + j] = k;
+        vals[w0 + j] = s_val[j];
+        atomicAdd(&hist[(uint32_t)k & mask], 1u);
+    }
+    __syncthreads();
+    for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + blockIdx.x] = hist[d];
 }
 
 template <typename K>
@@ -205,15 +244,20 @@ void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint2* tiles, 
 }
 
 template <typename K>
-void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats,
-                      const int* radii, int gx, int gy, int cull, K* keys, uint32_t* vals, hipStream_t st) {
-    if (P == 0) return;
-    k_duplicate<K><<<blocks_for(P), 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, cull, keys, vals);
+void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats, const int* radii,
+                      int gx, int gy, int cull, uint32_t* first, uint32_t win, int nwin, uint32_t L, K* keys,
+                      uint32_t* vals, int dbits, uint32_t* counts, hipStream_t st) {
+    if (P == 0 || L == 0) return;
+    k_window_starts<<<blocks_for(P), 256, 0, st>>>(P, offsets, win, nwin, first);
+    k_duplicate<K><<<nwin, 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, cull, first, win, L, keys,
+                                          vals, dbits, counts, nwin);
 }
-template void launch_duplicate<uint16_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int,
-                                         int, uint16_t*, uint32_t*, hipStream_t);
-template void launch_duplicate<uint32_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int,
-                                         int, uint32_t*, uint32_t*, hipStream_t);
+template void launch_duplicate<uint16_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int, int,
+                                         uint32_t*, uint32_t, int, uint32_t, uint16_t*, uint32_t*, int, uint32_t*,
+                                         hipStream_t);
+template void launch_duplicate<uint32_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int, int,
+                                         uint32_t*, uint32_t, int, uint32_t, uint32_t*, uint32_t*, int, uint32_t*,
+                                         hipStream_t);
 
 template <typename K>
 void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st) {

@@ -85,8 +85,9 @@ struct GaussBwdArgs {
 void launch_preprocess(const PreArgs& a, hipStream_t st);
 void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint2* tiles, uint2* out, hipStream_t st);
 template <typename K>
-void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats,
-                      const int* radii, int gx, int gy, int cull, K* keys, uint32_t* vals, hipStream_t st);
+void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats, const int* radii,
+                      int gx, int gy, int cull, uint32_t* first, uint32_t win, int nwin, uint32_t L, K* keys,
+                      uint32_t* vals, int dbits, uint32_t* counts, hipStream_t st);
 template <typename K>
 void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
@@ -100,7 +101,17 @@ template <typename K>
 size_t radix_sort_temp_bytes(size_t n, int bits);
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
-                            uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st);
+                            uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
+                            bool first_counts_ready = false);
+// Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
+// can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass
+// first_counts_ready = true).
+struct RadixPlan {
+    uint32_t* counts;
+    int units, unit_items, rounds, dbits0;
+};
+template <typename K>
+RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
 
 }  // namespace rr

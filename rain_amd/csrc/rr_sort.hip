@@ -212,8 +212,24 @@ size_t radix_sort_temp_bytes(size_t n, int bits) {
 }
 
 template <typename K>
+RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
+    RadixPlan p{};
+    const int bits = end_bit - begin_bit;
+    if (n == 0 || bits <= 0) return p;
+    const SortLayout s = sort_layout<K>(temp, n, bits);
+    const int passes = (bits + 7) / 8;
+    p.rounds = rounds_for(n);
+    p.unit_items = 64 * kWaves * p.rounds;
+    p.units = (int)((n + p.unit_items - 1) / p.unit_items);
+    p.dbits0 = (bits + passes - 1) / passes;
+    p.counts = s.counts;
+    return p;
+}
+
+template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
-                            uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st) {
+                            uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
+                            bool first_counts_ready) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
     if (n > 0xffffffffull || bits <= 0 || bits > (int)(8 * sizeof(K))) return hipErrorInvalidValue;
@@ -235,7 +251,8 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
         uint32_t* vdst = to_out ? vals_out : s.vals_alt;
         if (!last && kdst == nullptr) return hipErrorInvalidValue;  // intermediate passes need key storage
         const size_t nc = ((size_t)1 << dbits) * (size_t)units;
-        k_rs_count<K><<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units);
+        if (!(p == 0 && first_counts_ready))
+            k_rs_count<K><<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units);
         size_t sb = s.scan_bytes;
         hipError_t e = rocprim::exclusive_scan(s.scan_temp, sb, s.counts, s.offsets, 0u, nc,
                                                rocprim::plus<uint32_t>(), st);
@@ -252,8 +269,10 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
 template size_t radix_sort_temp_bytes<uint16_t>(size_t, int);
 template size_t radix_sort_temp_bytes<uint32_t>(size_t, int);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
-                                               size_t, int, int, hipStream_t);
+                                               size_t, int, int, hipStream_t, bool);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
-                                               size_t, int, int, hipStream_t);
+                                               size_t, int, int, hipStream_t, bool);
+template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int);
+template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int);
 
 }  // namespace rr
