@@ -62,6 +62,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
                                                             const uint32_t* __restrict__ offsets, int units) {
     __shared__ uint32_t wcnt[kWaves][256];  // per-wave digit counts, then per-wave cursors
     __shared__ uint32_t dstart[256];        // block-local start of each digit's run
+    __shared__ uint32_t goff[256];          // global slot of block-local position 0 of each digit's run
     __shared__ uint32_t s_val[kMaxUnitItems];
     __shared__ K s_key[kMaxUnitItems];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -72,6 +73,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     // wave w owns the contiguous items [wbase, wbase + 64 * rounds) of the unit
     const size_t wbase = ubase + (size_t)w * 64 * rounds;
     for (int d = lane; d < ndig; d += 64) wcnt[w][d] = 0;
+    for (int d = t; d < ndig; d += 64 * kWaves) goff[d] = offsets[(size_t)d * units + unit];
     // the wave's items go to registers once (all loads in flight together); counting, ranking
     // and staging then run from registers
     K kr[kMaxRounds];
@@ -113,6 +115,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     }
     __syncthreads();
     if (t < ndig) {
+        goff[t] -= dstart[t];
         uint32_t run = dstart[t];
 #pragma unroll
         for (int v = 0; v < kWaves; v++) {
@@ -152,7 +155,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     for (int j = t; j < nu; j += 64 * kWaves) {
         const K k = s_key[j];
         const uint32_t d = ((uint32_t)k >> shift) & mask;
-        const uint32_t pos = offsets[(size_t)d * units + unit] + ((uint32_t)j - dstart[d]);
+        const uint32_t pos = goff[d] + (uint32_t)j;
         if (keys_out) keys_out[pos] = k;
         vals_out[pos] = s_val[j];
     }
