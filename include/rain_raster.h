@@ -116,6 +116,25 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
                       void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
                       int num_pairs, float* out_color, float* out_depth, void* stream);
 
+/* Optional fused optimizer step for RR_FLAG_RAW_PARAMS backwards (rr_grads.adam): Adam over the six
+ * GaussianModel parameter groups (gaussian_model.py:144-153), applied in the same pass that forms
+ * the gradients, so the gradients never travel through HBM.  Same arithmetic as rain_train.h's
+ * rt_adam_step / torch's fused Adam; the caller supplies each group's lr and bias corrections
+ * (1 - beta1^step, sqrt(1 - beta2^step)).  param must be the array passed as the matching input
+ * (means3D, shs, shs_rest, opacities, scales, rotations); it is updated in place. */
+typedef struct rr_adam_group {
+    float* param;
+    float* exp_avg;
+    float* exp_avg_sq;
+    double lr;
+    float bias_correction1;
+    float bias_correction2_sqrt;
+} rr_adam_group;
+typedef struct rr_adam {
+    rr_adam_group xyz, f_dc, f_rest, opacity, scaling, rotation;
+    double beta1, beta2, eps;
+} rr_adam;
+
 /* Gradient outputs of _C.rasterize_gaussians_backward (rasterize_points.cu:145-153,190).
  * All arrays are fully written (no pre-zeroing needed). */
 typedef struct rr_grads {
@@ -137,6 +156,8 @@ typedef struct rr_grads {
     float* grad_accum;    /* [P] */
     float* denom;         /* [P] */
     float* max_radii2D;   /* [P] */
+    /* RR_FLAG_RAW_PARAMS only, optional: apply Adam in place; the six gradient outputs may then be NULL */
+    const rr_adam* adam;
 } rr_grads;
 
 /*

@@ -44,10 +44,22 @@ class RRGaussians(ctypes.Structure):
                 ("cov3D_precomp", ctypes.c_void_p), ("shs_rest", ctypes.c_void_p)]
 
 
+class RRAdamGroup(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
+                ("lr", ctypes.c_double), ("bias_correction1", ctypes.c_float),
+                ("bias_correction2_sqrt", ctypes.c_float)]
+
+
+class RRAdam(ctypes.Structure):
+    _fields_ = [(n, RRAdamGroup) for n in ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")] + \
+               [("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double)]
+
+
 class RRGrads(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D",
                                                 "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations",
-                                                "dL_dsh_rest", "grad_accum", "denom", "max_radii2D")]
+                                                "dL_dsh_rest", "grad_accum", "denom", "max_radii2D")] + \
+               [("adam", ctypes.POINTER(RRAdam))]
 
 
 class RRFrameStats(ctypes.Structure):

@@ -413,11 +413,24 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
     if (!out || !dL_dpix || !radii || !geom_buffer || !image_buffer || !workspace)
         return fail(RR_ERR_ARG, "null buffer");
     const bool raw = (f->flags & RR_FLAG_RAW_PARAMS) != 0;
-    if (!out->dL_dopacity || !out->dL_dmeans3D || !out->dL_dscales || !out->dL_drotations ||
-        (f->M > 0 && !out->dL_dsh) ||
-        (!raw && (!out->dL_dmeans2D || !out->dL_dcolors || !out->dL_dcov3D)) ||
-        (raw && f->M > 1 && !out->dL_dsh_rest))
+    const rr_adam* ad = out->adam;
+    if (ad && !raw) return fail(RR_ERR_ARG, "the fused optimizer step needs raw-parameter mode");
+    if (ad) {
+        const rr_adam_group* gs[6] = {&ad->xyz, &ad->f_dc, &ad->f_rest, &ad->opacity, &ad->scaling, &ad->rotation};
+        const void* in[6] = {g->means3D, g->shs, g->shs_rest, g->opacities, g->scales, g->rotations};
+        for (int i = 0; i < 6; i++) {
+            if (i == 2 && f->M <= 1) continue;
+            if (!gs[i]->param || !gs[i]->exp_avg || !gs[i]->exp_avg_sq)
+                return fail(RR_ERR_ARG, "null Adam group array");
+            if (gs[i]->param != in[i]) return fail(RR_ERR_ARG, "Adam group param must be the matching input array");
+        }
+    } else if (!out->dL_dopacity || !out->dL_dmeans3D || !out->dL_dscales || !out->dL_drotations ||
+               (f->M > 0 && !out->dL_dsh) ||
+               (!raw && (!out->dL_dmeans2D || !out->dL_dcolors || !out->dL_dcov3D)) ||
+               (raw && f->M > 1 && !out->dL_dsh_rest)) {
         return fail(RR_ERR_ARG, "null gradient output");
+    }
+    if (!raw && !out->dL_dopacity) return fail(RR_ERR_ARG, "null gradient output");
     if (out->grad_accum && (!raw || !out->denom || !out->max_radii2D))
         return fail(RR_ERR_ARG, "densification statistics need raw mode and grad_accum, denom, max_radii2D");
     if (workspace_bytes < rr_backward_workspace_bytes(P)) return fail(RR_ERR_CAPACITY, "workspace too small");
@@ -460,6 +473,8 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
         a.raw = raw ? 1 : 0; a.opacities = g->opacities; a.shs_rest = g->shs_rest;
         a.dL_dsh_rest = out->dL_dsh_rest;
         a.grad_accum = out->grad_accum; a.denom = out->denom; a.max_radii2D = out->max_radii2D;
+        a.use_adam = ad ? 1 : 0;
+        if (ad) a.adam = *ad;  // by value: the kernel must not dereference host memory
         launch_gauss_bwd(a, st);
     }
     RR_STAGE_CHECK("gaussian backward");

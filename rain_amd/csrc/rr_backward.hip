@@ -5,6 +5,7 @@
 //                      cov3D bwd :268-331) fused, writing every gradient output exactly once
 //                      (so the host allocates them uninitialised — no zero-fill pass).  It consumes
 //                      the per-Gaussian accumulators the blend backward (rr_blend.hip) filled.
+#include "adam_math.hpp"
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
@@ -88,32 +89,115 @@ __device__ __forceinline__ void sh_coeff_grads(v3 dir, v3 dL_dRGB, float* row, i
     for (int i = 3 * K; i < 3 * M; i++) row[i] = 0.f;
 }
 
+// The 11 per-Gaussian gradients of the small groups (xyz 3, opacity 1, scaling 3, rotation 4),
+// kept in registers so that the fused Adam step can batch its loads (rr_grads.adam).
+struct SmallGrads {
+    float v[11];
+};
+__device__ __forceinline__ void put(float* grad, size_t e, float g) {
+    if (grad) grad[e] = g;
+}
+
+// Adam over n elements whose (param, moment) addresses are given: all loads first, then the
+// math, then the stores (the compiler cannot batch them itself: the arrays may alias).
+template <int N>
+__device__ __forceinline__ void adam_batch(const GaussBwdArgs& a, float* const (&pp)[N], float* const (&mp)[N],
+                                           float* const (&vp)[N], const float (&g)[N], const rr_adam_group* const (&gr)[N]) {
+    float p[N], m[N], v[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        p[i] = *pp[i];
+        m[i] = *mp[i];
+        v[i] = *vp[i];
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        adam_elem(p[i], g[i], m[i], v[i], gr[i]->lr, gr[i]->bias_correction1, gr[i]->bias_correction2_sqrt,
+                  a.adam.beta1, a.adam.beta2, a.adam.eps);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        *pp[i] = p[i];
+        *mp[i] = m[i];
+        *vp[i] = v[i];
+    }
+}
+
+__device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const SmallGrads& sg) {
+    const rr_adam& ad = a.adam;
+    const rr_adam_group* gr[11];
+    size_t e[11];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        gr[i] = &ad.xyz;
+        e[i] = 3 * (size_t)idx + i;
+        gr[4 + i] = &ad.scaling;
+        e[4 + i] = 3 * (size_t)idx + i;
+    }
+    gr[3] = &ad.opacity;
+    e[3] = idx;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        gr[7 + i] = &ad.rotation;
+        e[7 + i] = 4 * (size_t)idx + i;
+    }
+    float* pp[11];
+    float* mp[11];
+    float* vp[11];
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        pp[i] = gr[i]->param + e[i];
+        mp[i] = gr[i]->exp_avg + e[i];
+        vp[i] = gr[i]->exp_avg_sq + e[i];
+    }
+    adam_batch<11>(a, pp, mp, vp, sg.v, gr);
+}
+
 // One Gaussian.  `row` is this thread's LDS row holding its SH coefficients (staged by the
 // kernel; coefficient k at row[3k..3k+2]) and receiving its SH gradients in the same layout; it is
 // nullptr when there are neither SH inputs nor SH gradients.
 template <int DEG>
-__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* row) {
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* row, SmallGrads& sg) {
     const int M = a.M;
     float* dmean2 = a.dL_dmeans2D ? a.dL_dmeans2D + 3 * (size_t)idx : nullptr;
     float* dcol = a.dL_dcolors ? a.dL_dcolors + 3 * (size_t)idx : nullptr;
-    float* dmean3 = a.dL_dmeans3D + 3 * (size_t)idx;
     float* dcov = a.dL_dcov3D ? a.dL_dcov3D + 6 * (size_t)idx : nullptr;
-    float* dscale = a.dL_dscales + 3 * (size_t)idx;
-    float4* drot = reinterpret_cast<float4*>(a.dL_drot) + idx;
+    // small-group gradients: written out if requested, and kept in sg for the fused Adam step
+    auto emit3 = [&](float* out, int slot, v3 g) {
+        sg.v[slot] = g.x;
+        sg.v[slot + 1] = g.y;
+        sg.v[slot + 2] = g.z;
+        put(out, 3 * (size_t)idx + 0, g.x);
+        put(out, 3 * (size_t)idx + 1, g.y);
+        put(out, 3 * (size_t)idx + 2, g.z);
+    };
+    auto emit_rot = [&](float4 g) {
+        sg.v[7] = g.x;
+        sg.v[8] = g.y;
+        sg.v[9] = g.z;
+        sg.v[10] = g.w;
+        put(a.dL_drot, 4 * (size_t)idx + 0, g.x);
+        put(a.dL_drot, 4 * (size_t)idx + 1, g.y);
+        put(a.dL_drot, 4 * (size_t)idx + 2, g.z);
+        put(a.dL_drot, 4 * (size_t)idx + 3, g.w);
+    };
+    auto emit_op = [&](float g) {
+        sg.v[3] = g;
+        put(a.dL_dopacity, idx, g);
+    };
 
     const int radius = a.radii[idx];
     if (!(radius > 0)) {  // untouched Gaussians: exact zeros (backward.cu:146,357)
         if (dmean2) dmean2[0] = dmean2[1] = dmean2[2] = 0.f;
         if (dcol) dcol[0] = dcol[1] = dcol[2] = 0.f;
-        a.dL_dopacity[idx] = 0.f;
-        dmean3[0] = dmean3[1] = dmean3[2] = 0.f;
+        emit_op(0.f);
+        emit3(a.dL_dmeans3D, 0, mk(0.f, 0.f, 0.f));
         if (dcov)
 #pragma unroll
             for (int i = 0; i < 6; i++) dcov[i] = 0.f;
         if (row)
             for (int i = 0; i < 3 * M; i++) row[i] = 0.f;
-        dscale[0] = dscale[1] = dscale[2] = 0.f;
-        *drot = make_float4(0.f, 0.f, 0.f, 0.f);
+        emit3(a.dL_dscales, 4, mk(0.f, 0.f, 0.f));
+        emit_rot(make_float4(0.f, 0.f, 0.f, 0.f));
         return;
     }
 
@@ -135,9 +219,9 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     }
     if (a.raw) {  // sigmoid backward (torch: grad * (1 - y) * y)
         const float o = act_opacity(a.opacities[idx]);
-        a.dL_dopacity[idx] = gb.y * (1.0f - o) * o;
+        emit_op(gb.y * (1.0f - o) * o);
     } else {
-        a.dL_dopacity[idx] = gb.y;
+        emit_op(gb.y);
     }
     if (a.grad_accum) {  // densification statistics (gaussian_model.py:419-421, train.py:133)
         a.grad_accum[idx] += sqrtf(dm2x * dm2x + dm2y * dm2y);
@@ -254,9 +338,7 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     } else if (row) {
         for (int i = 0; i < 3 * M; i++) row[i] = 0.f;
     }
-    dmean3[0] = dmean.x;
-    dmean3[1] = dmean.y;
-    dmean3[2] = dmean.z;
+    emit3(a.dL_dmeans3D, 0, dmean);
 
     // ---- cov3D bwd (backward.cu:268-331) ----
     if (a.scales) {
@@ -282,9 +364,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 #pragma unroll
         for (int i = 0; i < 3; i++) ds[i] = R[0][i] * dM[i][0] + R[1][i] * dM[i][1] + R[2][i] * dM[i][2];
         // raw mode: exp backward (torch: grad * result)
-        dscale[0] = a.raw ? ds[0] * scale.x : ds[0];
-        dscale[1] = a.raw ? ds[1] * scale.y : ds[1];
-        dscale[2] = a.raw ? ds[2] * scale.z : ds[2];
+        emit3(a.dL_dscales, 4,
+              a.raw ? mk(ds[0] * scale.x, ds[1] * scale.y, ds[2] * scale.z) : mk(ds[0], ds[1], ds[2]));
         float Gm[3][3];
 #pragma unroll
         for (int i = 0; i < 3; i++)
@@ -307,10 +388,10 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
             const float c = n >= 1e-12f ? -gx / (nd * nd) / n : 0.f;
             dq = make_float4(dq.x / nd + x.x * c, dq.y / nd + x.y * c, dq.z / nd + x.z * c, dq.w / nd + x.w * c);
         }
-        *drot = dq;
+        emit_rot(dq);
     } else {
-        dscale[0] = dscale[1] = dscale[2] = 0.f;
-        *drot = make_float4(0.f, 0.f, 0.f, 0.f);
+        emit3(a.dL_dscales, 4, mk(0.f, 0.f, 0.f));
+        emit_rot(make_float4(0.f, 0.f, 0.f, 0.f));
     }
 }
 
@@ -328,7 +409,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     const int i0 = blockIdx.x * kGB;
     const int nvalid = min(kGB, a.P - i0);
     const int M = a.M, nf = 3 * M;  // floats per Gaussian
-    const bool stage = M > 0 && (a.shs != nullptr || a.dL_dsh != nullptr);
+    const bool stage = M > 0 && (a.shs != nullptr || a.dL_dsh != nullptr || a.use_adam);
     if (stage && a.shs) {
         // flat, coalesced loads of the block's coefficient region(s), all in flight at once, then
         // scattered into the padded LDS rows; j = e / w via a float reciprocal (exact: e < 2^13)
@@ -358,22 +439,65 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
         }
     }
     __syncthreads();
-    if (t < nvalid) gauss_bwd_one<DEG>(a, i0 + t, stage ? s_sh + t * kShStride : nullptr);
+    if (t < nvalid) {
+        SmallGrads sg;
+        gauss_bwd_one<DEG>(a, i0 + t, stage ? s_sh + t * kShStride : nullptr, sg);
+        if (a.use_adam) adam_small(a, i0 + t, sg);
+    }
     __syncthreads();
-    if (stage && a.dL_dsh) {
-        auto stage_out = [&](float* dst, int w, int koff) {
+    if (stage && (a.dL_dsh || a.use_adam)) {
+        // gradients leave coalesced; with the fused step the SH groups' Adam runs here, on the
+        // same flat element order
+        auto stage_out = [&](float* dst, const rr_adam_group* grp, int w, int koff) {
             const int total = nvalid * w;
             const float inv = 1.0f / (float)w;
-            for (int e = t; e < total; e += kGB) {
-                const int j = (int)(((float)e + 0.5f) * inv);
-                dst[(size_t)i0 * w + e] = s_sh[j * kShStride + koff + (e - j * w)];
+            constexpr int kB = 8;  // Adam elements per batch of loads
+            for (int e0 = t; e0 < total; e0 += kB * kGB) {
+                float g[kB];
+                float* pp[kB];
+                float* mp[kB];
+                float* vp[kB];
+                const rr_adam_group* gr[kB];
+                int n = 0;
+#pragma unroll
+                for (int q = 0; q < kB; q++) {
+                    const int e = e0 + q * kGB;
+                    const bool ok = e < total;
+                    const int ee = ok ? e : e0;  // e0 < total: a valid dummy for the unused lanes of the batch
+                    const int j = (int)(((float)ee + 0.5f) * inv);
+                    g[q] = s_sh[j * kShStride + koff + (ee - j * w)];
+                    const size_t ge = (size_t)i0 * w + ee;
+                    if (ok) put(dst, ge, g[q]);
+                    n += ok;
+                    if (grp) {
+                        pp[q] = grp->param + ge;
+                        mp[q] = grp->exp_avg + ge;
+                        vp[q] = grp->exp_avg_sq + ge;
+                        gr[q] = grp;
+                    }
+                }
+                if (grp) {
+                    if (n == kB) {
+                        adam_batch<kB>(a, pp, mp, vp, g, gr);
+                    } else {  // tail: one at a time, never touching an element twice
+                        for (int q = 0; q < n; q++) {
+                            float p = *pp[q], m = *mp[q], v = *vp[q];
+                            adam_elem(p, g[q], m, v, grp->lr, grp->bias_correction1, grp->bias_correction2_sqrt,
+                                      a.adam.beta1, a.adam.beta2, a.adam.eps);
+                            *pp[q] = p;
+                            *mp[q] = m;
+                            *vp[q] = v;
+                        }
+                    }
+                }
             }
         };
+        const rr_adam* ad = a.use_adam ? &a.adam : nullptr;
         if (!a.raw) {
-            stage_out(a.dL_dsh, nf, 0);
+            stage_out(a.dL_dsh, nullptr, nf, 0);
         } else {
-            stage_out(a.dL_dsh, 3, 0);
-            if (nf > 3) stage_out(a.dL_dsh_rest, nf - 3, 3);
+            stage_out(a.dL_dsh, ad ? &ad->f_dc : nullptr, 3, 0);
+            if (nf > 3) stage_out(a.dL_dsh_rest, ad ? &ad->f_rest : nullptr, nf - 3, 3);
         }
     }
 }

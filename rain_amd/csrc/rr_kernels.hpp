@@ -1,6 +1,7 @@
 // rr_kernels.hpp — kernel argument blocks and host launchers shared by the .hip units.
 #pragma once
 #include "rr_common.hpp"
+#include "../../include/rain_raster.h"
 
 namespace rr {
 
@@ -80,6 +81,10 @@ struct GaussBwdArgs {
     float* grad_accum;
     float* denom;
     float* max_radii2D;
+    // fused optimizer step (raw mode): copied BY VALUE into the kernel arguments (the caller's
+    // rr_adam lives in host memory); use_adam says whether it is valid
+    rr_adam adam;
+    int use_adam;
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);

@@ -12,6 +12,7 @@
 #include <string>
 
 #include "../../include/rain_train.h"
+#include "adam_math.hpp"
 
 namespace {
 
@@ -43,16 +44,6 @@ struct AdamArgs {
     int n_groups;
     double beta1, beta2, eps;
 };
-
-// one element, exactly adam_math<float, float, 4, ORIGINAL, false> (fused_adam_utils.cuh)
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, double lr, float bc1, float bc2s,
-                                          double b1, double b2, double eps) {
-    m = (float)(b1 * (double)m + (1.0 - b1) * (double)g);
-    v = (float)(b2 * (double)v + (1.0 - b2) * (double)g * (double)g);
-    const float step_size = (float)(lr / (double)bc1);
-    const float denom = (float)((double)(sqrtf(v) / bc2s) + eps);
-    p -= step_size * m / denom;
-}
 
 __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
     const int b = blockIdx.x;

@@ -92,21 +92,29 @@ def forward(model, camera, bg: torch.Tensor, low_pass: float, scale_modifier: fl
     return color, radii, depth, st
 
 
-def backward(st: RawFrame, dL_dpix: torch.Tensor, grads: dict, stats: tuple | None = None):
+def backward(st: RawFrame, dL_dpix: torch.Tensor, grads: dict | None, stats: tuple | None = None,
+             adam: "N.RRAdam | None" = None):
     """Write dLoss/d(raw parameter) into grads['xyz'|'f_dc'|'f_rest'|'opacity'|'scaling'|'rotation']
     (contiguous fp32 tensors of the parameter shapes, fully overwritten) and, if `stats` =
     (grad_accum [P,1], denom [P,1], max_radii2D [P]) is given, update the densification statistics
-    in place for every Gaussian with radii > 0."""
+    in place for every Gaussian with radii > 0.  With `adam` (rain_amd.optim.FusedAdam.fused_step)
+    the optimizer step is applied to the parameters in the same pass and `grads` may be None."""
     if st.P == 0:
         return
     L = N.raster()
     dpix = dL_dpix.contiguous()
-    for k in ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"):
-        if not grads[k].is_contiguous():
+    names = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+    if grads is None:
+        if adam is None:
+            raise RuntimeError("rain_amd.fused.backward: nothing to do (no gradients requested, no optimizer step)")
+        grads = dict.fromkeys(names)
+    for k in names:
+        if grads[k] is not None and not grads[k].is_contiguous():
             raise RuntimeError(f"rain_amd.fused: grads[{k!r}] must be contiguous")
     acc, den, mr = stats if stats is not None else (None, None, None)
     out = N.RRGrads(None, None, _p(grads["opacity"]), _p(grads["xyz"]), None, _p(grads["f_dc"]),
-                    _p(grads["scaling"]), _p(grads["rotation"]), _p(grads["f_rest"]), _p(acc), _p(den), _p(mr))
+                    _p(grads["scaling"]), _p(grads["rotation"]), _p(grads["f_rest"]), _p(acc), _p(den), _p(mr),
+                    ctypes.pointer(adam) if adam is not None else None)
     dev = dpix.device
     ws = torch.empty((L.rr_backward_workspace_bytes(st.P),), dtype=torch.uint8, device=dev)
     N.check(L.rr_backward(ctypes.byref(st.frame), ctypes.byref(st.cam), ctypes.byref(st.gs), _p(st.radii),

@@ -25,6 +25,50 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, defaults)
         N.train_lib()  # fail loudly now if the native library is missing
 
+    def _param_group(self, p):
+        for g in self.param_groups:
+            for q in g["params"]:
+                if q is p:
+                    return g
+        raise KeyError("parameter is not managed by this optimizer")
+
+    @torch.no_grad()
+    def fused_step(self, model):
+        """Book-keeping of one Adam step over the six GaussianModel groups done by the backward
+        kernel itself (include/rain_raster.h rr_adam): advances each parameter's step count exactly
+        as step() would and returns the rr_adam block (lrs, bias corrections, moment buffers)."""
+        names = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+        params = (model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
+                  model._rotation)
+        ad = N.RRAdam()
+        betas = None
+        for name, p in zip(names, params):
+            group = self._param_group(p)
+            b1, b2 = group["betas"]
+            if betas is None:
+                betas = (float(b1), float(b2), float(group["eps"]))
+            elif betas != (float(b1), float(b2), float(group["eps"])):
+                raise RuntimeError("rain_amd FusedAdam.fused_step: all groups must share betas and eps")
+            state = self.state[p]
+            if len(state) == 0:
+                state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            stp = state["step"]
+            if stp.device.type != "cpu":
+                stp = state["step"] = stp.detach().to("cpu", torch.float32)
+            stp += 1.0
+            k = float(stp.item())
+            g = getattr(ad, name)
+            g.param = p.data_ptr()
+            g.exp_avg = state["exp_avg"].data_ptr()
+            g.exp_avg_sq = state["exp_avg_sq"].data_ptr()
+            g.lr = float(group["lr"])
+            g.bias_correction1 = 1.0 - math.pow(b1, k)
+            g.bias_correction2_sqrt = math.sqrt(1.0 - math.pow(b2, k))
+        ad.beta1, ad.beta2, ad.eps = betas
+        return ad
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

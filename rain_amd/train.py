@@ -121,7 +121,17 @@ class Trainer:
             self.low_pass = 0.3
         return vidx, cam
 
-    def _densify_and_adam(self, iteration):
+    def _events(self, iteration):
+        """(densify/prune now, opacity reset now) — train.py:136-143."""
+        opt, cfg = self.opt, self.cfg
+        if iteration >= opt.densify_until_iter:
+            return False, False
+        densify = cfg.densify and iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0
+        reset = iteration % opt.opacity_reset_interval == 0 or (cfg.white_background and
+                                                                 iteration == opt.densify_from_iter)
+        return densify, reset
+
+    def _densify_and_adam(self, iteration, adam_done=False):
         g, opt, cfg = self.g, self.opt, self.cfg
         densified = False
         if iteration < opt.densify_until_iter:
@@ -134,7 +144,7 @@ class Trainer:
             if iteration % opt.opacity_reset_interval == 0 or (cfg.white_background and
                                                                iteration == opt.densify_from_iter):
                 g.reset_opacity()
-        if iteration < opt.iterations:
+        if iteration < opt.iterations and not adam_done:
             # after densify_and_prune the parameters are new tensors with grad None, so this step
             # skips them, exactly as the reference's optimizer.step() does (train.py:145-147)
             g.optimizer.step()
@@ -154,16 +164,23 @@ class Trainer:
         vidx, cam = self._low_pass_and_view(iteration)
         P = g.get_xyz.shape[0]
         densify_phase = iteration < opt.densify_until_iter
+        # Single GPU, and no densify/prune or opacity reset this iteration (they replace parameter
+        # tensors before the reference's optimizer.step()): the Adam step runs inside the backward
+        # kernel and the gradients never exist in HBM.
+        densify_now, reset_now = self._events(iteration)
+        fuse_adam = (self.world == 1 and iteration < opt.iterations and not densify_now and not reset_now
+                     and hasattr(g.optimizer, "fused_step"))
         extra = 2 * P if (self.world > 1 and densify_phase) else 0
-        flat = g.bind_flat_grad(extra=extra, zero=False)  # the backward overwrites every gradient
+        flat = None if fuse_adam else g.bind_flat_grad(extra=extra, zero=False)  # backward overwrites all grads
         with torch.no_grad():
             image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass)
             gt = self.gt[vidx]
             loss, _parts, lws = l1_ssim_forward(image, gt, opt.lambda_dssim)
             dimg = l1_ssim_backward(image, gt, opt.lambda_dssim, lws)
-            grads = dict(xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad,
-                         opacity=g._opacity.grad, scaling=g._scaling.grad, rotation=g._rotation.grad)
-            nparam = flat.numel() - extra
+            grads = None if fuse_adam else dict(
+                xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad, opacity=g._opacity.grad,
+                scaling=g._scaling.grad, rotation=g._rotation.grad)
+            nparam = None if flat is None else flat.numel() - extra
             stats = None
             local_max = None
             if densify_phase:
@@ -172,7 +189,7 @@ class Trainer:
                     stats = (flat[nparam:nparam + P], flat[nparam + P:], local_max)
                 else:
                     stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D)
-            fused.backward(st, dimg, grads, stats)
+            fused.backward(st, dimg, grads, stats, adam=g.optimizer.fused_step(g) if fuse_adam else None)
             if self.world > 1:
                 dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
                 flat[:nparam].mul_(1.0 / self.world)
@@ -181,7 +198,7 @@ class Trainer:
                     g.max_radii2D = local_max
                     g.xyz_gradient_accum += flat[nparam:nparam + P].unsqueeze(1)
                     g.denom += flat[nparam + P:].unsqueeze(1)
-            densified = self._densify_and_adam(iteration)
+            densified = self._densify_and_adam(iteration, adam_done=fuse_adam)
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
                         view=vidx, low_pass=self.low_pass, densified=densified)
 

@@ -140,3 +140,35 @@ def test_fused_trainer_matches_autograd_trainer(gpu):
     assert rel_l1(ga.xyz_gradient_accum, gb.xyz_gradient_accum) < 1e-4
     assert torch.equal(ga.denom, gb.denom)
     assert torch.equal(ga.max_radii2D, gb.max_radii2D)
+
+
+def test_adam_fused_into_backward_matches_separate_step(gpu):
+    """rr_grads.adam: the optimizer step applied inside the backward kernel equals gradients written
+    out + FusedAdam.step() (which tests above pin to torch's Adam)."""
+    P, W, H = 20_000, 160, 120
+    cam = cameras.fibonacci_cameras(8, W, H)[2].to("cuda")
+    bg = torch.zeros(3, device="cuda")
+    gt = torch.rand(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(9))
+    models = []
+    for fuse in (False, True):
+        g = _model(P, 3, 3, seed=4)
+        g.training_setup(OptimizationParams())
+        for it in range(3):  # a few steps so the moments are non-trivial
+            color, radii, depth, st = fused.forward(g, cam, bg, 0.3)
+            _, _, ws = l1_ssim_forward(color, gt, 0.2)
+            dimg = l1_ssim_backward(color, gt, 0.2, ws)
+            if fuse:
+                fused.backward(st, dimg, None, None, adam=g.optimizer.fused_step(g))
+            else:
+                g.bind_flat_grad()
+                fused.backward(st, dimg, {k: v.grad for k, v in _params(g).items()}, None)
+                g.optimizer.step()
+        models.append(g)
+    a, b = models
+    for k in NAMES:
+        x, y = _params(a)[k].detach(), _params(b)[k].detach()
+        assert (x - y).abs().max() <= 1e-6 * max(1.0, float(y.abs().max())), (k, float((x - y).abs().max()))
+    for pa, pb in zip(a.params(), b.params()):
+        sa, sb = a.optimizer.state[pa], b.optimizer.state[pb]
+        assert float(sa["step"]) == float(sb["step"]) == 3.0
+        assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-4, atol=1e-12)
