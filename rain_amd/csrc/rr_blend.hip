@@ -1,4 +1,5 @@
-// rr_blend.hip — per-tile alpha blending, forward and backward (forward.cu:251-369, backward.cu:389-547).
+// rr_blend.hip — per-tile alpha blending backward (backward.cu:389-547); the forward blend lives in
+// rr_blend_fwd.hip (packed fp32 math, compiled with packed ops enabled).
 //
 // CDNA4 mapping.  A 16x16 tile is processed by NW wave64s (NW = 1, 2 or 4, chosen per kernel at
 // run time, see rr_set_blend_config), each lane owning PPL = 4/NW pixels of one column: thread t
@@ -24,143 +25,6 @@
 #include "rr_kernels.hpp"
 
 namespace rr {
-
-// Prefetch of one Splat record into three float4 registers.  Plain float4 variables: keeping
-// the prefetched record in a struct made hipcc place it in scratch (private memory).
-__device__ __forceinline__ void load_splat(const Splat* __restrict__ s, uint32_t i, float4& a, float4& b, float4& c) {
-    const float4* p = reinterpret_cast<const float4*>(s + i);
-    a = p[0];
-    b = p[1];
-    c = p[2];
-}
-
-// 1/x from v_rcp_f32 (1 ulp) refined by one Newton step (~0.5 ulp): 4 VALU ops instead of the
-// ~10-op IEEE division sequence hipcc emits for '/' and __fdividef.  x = 1 - alpha is in [0.01, 1).
-__device__ __forceinline__ float rcp_nr(float x) {
-    const float r = __builtin_amdgcn_rcpf(x);
-    return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.0f), r);
-}
-
-// Bijective block -> tile remap (cdna_hip_programming.md §5, "XCD swizzle must be bijective").
-__device__ __forceinline__ int xcd_tile(int b, int n) {
-    const int q = n >> 3, r = n & 7;
-    const int x = b & 7, s = b >> 3;
-    return x < r ? x * (q + 1) + s : r * (q + 1) + (x - r) * q + s;
-}
-
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
-    constexpr int PPL = 4 / NW;
-    constexpr int B = 64 * NW;
-    const int ntiles = a.gx * a.gy;
-    const int tile = xcd_tile(blockIdx.x, ntiles);
-    const int tx = tile % a.gx, ty = tile / a.gx;
-    const int t = threadIdx.x;
-    const int lane = t & 63, w = t >> 6;
-    const int px = tx * TILE_X + (lane & 15);
-    const int py0 = ty * TILE_Y + (lane >> 4) + 4 * w * PPL;
-    const float pfx = (float)px;
-
-    __shared__ float4 s_a[B];
-    __shared__ float4 s_b[B];
-    __shared__ float4 s_c[B];
-
-    float T[PPL], C0[PPL], C1[PPL], C2[PPL], Dp[PPL];
-    uint32_t contrib[PPL], last[PPL];
-    bool done[PPL];
-#pragma unroll
-    for (int q = 0; q < PPL; q++) {
-        T[q] = 1.0f;
-        C0[q] = C1[q] = C2[q] = Dp[q] = 0.f;
-        contrib[q] = last[q] = 0;
-        done[q] = !(px < a.W && py0 + 4 * q < a.H);
-    }
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-
-    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
-    if (t < n) load_splat(a.splats, a.point_list[range.x + t], na, nb, nc);
-    for (int base = 0; base < n; base += B) {
-        bool my_done = true;
-#pragma unroll
-        for (int q = 0; q < PPL; q++) my_done = my_done && done[q];
-        if (__syncthreads_count(my_done) == B) break;
-        if (base + t < n) {
-            s_a[t] = na;
-            s_b[t] = nb;
-            s_c[t] = nc;
-        }
-        __syncthreads();
-        if (base + B + t < n) load_splat(a.splats, a.point_list[range.x + base + B + t], na, nb, nc);  // next round
-        const int cnt = min(B, n - base);
-        for (int j = 0; j < cnt; j++) {
-            if (__all(my_done)) break;
-            const float4 A = s_a[j];
-            const float4 Bv = s_b[j];
-#pragma unroll
-            for (int q = 0; q < PPL; q++) {
-                if (!done[q]) {
-                    contrib[q]++;
-                    const float dx = A.x - pfx, dy = A.y - (float)(py0 + 4 * q);
-                    const float power = -0.5f * (A.z * dx * dx + Bv.x * dy * dy) - A.w * dx * dy;
-                    if (power <= 0.0f) {
-                        const float alpha = fminf(0.99f, Bv.y * __expf(power));
-                        if (alpha >= 1.0f / 255.0f) {
-                            const float test_T = T[q] * (1 - alpha);
-                            if (test_T < 0.0001f) {
-                                done[q] = true;
-                            } else {
-                                const float4 Cc = s_c[j];
-                                C0[q] += Cc.x * alpha * T[q];
-                                C1[q] += Cc.y * alpha * T[q];
-                                C2[q] += Cc.z * alpha * T[q];
-                                Dp[q] += Bv.z * alpha * T[q];
-                                T[q] = test_T;
-                                last[q] = contrib[q];
-                            }
-                        }
-                    }
-                }
-            }
-            my_done = true;
-#pragma unroll
-            for (int q = 0; q < PPL; q++) my_done = my_done && done[q];
-        }
-        __syncthreads();
-    }
-
-    uint32_t m = 0;
-    const size_t HW = (size_t)a.H * a.W;
-#pragma unroll
-    for (int q = 0; q < PPL; q++) {
-        const int py = py0 + 4 * q;
-        if (px < a.W && py < a.H) {
-            m = max(m, last[q]);
-            const int pix = a.W * py + px;
-            a.final_T[pix] = T[q];
-            a.n_contrib[pix] = last[q];
-            a.out_color[pix] = C0[q] + T[q] * a.bg[0];
-            a.out_color[HW + pix] = C1[q] + T[q] * a.bg[1];
-            a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
-            a.out_depth[pix] = Dp[q];
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    if (NW == 1) {
-        if (lane == 0) a.tile_max[tile] = m;
-    } else {
-        __shared__ uint32_t s_m[NW];
-        if (lane == 0) s_m[w] = m;
-        __syncthreads();
-        if (t == 0) {
-            uint32_t mm = s_m[0];
-#pragma unroll
-            for (int i = 1; i < NW; i++) mm = max(mm, s_m[i]);
-            a.tile_max[tile] = mm;
-        }
-    }
-}
 
 // OCC: minimum waves per SIMD requested from the register allocator (4 caps k_blend_bwd<1> at
 // 128 VGPRs, a few spills in the per-round flush; 1 = compiler's choice, 132 VGPRs / 3 waves).
@@ -238,8 +102,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
 #pragma unroll
             for (int q = 0; q < PPL; q++) {
                 const float dx = A.x - pfx, dy = A.y - (float)(py0 + 4 * q);
-                const float power = -0.5f * (A.z * dx * dx + Bv.x * dy * dy) - A.w * dx * dy;
-                const float G = __expf(power);
+                const float power = blend_power(A, Bv, dx, dy);  // identical to the forward's value
+                const float G = blend_G(power);
                 const float alpha = fminf(0.99f, Bv.y * G);
                 const bool act = contributor < last[q] && power <= 0.0f && alpha >= 1.0f / 255.0f;
                 if (act) {
@@ -307,8 +171,9 @@ int env_waves(const char* name, int dflt) {
 }
 }  // namespace
 
-// Defaults: measured on MI355X (profiles/, DESIGN.md §Blend kernels).
-constexpr int kFwdWavesDefault = 4;
+// Defaults: measured on MI355X (profiles/, DESIGN.md §Blend kernels).  The forward blend
+// (rr_blend_fwd.hip) runs 1 or 2 waves per tile (4 or 2 pixels per lane, packed in pairs).
+constexpr int kFwdWavesDefault = 2;
 constexpr int kBwdWavesDefault = 1;
 
 void set_blend_config(int fwd_waves, int bwd_waves) {
@@ -316,15 +181,9 @@ void set_blend_config(int fwd_waves, int bwd_waves) {
     g_bwd_waves = bwd_waves;
 }
 
-void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
-    const int T = a.gx * a.gy;
-    if (T == 0) return;
+int blend_fwd_waves() {
     const int nw = g_fwd_waves ? g_fwd_waves : env_waves("RAIN_BLEND_FWD_WAVES", kFwdWavesDefault);
-    switch (nw) {
-        case 1: k_blend_fwd<1><<<T, 64, 0, st>>>(a); break;
-        case 2: k_blend_fwd<2><<<T, 128, 0, st>>>(a); break;
-        default: k_blend_fwd<4><<<T, 256, 0, st>>>(a); break;
-    }
+    return nw == 1 ? 1 : 2;
 }
 
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {

@@ -1,0 +1,166 @@
+// rr_blend_fwd.hip — per-tile front-to-back alpha blend, forward (forward.cu:251-369).
+//
+// The kernel is VALU-issue bound (SQ counters: the SIMDs issue a VALU op nearly every cycle), so
+// it is written for CDNA4's packed fp32 pipe: every lane owns PAIRS x 2 pixels of one column and
+// evaluates each pair of pixels with v_pk_{fma,mul,add}_f32 (one instruction, two pixels).  The
+// two pixels of a pair share dx (same column), so the x-terms of the falloff are scalar.
+//
+// Layout: NW wave64s per 16x16 tile (NW = 2: one pixel pair per lane; NW = 1: two pairs), lane l
+// of wave w owns column l%16 and rows l/16 + 4k, k in the wave's share of {0,1,2,3}; pair p holds
+// rows (l/16 + 8p' + {0, 4}) with p' = w * PAIRS + p.
+//   * Each round stages 64*NW records (48 B, rr_common.hpp Splat) in LDS; the next round's
+//     records are prefetched into registers while the current one is blended.
+//   * A round starts only if some pixel of the tile is still open (__syncthreads_count,
+//     forward.cu:302-304); inside a round a wave leaves as soon as all its pixels are saturated.
+//   * The falloff uses blend_power/blend_G (rr_common.hpp), the same op sequence as the backward.
+//   * n_contrib: a pixel that is still open has processed every pair before the current one, so its
+//     contributor count is just (pair index + 1) — no per-pixel counter.
+#include "rr_common.hpp"
+#include "rr_kernels.hpp"
+
+namespace rr {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
+#pragma clang fp contract(off)  // exactly blend_power's rounding: every fma below is explicit
+    constexpr int PAIRS = 2 / NW;  // pixel pairs per lane
+    constexpr int B = 64 * NW;     // records per round
+    const int ntiles = a.gx * a.gy;
+    const int tile = xcd_tile(blockIdx.x, ntiles);
+    const int tx = tile % a.gx, ty = tile / a.gx;
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int px = tx * TILE_X + (lane & 15);
+    const float pfx = (float)px;
+
+    __shared__ float4 s_a[B];
+    __shared__ float4 s_b[B];
+    __shared__ float4 s_c[B];
+
+    // per pixel pair: T (transmittance), om (1 while the pixel is open, 0 once saturated: it zeroes
+    // alpha, so a closed pixel neither blends nor changes T), colour / depth accumulators
+    int py[PAIRS][2];
+    f2 pfy[PAIRS], T[PAIRS], om[PAIRS], C0[PAIRS], C1[PAIRS], C2[PAIRS], Dp[PAIRS];
+    uint32_t last[PAIRS][2];
+#pragma unroll
+    for (int p = 0; p < PAIRS; p++) {
+        const int row0 = ty * TILE_Y + (lane >> 4) + 8 * (w * PAIRS + p);
+        py[p][0] = row0;
+        py[p][1] = row0 + 4;
+        pfy[p] = f2{(float)row0, (float)(row0 + 4)};
+        T[p] = f2{1.f, 1.f};
+        om[p] = f2{(px < a.W && row0 < a.H) ? 1.f : 0.f, (px < a.W && row0 + 4 < a.H) ? 1.f : 0.f};
+        C0[p] = C1[p] = C2[p] = Dp[p] = f2{0.f, 0.f};
+        last[p][0] = last[p][1] = 0;
+    }
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+    auto all_closed = [&]() {
+        bool c = true;
+#pragma unroll
+        for (int p = 0; p < PAIRS; p++) c = c && om[p].x == 0.f && om[p].y == 0.f;
+        return c;
+    };
+
+    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
+    if (t < n) load_splat(a.splats, a.point_list[range.x + t], na, nb, nc);
+    for (int base = 0; base < n; base += B) {
+        if (__syncthreads_count(all_closed()) == B) break;
+        if (base + t < n) {
+            s_a[t] = na;
+            s_b[t] = nb;
+            s_c[t] = nc;
+        }
+        __syncthreads();
+        if (base + B + t < n) load_splat(a.splats, a.point_list[range.x + base + B + t], na, nb, nc);
+        const int cnt = min(B, n - base);
+        for (int j = 0; j < cnt; j++) {
+            if ((j & 3) == 0 && __all(all_closed())) break;
+            const float4 A = s_a[j];
+            const float4 Bv = s_b[j];
+            const float4 Cc = s_c[j];
+            const uint32_t k1 = (uint32_t)(base + j + 1);
+            // x-terms shared by both pixels of a pair (blend_power's op sequence)
+            const float dx = A.x - pfx;
+            const float cxdx2 = (A.z * dx) * dx;
+            const float wdx = A.w * dx;
+#pragma unroll
+            for (int p = 0; p < PAIRS; p++) {
+                const f2 dy = f2{A.y, A.y} - pfy[p];
+                const f2 tq = fma2(f2{Bv.x, Bv.x} * dy, dy, f2{cxdx2, cxdx2});
+                const f2 u = f2{wdx, wdx} * dy;
+                const f2 power = fma2(f2{-0.5f, -0.5f}, tq, -u);
+                const f2 pl = power * f2{kLog2e, kLog2e};
+                f2 al = f2{Bv.y, Bv.y} * f2{__builtin_amdgcn_exp2f(pl.x), __builtin_amdgcn_exp2f(pl.y)};
+                // forward.cu:333-336: skip power > 0 and alpha < 1/255 (alpha := 0)
+                al.x = (power.x <= 0.0f && fminf(0.99f, al.x) >= 1.0f / 255.0f) ? fminf(0.99f, al.x) : 0.f;
+                al.y = (power.y <= 0.0f && fminf(0.99f, al.y) >= 1.0f / 255.0f) ? fminf(0.99f, al.y) : 0.f;
+                al = al * om[p];
+                const f2 testT = T[p] * (f2{1.f, 1.f} - al);
+                // forward.cu:337-341: saturation closes the pixel without blending this Gaussian
+                const bool sat0 = testT.x < 0.0001f, sat1 = testT.y < 0.0001f;
+                f2 wgt = al * T[p];
+                wgt.x = sat0 ? 0.f : wgt.x;
+                wgt.y = sat1 ? 0.f : wgt.y;
+                C0[p] = fma2(f2{Cc.x, Cc.x}, wgt, C0[p]);
+                C1[p] = fma2(f2{Cc.y, Cc.y}, wgt, C1[p]);
+                C2[p] = fma2(f2{Cc.z, Cc.z}, wgt, C2[p]);
+                Dp[p] = fma2(f2{Bv.z, Bv.z}, wgt, Dp[p]);
+                T[p].x = sat0 ? T[p].x : testT.x;
+                T[p].y = sat1 ? T[p].y : testT.y;
+                om[p].x = sat0 ? 0.f : om[p].x;
+                om[p].y = sat1 ? 0.f : om[p].y;
+                last[p][0] = wgt.x > 0.f ? k1 : last[p][0];
+                last[p][1] = wgt.y > 0.f ? k1 : last[p][1];
+            }
+        }
+        __syncthreads();
+    }
+
+    uint32_t m = 0;
+    const size_t HW = (size_t)a.H * a.W;
+#pragma unroll
+    for (int p = 0; p < PAIRS; p++)
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (px < a.W && py[p][k] < a.H) {
+                const float Tk = k ? T[p].y : T[p].x;
+                m = max(m, last[p][k]);
+                const int pix = a.W * py[p][k] + px;
+                a.final_T[pix] = Tk;
+                a.n_contrib[pix] = last[p][k];
+                a.out_color[pix] = (k ? C0[p].y : C0[p].x) + Tk * a.bg[0];
+                a.out_color[HW + pix] = (k ? C1[p].y : C1[p].x) + Tk * a.bg[1];
+                a.out_color[2 * HW + pix] = (k ? C2[p].y : C2[p].x) + Tk * a.bg[2];
+                a.out_depth[pix] = k ? Dp[p].y : Dp[p].x;
+            }
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if (NW == 1) {
+        if (lane == 0) a.tile_max[tile] = m;
+    } else {
+        __shared__ uint32_t s_m[NW];
+        if (lane == 0) s_m[w] = m;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t mm = s_m[0];
+#pragma unroll
+            for (int i = 1; i < NW; i++) mm = max(mm, s_m[i]);
+            a.tile_max[tile] = mm;
+        }
+    }
+}
+
+void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
+    const int T = a.gx * a.gy;
+    if (T == 0) return;
+    if (blend_fwd_waves() == 1) k_blend_fwd<1><<<T, 64, 0, st>>>(a);
+    else k_blend_fwd<2><<<T, 128, 0, st>>>(a);
+}
+
+}  // namespace rr

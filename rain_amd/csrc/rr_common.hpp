@@ -251,6 +251,42 @@ __device__ __forceinline__ v3 sh_eval(v3 dir, const float* dc, const float* rest
     return mk(r.x + 0.5f, r.y + 0.5f, r.z + 0.5f);
 }
 
+// Prefetch of one Splat record into three float4 registers.  Plain float4 variables: keeping
+// the prefetched record in a struct made hipcc place it in scratch (private memory).
+__device__ __forceinline__ void load_splat(const Splat* __restrict__ s, uint32_t i, float4& a, float4& b, float4& c) {
+    const float4* p = reinterpret_cast<const float4*>(s + i);
+    a = p[0];
+    b = p[1];
+    c = p[2];
+}
+
+// 1/x from v_rcp_f32 (1 ulp) refined by one Newton step (~0.5 ulp): 4 VALU ops instead of the
+// ~10-op IEEE division sequence hipcc emits for '/' and __fdividef.  x = 1 - alpha is in [0.01, 1).
+__device__ __forceinline__ float rcp_nr(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(r, __builtin_fmaf(-x, r, 1.0f), r);
+}
+
+// Bijective block -> tile remap (cdna_hip_programming.md §5, "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int x = b & 7, s = b >> 3;
+    return x < r ? x * (q + 1) + s : r * (q + 1) + (x - r) * q + s;
+}
+
+// Falloff exponent of a (pair, pixel) (forward.cu:329-331 / backward.cu:481-486) with a fixed op
+// sequence — explicit fmas, no contraction — shared by the forward (packed, rr_blend_fwd.hip) and
+// backward (scalar) blends, so both take bitwise-identical alpha decisions.  dx, dy = mean - pixel.
+__device__ __forceinline__ float blend_power(float4 A, float4 Bv, float dx, float dy) {
+#pragma clang fp contract(off)
+    const float cxdx2 = (A.z * dx) * dx;
+    const float t = __builtin_fmaf(Bv.x * dy, dy, cxdx2);
+    const float u = (A.w * dx) * dy;
+    return __builtin_fmaf(-0.5f, t, -u);
+}
+constexpr float kLog2e = 1.44269504088896340736f;
+__device__ __forceinline__ float blend_G(float power) { return __builtin_amdgcn_exp2f(power * kLog2e); }
+
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 // Wave64 sum with DPP row shifts + row broadcasts; the total lands in lane 63.

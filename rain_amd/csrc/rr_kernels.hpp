@@ -124,4 +124,5 @@ void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
 namespace rr {
 // Tuning knob: waves per tile (1, 2, 4) of the blend kernels; 0 = default / env override.
 void set_blend_config(int fwd_waves, int bwd_waves);
+int blend_fwd_waves();  // 1 or 2 (forward blend, rr_blend_fwd.hip)
 }  // namespace rr
