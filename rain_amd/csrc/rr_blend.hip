@@ -130,11 +130,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     const float gdx = G * dx, gdy = G * dy;
                     const float dG_ddelx = -gdx * A.z - gdy * A.w;
                     const float dG_ddely = -gdy * Bv.x - gdx * A.w;
-                    g0 += dL_dG * dG_ddelx * ddelx_dx;
-                    g1 += dL_dG * dG_ddely * ddely_dy;
-                    g2 += -0.5f * gdx * dx * dL_dG;
-                    g3 += -0.5f * gdx * dy * dL_dG;
-                    g4 += -0.5f * gdy * dy * dL_dG;
+                    // the constant factors (0.5 W, 0.5 H, -0.5) are applied once per (tile,
+                    // Gaussian, component) at the flush below, not per pixel
+                    g0 += dL_dG * dG_ddelx;
+                    g1 += dL_dG * dG_ddely;
+                    g2 += gdx * dx * dL_dG;
+                    g3 += gdx * dy * dL_dG;
+                    g4 += gdy * dy * dL_dG;
                     g5 += G * dL_dalpha;
                 }
             }
@@ -153,7 +155,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                 float v = s_g[0][e];
 #pragma unroll
                 for (int i = 1; i < NW; i++) v += s_g[i][e];
-                if (v != 0.f) atomicAdd(a.gacc + (size_t)s_id[pair] * GACC_STRIDE + (e - pair * NGRAD), v);
+                const int comp = e - pair * NGRAD;
+                v *= comp == 0 ? ddelx_dx : comp == 1 ? ddely_dy : comp <= 4 ? -0.5f : 1.f;
+                if (v != 0.f) atomicAdd(a.gacc + (size_t)s_id[pair] * GACC_STRIDE + comp, v);
             }
         }
         __syncthreads();
