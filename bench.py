@@ -197,7 +197,10 @@ def main():
         gbs = byts / (kernels[dom]["ms_per_launch"] * 1e-3) / 1e9
         roofline = {"kernel": dom, "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(dom),
-                    "algorithmic_bytes_per_launch": int(byts)}
+                    "algorithmic_bytes_per_launch": int(byts),
+                    # the blend kernels are VALU-issue bound, not HBM bound: fraction of SIMD
+                    # cycles issuing a VALU op, from the committed SQ counter pass
+                    "valu_busy": _pmc_field(dom, "valu_busy")}
         for k in kernels:
             b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2)
             if b is not None:
@@ -243,6 +246,15 @@ def _settings(cam, gauss, bg):
     from rain_amd.synthetic import settings_for
 
     return settings_for(cam, gauss.active_sh_degree, bg=bg)
+
+
+def _pmc_field(kernel, field):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("kernels", {}).get(kernel, {}).get(field)
+    except (OSError, ValueError):
+        return None
 
 
 def _pmc_traffic(kernel):

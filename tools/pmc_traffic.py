@@ -19,6 +19,8 @@ import statistics
 
 STAGES = [  # kernel-name pattern -> bench.py stage name
     (r"k_blend_bwd", "blend_bwd"),
+    (r"k_rs_scatter", "sort_scatter"),
+    (r"k_rs_count", "sort_count"),
     (r"k_blend_fwd", "blend_fwd"),
     (r"k_preprocess", "preprocess"),
     (r"k_gauss_bwd", "gauss_bwd"),
@@ -54,10 +56,39 @@ def _read(dirname, counter):
     return {st: list(d.values()) for st, d in per.items()}
 
 
+SIMDS = 256 * 4       # MI355X: 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4       # peak engine clock (MI355X_MICROARCH.md)
+
+
+def _valu_busy(dirname):
+    """Fraction of SIMD issue cycles with a VALU instruction, per kernel: sum over waves of
+    SQ_ACTIVE_INST_VALU (quad-cycles, x4) / (kernel duration x SIMDs x clock)."""
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
+    out = {}
+    for fn in files:
+        per = {}
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                st = _stage(row.get("Kernel_Name", ""))
+                if st is None:
+                    continue
+                key = row.get("Dispatch_Id")
+                d = per.setdefault((st, key), {"dur": None})
+                d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                if row.get("End_Timestamp") and row.get("Start_Timestamp"):
+                    d["dur"] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+        for (st, _), d in per.items():
+            if d.get("dur") and "SQ_ACTIVE_INST_VALU" in d:
+                busy = 4.0 * d["SQ_ACTIVE_INST_VALU"] / (d["dur"] * CLOCK_GHZ * SIMDS)
+                out.setdefault(st, []).append(busy)
+    return {st: statistics.median(v) for st, v in out.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
+    ap.add_argument("--sq-dir", default=None, help="a third pass with SQ_ACTIVE_INST_VALU (VALU busy)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
@@ -74,6 +105,11 @@ def main():
             "fetch_bytes_raw": f, "write_bytes": w,
             "hbm_bytes_per_launch": (2 * f + w) if (f is not None and w is not None) else None,
         }
+    if a.sq_dir:
+        out["valu_busy_note"] = ("sum of SQ_ACTIVE_INST_VALU quad-cycles x4 / (kernel duration x 1024 SIMDs x "
+                                 f"{CLOCK_GHZ} GHz): fraction of SIMD cycles issuing a VALU op")
+        for st, v in _valu_busy(a.sq_dir).items():
+            out["kernels"].setdefault(st, {})["valu_busy"] = round(v, 3)
     with open(a.out, "w") as fo:
         json.dump(out, fo, indent=1)
     print(json.dumps(out, indent=1))
