@@ -144,8 +144,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                                                    uint32_t win, uint32_t L, K* __restrict__ keys,
                                                    uint32_t* __restrict__ vals, int dbits,
                                                    uint32_t* __restrict__ counts, int units) {
-    __shared__ K s_key[4096];
-    __shared__ uint32_t s_val[4096];
+    __shared__ K s_key[kSortMaxUnit];
+    __shared__ uint32_t s_val[kSortMaxUnit];
     __shared__ uint32_t hist[256];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
@@ -247,7 +247,7 @@ template <typename K>
 void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats, const int* radii,
                       int gx, int gy, int cull, uint32_t* first, uint32_t win, int nwin, uint32_t L, K* keys,
                       uint32_t* vals, int dbits, uint32_t* counts, hipStream_t st) {
-    if (P == 0 || L == 0) return;
+    if (P == 0 || L == 0 || win > (uint32_t)kSortMaxUnit) return;  // win comes from radix_sort_plan
     k_window_starts<<<blocks_for(P), 256, 0, st>>>(P, offsets, win, nwin, first);
     k_duplicate<K><<<nwin, 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, cull, first, win, L, keys,
                                           vals, dbits, counts, nwin);

@@ -100,6 +100,10 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);
 
+// Largest sort unit (items per workgroup) of rr_sort.hip; the duplicate kernel's LDS windows are
+// sort units, so it sizes its staging arrays with this too.
+constexpr int kSortMaxUnit = 4096;
+
 // rr_sort.hip: stable LSD radix sort of (K key, u32 value) pairs on bits [begin_bit, end_bit).
 // vals_in == nullptr means values = input index.  keys_out may be nullptr only for a single pass.
 template <typename K>

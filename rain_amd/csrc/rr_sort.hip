@@ -29,6 +29,7 @@ namespace {
 constexpr int kWaves = 4;       // waves per workgroup (unit)
 constexpr int kMaxRounds = 16;  // rounds of 64 items per wave
 constexpr int kMaxUnitItems = 64 * kWaves * kMaxRounds;  // 4096
+static_assert(kMaxUnitItems == kSortMaxUnit, "rr_kernels.hpp kSortMaxUnit");
 
 template <typename K>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ keys, size_t n, int shift, int dbits,
@@ -92,36 +93,41 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
         if (r < rounds && i < n) atomicAdd(&wcnt[w][((uint32_t)kr[r] >> shift) & mask], 1u);
     }
     __syncthreads();
-    // block-local starts: digits in order, then waves in order inside each digit
-    if (t < ndig) {
-        uint32_t c[kWaves], tot = 0;
+    // block-local starts: digits in order, then waves in order inside each digit.  Wave 0 scans the
+    // <= 256 digit totals: 4 consecutive digits per lane, then a 6-step shuffle scan of lane sums.
+    if (w == 0) {
+        uint32_t tot[4], sum = 0;
 #pragma unroll
-        for (int v = 0; v < kWaves; v++) {
-            c[v] = wcnt[v][t];
-            tot += c[v];
+        for (int i = 0; i < 4; i++) {
+            const int d = 4 * lane + i;
+            tot[i] = 0;
+            if (d < ndig)
+#pragma unroll
+                for (int v = 0; v < kWaves; v++) tot[i] += wcnt[v][d];
+            sum += tot[i];
         }
-        dstart[t] = tot;  // turned into an exclusive prefix below
+        uint32_t incl = sum;
 #pragma unroll
-        for (int v = 0; v < kWaves; v++) wcnt[v][t] = c[v];
-    }
-    __syncthreads();
-    if (t == 0) {  // exclusive scan of <= 256 digit totals (cheap, one thread)
-        uint32_t run = 0;
-        for (int d = 0; d < ndig; d++) {
-            const uint32_t x = dstart[d];
-            dstart[d] = run;
-            run += x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += y;
         }
-    }
-    __syncthreads();
-    if (t < ndig) {
-        goff[t] -= dstart[t];
-        uint32_t run = dstart[t];
+        uint32_t run = incl - sum;  // exclusive prefix of this lane's first digit
 #pragma unroll
-        for (int v = 0; v < kWaves; v++) {
-            const uint32_t x = wcnt[v][t];
-            wcnt[v][t] = run;
-            run += x;
+        for (int i = 0; i < 4; i++) {
+            const int d = 4 * lane + i;
+            if (d < ndig) {
+                dstart[d] = run;
+                goff[d] -= run;
+                uint32_t r2 = run;
+#pragma unroll
+                for (int v = 0; v < kWaves; v++) {
+                    const uint32_t x = wcnt[v][d];
+                    wcnt[v][d] = r2;
+                    r2 += x;
+                }
+            }
+            run += tot[i];
         }
     }
     __syncthreads();
