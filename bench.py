@@ -52,6 +52,9 @@ def parse():
     return p.parse_args()
 
 
+MODELED = ("preprocess", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd", "blend_bwd", "gauss_bwd")
+
+
 def algorithmic_bytes(stage, st, P, W, H, K):
     """SURVEY §8(d) per-launch algorithmic bytes.  L is the number of (tile, Gaussian) pairs this
     implementation actually bins (num_pairs, after exact tile culling), not the reference's larger
@@ -118,19 +121,31 @@ def main():
     trainer = Trainer(gauss, cams, gts, opt, pipe, TrainConfig(seed=0), scene_extent=extent)
 
     K, Wm = args.steps, args.warmup
-    end_iter = max(1000, int(math.ceil((Wm + K + 1) / 100.0)) * 100)
-    start_iter = end_iter - K - Wm + 1
+    prof = not args.no_profile
+    # untimed per-stage breakdown window (every stage event-timed) between warmup and the timed loop
+    PW = min(20, K) if prof else 0
+    end_iter = max(1000, int(math.ceil((Wm + PW + K + 1) / 100.0)) * 100)
+    start_iter = end_iter - K - PW - Wm + 1
     it = start_iter
     for _ in range(Wm):
         trainer.step(it)
         it += 1
+    breakdown, dom = {}, None
+    if prof:
+        _native.Profiler.collect()  # drop anything recorded before the window
+        with _native.Profiler():
+            for _ in range(PW):
+                trainer.step(it)
+                it += 1
+        breakdown = _native.Profiler.collect()
+        modeled = [k for k in breakdown if breakdown[k][1] and k in MODELED]
+        dom = max(modeled, key=lambda k: breakdown[k][0]) if modeled else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    prof = not args.no_profile
-    if prof:
-        _native.raster().rr_profile_enable(1)
-        _native.Profiler.collect()  # drop anything recorded before the window
+    timer = _native.Profiler([dom]) if dom else None
+    if timer:  # the timed loop records only the reported kernel: two events per launch
+        timer.__enter__()
     t0 = time.perf_counter()
     views_used = []
     for _ in range(K):
@@ -141,10 +156,10 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    stage_ms = {}
-    if prof:
-        _native.raster().rr_profile_enable(0)
-        stage_ms = _native.Profiler.collect()
+    dom_timed = None
+    if timer:
+        timer.__exit__()
+        dom_timed = _native.Profiler.collect()[dom]
     elapsed = t1 - t0
     if world > 1:
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -187,15 +202,15 @@ def main():
 
     roofline = None
     kernels = {}
-    if stage_ms:
-        for name, (ms, cnt) in stage_ms.items():
-            if cnt:
-                kernels[name] = {"ms_per_launch": ms / cnt, "launches": int(cnt), "total_ms": ms}
-        dom = max((k for k in kernels if algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2) is not None),
-                  key=lambda k: kernels[k]["total_ms"])
+    for name, (ms, cnt) in breakdown.items():
+        if cnt:
+            kernels[name] = {"ms_per_launch": ms / cnt, "launches": int(cnt), "total_ms": ms}
+    if dom_timed and dom_timed[1]:
         byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2)
-        gbs = byts / (kernels[dom]["ms_per_launch"] * 1e-3) / 1e9
+        dom_ms = dom_timed[0] / dom_timed[1]  # HIP events around every launch inside the timed loop
+        gbs = byts / (dom_ms * 1e-3) / 1e9
         roofline = {"kernel": dom, "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "ms_per_launch": round(dom_ms, 5), "launches": int(dom_timed[1]),
                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(dom),
                     "algorithmic_bytes_per_launch": int(byts),
                     # the blend kernels are VALU-issue bound, not HBM bound: fraction of SIMD
@@ -228,12 +243,13 @@ def main():
                                f"view-sharded dp{world}",
                    "gaussians": P, "width": W, "height": H, "sh_degree": D, "views": args.views,
                    "parallelism": f"dp{world} (view-sharded, RCCL all-reduce)" if world > 1 else "dp1",
-                   "iterations": [start_iter + Wm, end_iter]},
+                   "iterations": [start_iter + Wm + PW, end_iter]},
         "forward_mpix_per_s": round(fwd_mpix, 2),
         "gaussians_after": int(Pn),
         "frame_stats": {k: int(v) for k, v in mean_stats.items()},
         "roofline": roofline,
         "kernels": kernels,
+        "kernels_window": f"{PW} untimed profiled iterations between warmup and the timed loop (all stages event-timed)",
         "cpu_baseline": cpu,
     }
     if rank == 0:

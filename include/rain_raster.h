@@ -202,8 +202,10 @@ int rr_debug_get_views(const rr_frame* f, const void* geom_buffer, const void* i
                        const void* binning_buffer, int num_rendered, rr_debug_views* out);
 
 /* Kernel timing with HIP events on the launch stream (bench.py's live roofline numbers).
- * rr_profile_enable(1) starts recording every stage; rr_profile_collect() synchronizes, adds
- * the elapsed ms per stage into ms[RR_NUM_STAGES] / counts, and clears the record. */
+ * rr_profile_enable(1) starts recording the selected stages (rr_profile_select: bit s = stage s,
+ * default all); rr_profile_collect() synchronizes, adds the elapsed ms per stage into
+ * ms[RR_NUM_STAGES] / counts, and clears the record.  Each recorded stage costs two event records
+ * on the stream, so a timed loop selects only the kernel it reports. */
 enum rr_stage {
     RR_STAGE_PREPROCESS = 0,
     RR_STAGE_DEPTH_SORT,
@@ -218,6 +220,7 @@ enum rr_stage {
     RR_NUM_STAGES
 };
 int rr_profile_enable(int enable);
+int rr_profile_select(unsigned stage_mask);
 
 /* Tuning knob (diagnostics / A-B tests): wave64s per 16x16 tile used by the forward and backward
  * blend kernels (1, 2 or 4; 0 restores the default).  Results are identical for every choice. */

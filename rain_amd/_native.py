@@ -76,7 +76,7 @@ class RRDebugViews(ctypes.Structure):
 RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
                   "rr_forward_geometry", "rr_forward_render", "rr_backward", "rr_mark_visible", "rr_last_error",
                   "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config", "rr_profile_enable",
-                  "rr_profile_collect", "rr_stage_name"]
+                  "rr_profile_select", "rr_profile_collect", "rr_stage_name"]
 
 _raster = None
 _knn = None
@@ -122,6 +122,8 @@ def raster():
         L.rr_set_blend_config.argtypes = [ci, ci]
         L.rr_profile_enable.restype = ci
         L.rr_profile_enable.argtypes = [ci]
+        L.rr_profile_select.restype = ci
+        L.rr_profile_select.argtypes = [ctypes.c_uint]
         L.rr_profile_collect.restype = ci
         L.rr_profile_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
         L.rr_stage_name.restype = ctypes.c_char_p
@@ -202,12 +204,17 @@ def stream_of(t: torch.Tensor):
 class Profiler:
     """Per-stage kernel time via HIP events recorded by the library on the launch stream."""
 
+    def __init__(self, stages=None):
+        self.mask = 0xFFFFFFFF if stages is None else sum(1 << STAGES.index(s) for s in stages)
+
     def __enter__(self):
+        raster().rr_profile_select(self.mask)
         raster().rr_profile_enable(1)
         return self
 
     def __exit__(self, *exc):
         raster().rr_profile_enable(0)
+        raster().rr_profile_select(0xFFFFFFFF)
 
     @staticmethod
     def collect():

@@ -123,28 +123,49 @@ __global__ __launch_bounds__(256) void k_ssim_fwd(const float* __restrict__ img,
     }
 }
 
-__global__ __launch_bounds__(256) void k_loss_finalize(const float2* __restrict__ partial, int nb, float lambda,
-                                                       float inv_n, float* __restrict__ loss,
-                                                       float* __restrict__ parts) {
-    __shared__ double rs[256], rl[256];
-    double s = 0.0, l = 0.0;
-    for (int i = threadIdx.x; i < nb; i += 256) {
-        s += partial[i].x;
-        l += partial[i].y;
-    }
-    rs[threadIdx.x] = s;
-    rl[threadIdx.x] = l;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            rs[threadIdx.x] += rs[threadIdx.x + o];
-            rl[threadIdx.x] += rl[threadIdx.x + o];
+// One block of 1024 threads; every thread keeps four independent double accumulators per sum so
+// its loads are all in flight (a single chain of dependent adds made this a 25 us latency-bound
+// kernel).  Fixed summation order: the result is deterministic.
+constexpr int kFinT = 1024;
+__global__ __launch_bounds__(kFinT) void k_loss_finalize(const float2* __restrict__ partial, int nb, float lambda,
+                                                         float inv_n, float* __restrict__ loss,
+                                                         float* __restrict__ parts) {
+    __shared__ double rs[kFinT / 64], rl[kFinT / 64];
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, l[4] = {0.0, 0.0, 0.0, 0.0};
+    int i = threadIdx.x;
+    for (; i + 3 * kFinT < nb; i += 4 * kFinT) {
+        float2 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = partial[i + k * kFinT];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            s[k] += v[k].x;
+            l[k] += v[k].y;
         }
-        __syncthreads();
     }
+    for (int k = 0; i < nb; i += kFinT, k++) {
+        s[k] += partial[i].x;
+        l[k] += partial[i].y;
+    }
+    double ss = (s[0] + s[1]) + (s[2] + s[3]), ll = (l[0] + l[1]) + (l[2] + l[3]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ss += __shfl_xor(ss, o);
+        ll += __shfl_xor(ll, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        rs[threadIdx.x >> 6] = ss;
+        rl[threadIdx.x >> 6] = ll;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        const float ssim = (float)(rs[0] * inv_n);
-        const float l1 = (float)(rl[0] * inv_n);
+        double S = 0.0, Lv = 0.0;
+        for (int w = 0; w < kFinT / 64; w++) {
+            S += rs[w];
+            Lv += rl[w];
+        }
+        const float ssim = (float)(S * inv_n);
+        const float l1 = (float)(Lv * inv_n);
         const float total = (1.0f - lambda) * l1 + lambda * (1.0f - ssim);
         loss[0] = total;
         if (parts) {
@@ -243,7 +264,7 @@ int rl_l1_ssim_forward(const float* img, const float* gt, int C, int H, int W, f
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((W + TS - 1) / TS, (H + TS - 1) / TS, C);
     k_ssim_fwd<<<grid, 256, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g11, g12, partial);
-    k_loss_finalize<<<1, 256, 0, st>>>(partial, nblocks(C, H, W), lambda, inv_n, loss, parts);
+    k_loss_finalize<<<1, kFinT, 0, st>>>(partial, nblocks(C, H, W), lambda, inv_n, loss, parts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("rl_l1_ssim_forward: ") + hipGetErrorString(e);

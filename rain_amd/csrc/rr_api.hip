@@ -174,6 +174,7 @@ struct EvRec {
     hipEvent_t a, b;
 };
 bool g_prof = false;
+unsigned g_prof_mask = 0xffffffffu;  // stages recorded while profiling (rr_profile_select)
 std::vector<EvRec> g_recs;
 std::vector<hipEvent_t> g_pool;
 
@@ -193,13 +194,13 @@ struct StageTimer {
     hipStream_t st;
     hipEvent_t a = nullptr;
     StageTimer(int s, hipStream_t stream) : stage(s), st(stream) {
-        if (g_prof) {
+        if (g_prof && ((g_prof_mask >> s) & 1u)) {
             a = ev_get();
             (void)hipEventRecord(a, st);
         }
     }
     ~StageTimer() {
-        if (g_prof) {
+        if (a) {
             hipEvent_t b = ev_get();
             (void)hipEventRecord(b, st);
             g_recs.push_back({stage, a, b});
@@ -547,6 +548,11 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves) {
 
 int rr_profile_enable(int enable) {
     g_prof = enable != 0;
+    return RR_OK;
+}
+
+int rr_profile_select(unsigned stage_mask) {
+    g_prof_mask = stage_mask;
     return RR_OK;
 }
 
