@@ -35,8 +35,13 @@ LIBS = {
 # Per-source extra device flags.  rr_blend.hip: no packed-fp32 (v_pk_*) formation — in the blend
 # loops hipcc pairs unrelated scalars into v_pk ops and pays for it with v_mov shuffles and ~30
 # extra VGPRs (measured: 132 vs 166 VGPRs, 537 vs 602 instructions in k_blend_bwd<1>).
+# loss.hip: the SSIM kernels' band loop must unroll fully (compile-time ring / queue slots) and is
+# larger than clang's default pragma-unroll size limit; packed-fp32 formation is off for the same
+# reason as rr_blend.hip (it pairs unrelated scalars: 940 v_mov, 244 VGPRs in k_ssim_fwd).
 EXTRA = {
     "rr_blend.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
+    "loss.hip": ["-mllvm", "-pragma-unroll-threshold=200000",
+                 "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
 }
 
 

@@ -171,4 +171,10 @@ def test_adam_fused_into_backward_matches_separate_step(gpu):
     for pa, pb in zip(a.params(), b.params()):
         sa, sb = a.optimizer.state[pa], b.optimizer.state[pb]
         assert float(sa["step"]) == float(sb["step"]) == 3.0
-        assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-4, atol=1e-12)
+        # the backward's atomics add per-Gaussian gradients in a run-dependent order, so moments
+        # near zero differ in their last bits: compare against the tensor's scale
+        for m in ("exp_avg", "exp_avg_sq"):
+            x, y = sa[m], sb[m]
+            scale = max(float(y.abs().max()), 1e-30)
+            assert float((x - y).abs().max()) <= 1e-4 * scale, (m, float((x - y).abs().max()), scale)
+            assert rel_l1(x, y) < 1e-4, (m, rel_l1(x, y))

@@ -7,7 +7,7 @@ from rain_amd.loss import fused_l1_ssim_loss, l1_loss, ssim
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("H,W", [(96, 128), (75, 100), (540, 960)])
+@pytest.mark.parametrize("H,W", [(96, 128), (75, 100), (9, 200), (540, 960), (1080, 1920)])
 def test_fused_loss_matches_reference(gpu, H, W):
     g = torch.Generator().manual_seed(H * W)
     img = torch.rand((3, H, W), generator=g).to(gpu)
