@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-profile", action="store_true", help="skip HIP-event stage timing in the timed region")
+    p.add_argument("--binning-split", type=int, default=0,
+                   help="early-stop binning: phase A = 1/N of the pairs (1 = one phase; 0 = library default)")
     return p.parse_args()
 
 
@@ -99,6 +101,8 @@ def main():
     from rain_amd.train import TrainConfig, Trainer
 
     P, W, H, D = args.points, args.width, args.height, args.sh_degree
+    if args.binning_split:
+        _native.check(_native.raster().rr_set_binning_config(args.binning_split, 0), "binning config")
     cams = [c.to(dev) for c in fibonacci_cameras(args.views, W, H)]
     extent = 4.0 * 1.1  # getNerfppNorm of the camera rig (dataset_readers.py:34-55): radius 4, x1.1
 

@@ -66,6 +66,15 @@ typedef struct rr_frame {
  * pass.  Requires shs and scales/rotations (no precomputed colours or covariances). */
 #define RR_FLAG_RAW_PARAMS 2
 
+/* Early-stop binning (default ON for frames of >= 2^16 pairs; rr_set_binning_config): the tile
+ * lists are built in two phases.  The first 1/4 of the depth-ordered pairs is binned and blended
+ * for every tile; the rest is binned only for tiles with a pixel still unsaturated, and their
+ * blend resumes where it stopped.  Pairs past a tile's saturation are never blended by any pixel
+ * (forward.cu:337-341; the backward walk starts at the last contributor), so images, depth and
+ * gradients are those of the full lists; only the internal lists are shorter.  The flag bins
+ * every pair in one phase (the pair-order tests compare full lists with the reference's). */
+#define RR_FLAG_FULL_BINNING 4
+
 /* Camera / per-frame device arrays (reference args of the same names). */
 typedef struct rr_camera {
     const float* background; /* [3] */
@@ -183,7 +192,8 @@ typedef struct rr_frame_stats {
     int64_t num_visible;   /* V */
     int64_t l_eff;         /* sum over tiles of max n_contrib (needs rr_read_frame_stats) */
     int64_t tiles;         /* T */
-    int64_t num_pairs;     /* pairs actually binned (after exact tile culling) */
+    int64_t num_pairs;     /* pairs emitted by exact tile culling (before early-stop binning) */
+    int64_t num_binned;    /* pairs actually sorted into tile lists (phase A + phase B) */
 } rr_frame_stats;
 int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* image_buffer, rr_frame_stats* out,
                         void* stream);
@@ -225,6 +235,12 @@ int rr_profile_select(unsigned stage_mask);
 /* Tuning knob (diagnostics / A-B tests): wave64s per 16x16 tile used by the forward and backward
  * blend kernels (1, 2 or 4; 0 restores the default).  Results are identical for every choice. */
 int rr_set_blend_config(int fwd_waves, int bwd_waves);
+
+/* Tuning knob (diagnostics / tests): early-stop binning bins L / split_denominator pairs in phase A
+ * (1 = one phase) for frames of at least min_pairs pairs; 0 restores a default (4, 2^16).  Results
+ * are identical for every choice.  Applies to frames rendered after the call (a backward finds its
+ * frame's lists in the image buffer). */
+int rr_set_binning_config(int split_denominator, int min_pairs);
 int rr_profile_collect(double* ms, int64_t* counts);
 const char* rr_stage_name(int stage);
 

@@ -31,6 +31,7 @@ class RRFrame(ctypes.Structure):
 
 RR_FLAG_NO_TILE_CULLING = 1
 RR_FLAG_RAW_PARAMS = 2
+RR_FLAG_FULL_BINNING = 4
 
 
 class RRCamera(ctypes.Structure):
@@ -64,7 +65,7 @@ class RRGrads(ctypes.Structure):
 
 class RRFrameStats(ctypes.Structure):
     _fields_ = [("num_rendered", ctypes.c_int64), ("num_visible", ctypes.c_int64), ("l_eff", ctypes.c_int64),
-                ("tiles", ctypes.c_int64), ("num_pairs", ctypes.c_int64)]
+                ("tiles", ctypes.c_int64), ("num_pairs", ctypes.c_int64), ("num_binned", ctypes.c_int64)]
 
 
 class RRDebugViews(ctypes.Structure):
@@ -75,7 +76,8 @@ class RRDebugViews(ctypes.Structure):
 # every symbol include/rain_raster.h declares (tests check the .so exports all of them)
 RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
                   "rr_forward_geometry", "rr_forward_render", "rr_backward", "rr_mark_visible", "rr_last_error",
-                  "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config", "rr_profile_enable",
+                  "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
+                  "rr_set_binning_config", "rr_profile_enable",
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name"]
 
 _raster = None
@@ -122,6 +124,8 @@ def raster():
         L.rr_set_blend_config.argtypes = [ci, ci]
         L.rr_profile_enable.restype = ci
         L.rr_profile_enable.argtypes = [ci]
+        L.rr_set_binning_config.restype = ci
+        L.rr_set_binning_config.argtypes = [ci, ci]
         L.rr_profile_select.restype = ci
         L.rr_profile_select.argtypes = [ctypes.c_uint]
         L.rr_profile_collect.restype = ci

@@ -114,8 +114,14 @@ Geom carve_geom(void* buf, int P) {
 struct Img {
     float* final_T;
     uint32_t* n_contrib;
-    uint2* ranges;
+    uint2* ranges;      // phase-A (or single-phase) lists; ranges_b and counters follow it
+    uint2* ranges_b;    // phase-B lists of early-stop binning (all {0,0} otherwise)
+    uint32_t* counters; // [0] = phase-B pair count (device-side)
+    size_t zero_bytes;  // ranges .. counters: cleared before every render
     uint32_t* tile_max;
+    uint8_t* open;      // [T] tile still open after phase A
+    uint32_t* sat;      // [(gy+1)*(gx+1)] 2-D prefix sum of open
+    uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask
     size_t total;
 };
 Img carve_img(void* buf, int W, int H) {
@@ -125,10 +131,30 @@ Img carve_img(void* buf, int W, int H) {
     const size_t T = (size_t)std::max(grid_x(W) * grid_y(H), 1);
     m.final_T = c.take<float>(N);
     m.n_contrib = c.take<uint32_t>(N);
-    m.ranges = c.take<uint2>(T);
+    m.ranges = c.take<uint2>(2 * T + 2);  // one block: ranges [T], ranges_b [T], counters [4]
+    m.ranges_b = m.ranges ? m.ranges + T : nullptr;
+    m.counters = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T) : nullptr;
+    m.zero_bytes = (2 * T + 2) * sizeof(uint2);
     m.tile_max = c.take<uint32_t>(T);
+    m.open = c.take<uint8_t>(T);
+    m.sat = c.take<uint32_t>((size_t)(grid_x(W) + 1) * (grid_y(H) + 1));
+    m.open_bits = c.take<uint32_t>((T + 31) / 32);
     m.total = align_up(c.off);
     return m;
+}
+
+// Early-stop binning split: phase A bins the first L_A pairs (depth order) for every tile, phase B
+// the rest for the tiles phase A left open (rr_kernels.hpp BlendPhase).  L_A = L/4: on the bench
+// frames (1M Gaussians, 1080p) most tiles saturate inside it and phase A + B bin ~25% of the pairs
+// (tools/saturation_stats.py); measured per training step 1.671 ms vs 1.742 ms for one phase, and
+// 1.695 / 1.688 / 1.712 for L/2, L/3, L/6 (tools/host_profile.py --binning-split).  Frames below
+// kEarlyMin pairs are binned in one phase.  rr_set_binning_config changes both (tests force the
+// split onto small frames).
+constexpr uint32_t kEarlyDen = 4, kEarlyMin = 1u << 16;
+uint32_t g_early_den = kEarlyDen, g_early_min = kEarlyMin;
+uint32_t early_split(uint32_t L) {
+    if (g_early_den <= 1 || L < g_early_min) return L;
+    return std::max<uint32_t>(L / g_early_den, 1u);
 }
 
 struct Bin {
@@ -136,19 +162,28 @@ struct Bin {
     void* keys;
     void* keys_sorted;
     uint32_t* vals;
-    uint32_t* first;  // first Gaussian of every duplicate window (= sort unit)
-    void* temp;
+    uint32_t* first;     // first Gaussian of every duplicate window (= sort unit), phase A then B
+    uint32_t* unit_len;  // phase B: pairs kept per window
+    void* temp;          // tile-sort scratch, shared by the two phases
     size_t temp_bytes;
     bool wide;  // 32-bit tile keys (T > 65536)
     int bits;
+    uint32_t L, LA;  // pairs, and pairs binned for every tile in phase A (LA == L: one phase)
     size_t total;
 };
+template <typename K>
+RadixPlan tile_plan(void* temp, uint32_t n, int bits) {
+    return radix_sort_plan<K>(temp, (size_t)n, 0, bits);
+}
 Bin carve_bin(void* buf, int L, int W, int H) {
     Carver c(buf);
     Bin b;
     const int T = grid_x(W) * grid_y(H);
     b.wide = T > 65536;
     b.bits = std::max(1, (int)higher_msb((uint32_t)T));  // >= 1: the duplicate windows are sort units
+    b.L = (uint32_t)std::max(L, 0);
+    b.LA = early_split(b.L);
+    const uint32_t LB = b.L - b.LA;
     const size_t n = (size_t)std::max(L, 1);
     b.point_list = c.take<uint32_t>(n);
     if (b.wide) {
@@ -159,10 +194,15 @@ Bin carve_bin(void* buf, int L, int W, int H) {
         b.keys_sorted = c.take<uint16_t>(n);
     }
     b.vals = c.take<uint32_t>(n);
-    const RadixPlan pl = b.wide ? radix_sort_plan<uint32_t>(nullptr, (size_t)L, 0, b.bits)
-                                : radix_sort_plan<uint16_t>(nullptr, (size_t)L, 0, b.bits);
-    b.first = c.take<uint32_t>((size_t)std::max(pl.units, 1));
-    b.temp_bytes = b.wide ? tile_sort_temp<uint32_t>(L, b.bits) : tile_sort_temp<uint16_t>(L, b.bits);
+    const int ua = b.wide ? tile_plan<uint32_t>(nullptr, b.LA, b.bits).units : tile_plan<uint16_t>(nullptr, b.LA, b.bits).units;
+    const int ub = b.wide ? tile_plan<uint32_t>(nullptr, LB, b.bits).units : tile_plan<uint16_t>(nullptr, LB, b.bits).units;
+    b.first = c.take<uint32_t>((size_t)std::max(ua + ub, 1));
+    b.unit_len = c.take<uint32_t>((size_t)std::max(ub, 1));
+    // sized for either path: RR_FLAG_FULL_BINNING sorts all L pairs in one phase
+    b.temp_bytes = b.wide ? std::max({tile_sort_temp<uint32_t>(b.L, b.bits), tile_sort_temp<uint32_t>(b.LA, b.bits),
+                                      tile_sort_temp<uint32_t>(LB, b.bits)})
+                          : std::max({tile_sort_temp<uint16_t>(b.L, b.bits), tile_sort_temp<uint16_t>(b.LA, b.bits),
+                                      tile_sort_temp<uint16_t>(LB, b.bits)});
     b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
     b.total = align_up(c.off);
     return b;
@@ -333,6 +373,88 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     return RR_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Tile lists for one frame: duplicate -> tile sort -> ranges -> blend, once (single phase) or as
+// the two phases of early-stop binning (rr_kernels.hpp BlendPhase).
+template <typename K>
+int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn, const int* radii, int P, int W,
+                 int H, int cull, bool early, BlendFwdArgs b, hipStream_t st) {
+    const int gx = grid_x(W), gy = grid_y(H);
+    const uint32_t L = bn.L, LA = early ? bn.LA : bn.L, LB = L - LA;
+    K* keys = static_cast<K*>(bn.keys);
+    K* keys_sorted = static_cast<K*>(bn.keys_sorted);
+    DupArgs<K> d{};
+    d.P = P; d.idx_sorted = gm.idx_sorted; d.offsets = gm.offsets; d.splats = gm.splats; d.radii = radii;
+    d.gx = gx; d.gy = gy; d.cull = cull;
+    // phase A (or the only phase): pairs [0, LA) for every tile
+    const RadixPlan pa = tile_plan<K>(bn.temp, LA, bn.bits);
+    if (LA > 0) {
+        {
+            StageTimer tm(RR_STAGE_DUPLICATE, st);
+            d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L = LA;
+            d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
+            launch_duplicate<K>(d, st);
+        }
+        RR_STAGE_CHECK("duplicate");
+        {
+            StageTimer tm(RR_STAGE_TILE_SORT, st);
+            RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.point_list, LA, 0,
+                                         bn.bits, st, true),
+                     std::string("tile sort (") + radix_sort_last_error() + ")");
+        }
+        RR_STAGE_CHECK("tile sort");
+        {
+            StageTimer tm(RR_STAGE_RANGES, st);
+            launch_ranges<K>((int)LA, keys_sorted, im.ranges, 0u, nullptr, st);
+        }
+        RR_STAGE_CHECK("ranges");
+    }
+    {
+        StageTimer tm(RR_STAGE_BLEND_FWD, st);
+        b.phase = early ? kBlendPhaseA : kBlendSingle;
+        launch_blend_fwd(b, st);
+    }
+    RR_STAGE_CHECK("blend forward");
+    if (!early) return RR_OK;
+    // phase B: pairs [LA, L), only for tiles phase A left open; positions LA.. of the arrays
+    const RadixPlan pb = tile_plan<K>(bn.temp, LB, bn.bits);
+    {
+        StageTimer tm(RR_STAGE_DUPLICATE, st);
+        launch_open_sat(gx, gy, im.open, im.sat, im.open_bits, st);
+        d.first = bn.first + pa.units; d.pair0 = LA; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units; d.L = L;
+        d.keys = keys + LA; d.vals = bn.vals + LA; d.dbits = pb.dbits0; d.counts = pb.counts;
+        d.sat = im.sat; d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
+        launch_duplicate<K>(d, st);
+    }
+    RR_STAGE_CHECK("duplicate (phase B)");
+    {
+        StageTimer tm(RR_STAGE_TILE_SORT, st);
+        RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys + LA, keys_sorted + LA, bn.vals + LA,
+                                     bn.point_list + LA, LB, 0, bn.bits, st, true, bn.unit_len, im.counters),
+                 std::string("tile sort, phase B (") + radix_sort_last_error() + ")");
+    }
+    RR_STAGE_CHECK("tile sort (phase B)");
+    {
+        StageTimer tm(RR_STAGE_RANGES, st);
+        launch_ranges<K>((int)LB, keys_sorted + LA, im.ranges_b, LA, im.counters, st);
+    }
+    RR_STAGE_CHECK("ranges (phase B)");
+    {
+        StageTimer tm(RR_STAGE_BLEND_FWD, st);
+        b.phase = kBlendPhaseB;
+        launch_blend_fwd(b, st);
+    }
+    RR_STAGE_CHECK("blend forward (phase B)");
+    return RR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                       void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
                       int num_pairs, float* out_color, float* out_depth, void* stream) {
@@ -348,60 +470,20 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
     const Bin bn = carve_bin(binning_buffer, L, W, H);
     if (L > 0 && binning_bytes < bn.total) return fail(RR_ERR_CAPACITY, "binning buffer too small");
     hipStream_t st = (hipStream_t)stream;
-    const int gx = grid_x(W), gy = grid_y(H), T = gx * gy;
-
-    if (L > 0) {
-        {
-            StageTimer tm(RR_STAGE_DUPLICATE, st);
-            // windows of the duplicate kernel == units of the tile sort; it also writes the sort's
-            // first-pass digit counts
-            if (bn.wide) {
-                const RadixPlan pl = radix_sort_plan<uint32_t>(bn.temp, (size_t)L, 0, bn.bits);
-                launch_duplicate<uint32_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull, bn.first,
-                                           (uint32_t)pl.unit_items, pl.units, (uint32_t)L, (uint32_t*)bn.keys,
-                                           bn.vals, pl.dbits0, pl.counts, st);
-            } else {
-                const RadixPlan pl = radix_sort_plan<uint16_t>(bn.temp, (size_t)L, 0, bn.bits);
-                launch_duplicate<uint16_t>(P, gm.idx_sorted, gm.offsets, gm.splats, radii, gx, gy, cull, bn.first,
-                                           (uint32_t)pl.unit_items, pl.units, (uint32_t)L, (uint16_t*)bn.keys,
-                                           bn.vals, pl.dbits0, pl.counts, st);
-            }
-        }
-        RR_STAGE_CHECK("duplicate");
-        {
-            StageTimer tm(RR_STAGE_TILE_SORT, st);
-            size_t tb = bn.temp_bytes;
-            if (bn.wide)
-                RR_CHECK(radix_sort_pairs<uint32_t>(bn.temp, tb, (const uint32_t*)bn.keys, (uint32_t*)bn.keys_sorted,
-                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st, true),
-                         "tile sort");
-            else
-                RR_CHECK(radix_sort_pairs<uint16_t>(bn.temp, tb, (const uint16_t*)bn.keys, (uint16_t*)bn.keys_sorted,
-                                                    bn.vals, bn.point_list, (size_t)L, 0, bn.bits, st, true),
-                         "tile sort");
-        }
-        RR_STAGE_CHECK("tile sort");
-    }
+    const int gx = grid_x(W), gy = grid_y(H);
+    const bool early = L > 0 && bn.LA < bn.L && !(f->flags & RR_FLAG_FULL_BINNING);
     {
         StageTimer tm(RR_STAGE_RANGES, st);
-        RR_CHECK(hipMemsetAsync(im.ranges, 0, (size_t)T * sizeof(uint2), st), "memset ranges");
-        if (L > 0) {
-            if (bn.wide) launch_ranges<uint32_t>(L, (const uint32_t*)bn.keys_sorted, im.ranges, st);
-            else launch_ranges<uint16_t>(L, (const uint16_t*)bn.keys_sorted, im.ranges, st);
-        }
+        RR_CHECK(hipMemsetAsync(im.ranges, 0, im.zero_bytes, st), "memset ranges");
     }
-    RR_STAGE_CHECK("ranges");
-    {
-        StageTimer tm(RR_STAGE_BLEND_FWD, st);
-        BlendFwdArgs b{};
-        b.W = W; b.H = H; b.gx = gx; b.gy = gy;
-        b.ranges = im.ranges; b.point_list = bn.point_list; b.splats = gm.splats; b.bg = cam->background;
-        b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
-        b.out_color = out_color; b.out_depth = out_depth;
-        launch_blend_fwd(b, st);
-    }
-    RR_STAGE_CHECK("blend forward");
-    return RR_OK;
+    BlendFwdArgs b{};
+    b.W = W; b.H = H; b.gx = gx; b.gy = gy;
+    b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.open = im.open;
+    b.point_list = bn.point_list; b.splats = gm.splats; b.bg = cam->background;
+    b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
+    b.out_color = out_color; b.out_depth = out_depth;
+    return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
+                   : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
 }
 
 int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
@@ -451,7 +533,8 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
         StageTimer tm(RR_STAGE_BLEND_BWD, st);
         BlendBwdArgs b{};
         b.W = W; b.H = H; b.gx = gx; b.gy = gy;
-        b.ranges = im.ranges; b.point_list = bn.point_list; b.splats = gm.splats; b.tile_max = im.tile_max;
+        b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.point_list = bn.point_list; b.splats = gm.splats;
+        b.tile_max = im.tile_max;
         b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.bg = cam->background; b.dL_dpix = dL_dpix;
         b.gacc = gacc;
         launch_blend_bwd(b, st);
@@ -510,6 +593,8 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     RR_CHECK(hipMemcpyAsync(&tot, gm.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(per.data(), gm.tiles, (size_t)P * sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
+    uint32_t nb = 0;  // phase-B pairs of the last render into this image buffer
+    RR_CHECK(hipMemcpyAsync(&nb, im.counters, 4, hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipStreamSynchronize(st), "stats");
     int64_t vis = 0;
     for (const uint2& v : per) vis += v.y > 0;  // a Gaussian is visible iff its rect is non-empty (radii > 0)
@@ -519,6 +604,9 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     int64_t s = 0;
     for (uint32_t v : tm) s += v;
     out->l_eff = s;
+    const uint32_t LA = early_split(tot.x);
+    const bool early = LA < tot.x && !(f->flags & RR_FLAG_FULL_BINNING);
+    out->num_binned = early ? (int64_t)LA + nb : (int64_t)tot.x;
     return RR_OK;
 }
 
@@ -543,6 +631,13 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves) {
     if (!ok(fwd_waves) || !(ok(bwd_waves) || bwd_waves == 3))
         return fail(RR_ERR_ARG, "waves per tile must be 0, 1, 2 or 4");
     set_blend_config(fwd_waves, bwd_waves);
+    return RR_OK;
+}
+
+int rr_set_binning_config(int split_denominator, int min_pairs) {
+    if (split_denominator < 0 || min_pairs < 0) return fail(RR_ERR_ARG, "negative binning config");
+    g_early_den = split_denominator == 0 ? kEarlyDen : (uint32_t)split_denominator;
+    g_early_min = min_pairs == 0 ? kEarlyMin : (uint32_t)min_pairs;
     return RR_OK;
 }
 

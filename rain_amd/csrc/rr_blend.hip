@@ -70,13 +70,18 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
         ar0[q] = ar1[q] = ar2[q] = lc0[q] = lc1[q] = lc2[q] = la[q] = 0.f;
     }
     const uint2 range = a.ranges[tile];
+    const uint2 range_b = a.ranges_b[tile];
+    const uint32_t na_len = range.y - range.x;  // list = A-list ++ B-list (early-stop binning)
+    auto pair_at = [&](int idx) -> uint32_t {
+        return (uint32_t)idx < na_len ? range.x + idx : range_b.x + ((uint32_t)idx - na_len);
+    };
     const float ddelx_dx = 0.5f * a.W;
     const float ddely_dy = 0.5f * a.H;
 
     uint32_t nid = 0;
     float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
     if (t < nmax) {
-        nid = a.point_list[range.x + nmax - 1 - t];
+        nid = a.point_list[pair_at(nmax - 1 - t)];
         load_splat(a.splats, nid, na, nb, nc);
     }
     for (int base = 0; base < nmax; base += B) {
@@ -89,7 +94,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
         __syncthreads();
         const int k2 = base + B + t;  // prefetch the next round while this one is blended
         if (k2 < nmax) {
-            nid = a.point_list[range.x + nmax - 1 - k2];
+            nid = a.point_list[pair_at(nmax - 1 - k2)];
             load_splat(a.splats, nid, na, nb, nc);
         }
         const int cnt = min(B, nmax - base);

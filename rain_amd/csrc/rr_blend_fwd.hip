@@ -31,6 +31,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
     constexpr int B = 64 * NW;     // records per round
     const int ntiles = a.gx * a.gy;
     const int tile = xcd_tile(blockIdx.x, ntiles);
+    if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int t = threadIdx.x;
     const int lane = t & 63, w = t >> 6;
@@ -57,7 +58,34 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
         C0[p] = C1[p] = C2[p] = Dp[p] = f2{0.f, 0.f};
         last[p][0] = last[p][1] = 0;
     }
-    const uint2 range = a.ranges[tile];
+    const size_t HW = (size_t)a.H * a.W;
+    uint2 range = a.ranges[tile];
+    uint32_t koff = 0;  // contributor index of the list's first pair
+    if (a.phase == kBlendPhaseB) {
+        // resume: the state phase A left for this open tile (raw colour / depth sums, T, last
+        // contributor, saturated flag), then continue over the phase-B list
+        koff = range.y - range.x;
+        range = a.ranges_b[tile];
+#pragma unroll
+        for (int p = 0; p < PAIRS; p++)
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                if (px < a.W && py[p][k] < a.H) {
+                    const int pix = a.W * py[p][k] + px;
+                    const uint32_t nc = a.n_contrib[pix];
+                    const float tv = a.final_T[pix], c0 = a.out_color[pix], c1 = a.out_color[HW + pix],
+                                c2 = a.out_color[2 * HW + pix], dv = a.out_depth[pix];
+                    if (k) {
+                        T[p].y = tv; C0[p].y = c0; C1[p].y = c1; C2[p].y = c2; Dp[p].y = dv;
+                        om[p].y = (nc & kDoneBit) ? 0.f : 1.f;
+                    } else {
+                        T[p].x = tv; C0[p].x = c0; C1[p].x = c1; C2[p].x = c2; Dp[p].x = dv;
+                        om[p].x = (nc & kDoneBit) ? 0.f : 1.f;
+                    }
+                    last[p][k] = nc & ~kDoneBit;
+                }
+            }
+    }
     const int n = (int)(range.y - range.x);
     auto all_closed = [&]() {
         bool c = true;
@@ -83,7 +111,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
             const float4 A = s_a[j];
             const float4 Bv = s_b[j];
             const float4 Cc = s_c[j];
-            const uint32_t k1 = (uint32_t)(base + j + 1);
+            const uint32_t k1 = koff + (uint32_t)(base + j + 1);
             // x-terms shared by both pixels of a pair (blend_power's op sequence)
             const float dx = A.x - pfx;
             const float cxdx2 = (A.z * dx) * dx;
@@ -121,8 +149,30 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
         __syncthreads();
     }
 
+    if (a.phase == kBlendPhaseA) {
+        // still open: leave the raw state for phase B (no background yet)
+        const bool closed = __syncthreads_count(all_closed()) == B;
+        if (threadIdx.x == 0) a.open[tile] = closed ? 0 : 1;
+        if (!closed) {
+#pragma unroll
+            for (int p = 0; p < PAIRS; p++)
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    if (px < a.W && py[p][k] < a.H) {
+                        const int pix = a.W * py[p][k] + px;
+                        const bool done = (k ? om[p].y : om[p].x) == 0.f;
+                        a.final_T[pix] = k ? T[p].y : T[p].x;
+                        a.n_contrib[pix] = last[p][k] | (done ? kDoneBit : 0u);
+                        a.out_color[pix] = k ? C0[p].y : C0[p].x;
+                        a.out_color[HW + pix] = k ? C1[p].y : C1[p].x;
+                        a.out_color[2 * HW + pix] = k ? C2[p].y : C2[p].x;
+                        a.out_depth[pix] = k ? Dp[p].y : Dp[p].x;
+                    }
+                }
+            return;
+        }
+    }
     uint32_t m = 0;
-    const size_t HW = (size_t)a.H * a.W;
 #pragma unroll
     for (int p = 0; p < PAIRS; p++)
 #pragma unroll

@@ -120,37 +120,115 @@ __global__ __launch_bounds__(256) void k_gather_tiles(int P, const uint32_t* __r
     tiles_sorted[s] = tiles[idx_sorted[s]];
 }
 
-// First Gaussian (depth rank) of every window of `win` consecutive pairs: window k starts inside
-// the pair range [a, b) of exactly one Gaussian.
-__global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __restrict__ offsets, uint32_t win,
-                                                       int nwin, uint32_t* __restrict__ first) {
+// First Gaussian (depth rank) of every window of `win` consecutive pairs starting at pair0:
+// window k = [pair0 + k*win, pair0 + (k+1)*win) starts inside the pair range [a, b) of exactly
+// one Gaussian.
+__global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __restrict__ offsets, uint32_t pair0,
+                                                       uint32_t win, int nwin, uint32_t* __restrict__ first) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P) return;
     const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
-    if (a == b) return;
-    for (uint32_t k = (a + win - 1) / win; k <= (b - 1) / win && k < (uint32_t)nwin; k++) first[k] = (uint32_t)s;
+    if (a == b || b <= pair0) return;
+    const uint32_t k0 = a <= pair0 ? 0u : (a - pair0 + win - 1) / win;
+    for (uint32_t k = k0; k <= (b - 1 - pair0) / win && k < (uint32_t)nwin; k++) first[k] = (uint32_t)s;
+}
+
+// 2-D inclusive prefix sum of the open-tile flags (phase B's per-Gaussian rectangle test):
+// sat[(y + 1) * (gx + 1) + (x + 1)] = open tiles in [0, x] x [0, y].  One workgroup; rows are
+// scanned by waves (64 tiles per step), then columns by threads, in LDS when the table fits.
+constexpr int kSatLds = 16384;  // u32 entries of LDS (64 KiB): up to ~128 x 127 tiles
+template <bool LDS>
+__global__ __launch_bounds__(1024) void k_open_sat(int gx, int gy, const uint8_t* __restrict__ open,
+                                                   uint32_t* __restrict__ sat, uint32_t* __restrict__ open_bits) {
+    __shared__ uint32_t s_sat[LDS ? kSatLds : 1];
+    uint32_t* tab = LDS ? s_sat : sat;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int sw = gx + 1;
+    const int nt = gx * gy;
+    for (int i = t; i < (nt + 31) / 32; i += 1024) {  // the same flags as a bitmask
+        uint32_t m = 0;
+        for (int b = 0; b < 32; b++) {
+            const int tile = 32 * i + b;
+            m |= (tile < nt && open[tile]) ? (1u << b) : 0u;
+        }
+        open_bits[i] = m;
+    }
+    for (int x = t; x < sw; x += 1024) tab[x] = 0;
+    for (int y = w; y < gy; y += 16) {  // rows: one wave per row
+        uint32_t carry = 0;
+        if (lane == 0) tab[(y + 1) * sw] = 0;
+        for (int x0 = 0; x0 < gx; x0 += 64) {
+            const int x = x0 + lane;
+            uint32_t incl = x < gx ? open[y * gx + x] : 0u;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
+                if (lane >= o) incl += v;
+            }
+            if (x < gx) tab[(y + 1) * sw + x + 1] = carry + incl;
+            carry += (uint32_t)__shfl((int)incl, 63);
+        }
+    }
+    __syncthreads();
+    for (int x = t; x < gx; x += 1024) {  // columns
+        uint32_t run = 0;
+        for (int y = 0; y < gy; y++) {
+            run += tab[(y + 1) * sw + x + 1];
+            tab[(y + 1) * sw + x + 1] = run;
+        }
+    }
+    if (LDS) {
+        __syncthreads();
+        for (int i = t; i < sw * (gy + 1); i += 1024) sat[i] = tab[i];
+    }
 }
 
 // duplicateWithKeys (rasterizer_impl.cu:59-100), output-driven: workgroup k produces exactly the
-// pairs [k*win, (k+1)*win) of the depth-ordered pair list.  Its Gaussians (from first[k] on) emit
-// into an LDS window, which then leaves with coalesced stores — the per-Gaussian form scatters
-// every pair to its own cache line — and the window's histogram of the lowest `dbits` key bits is
-// written as the tile sort's first-pass digit counts (rr_sort.hip units == windows).
+// pairs [pair0 + k*win, pair0 + (k+1)*win) of the depth-ordered pair list.  Its Gaussians (from
+// first[k] on) emit into an LDS window, which then leaves with coalesced stores — the
+// per-Gaussian form scatters every pair to its own cache line — and the window's histogram of
+// the lowest `dbits` key bits is written as the tile sort's first-pass digit counts (rr_sort.hip
+// units == windows).  Output of window k goes to [k*win, ...) of keys / vals.
+//
+// Phase B of early-stop binning (sat != nullptr): only pairs whose tile is still open are kept.
+// A Gaussian whose tile rectangle holds no open tile (2-D prefix-sum test) is skipped without
+// enumerating its rows; the kept pairs of the window are compacted (order preserved) and the
+// window's length goes to unit_len[k] (a sparse sort unit) and into *n_total.
 template <typename K>
 __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __restrict__ idx_sorted,
                                                    const uint2* __restrict__ offsets,
                                                    const Splat* __restrict__ splats, const int* __restrict__ radii,
                                                    int gx, int gy, int cull, const uint32_t* __restrict__ first,
-                                                   uint32_t win, uint32_t L, K* __restrict__ keys,
+                                                   uint32_t pair0, uint32_t win, uint32_t L, K* __restrict__ keys,
                                                    uint32_t* __restrict__ vals, int dbits,
-                                                   uint32_t* __restrict__ counts, int units) {
+                                                   uint32_t* __restrict__ counts, int units,
+                                                   const uint32_t* __restrict__ sat,
+                                                   const uint32_t* __restrict__ open_bits,
+                                                   uint32_t* __restrict__ unit_len, uint32_t* __restrict__ n_total) {
+    // open-tile bitmask in LDS for 16-bit tile ids (T <= 65536); wider grids read open[] directly
+    constexpr bool kMaskLds = sizeof(K) == 2;
     __shared__ K s_key[kSortMaxUnit];
     __shared__ uint32_t s_val[kSortMaxUnit];
     __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_open[kMaskLds ? 2048 : 1];
+    __shared__ uint32_t wsum[4];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
+    const bool filter = sat != nullptr;
     for (int d = t; d < ndig; d += 256) hist[d] = 0;
-    const uint32_t w0 = blockIdx.x * win, w1 = min(w0 + win, L);
+    const uint32_t w0 = pair0 + blockIdx.x * win, w1 = min(w0 + win, L);
+    const uint32_t wn = w1 - w0;
+    if (filter) {
+        for (uint32_t j = t; j < wn; j += 256) s_val[j] = 0xffffffffu;  // not emitted
+        if (kMaskLds)
+            for (int i = t; i < (gx * gy + 31) / 32; i += 256) s_open[i] = open_bits[i];
+        __syncthreads();
+    }
+    auto is_open = [&](uint32_t tile) -> bool {
+        const uint32_t word = kMaskLds ? s_open[tile >> 5] : open_bits[tile >> 5];
+        return ((word >> (tile & 31)) & 1u) != 0;
+    };
+    const int sw = gx + 1;
     const int s0 = (int)first[blockIdx.x];
     for (int base = s0;; base += 256) {
         const int s = base + t;
@@ -163,22 +241,29 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                 const float4 A = splats[g].a;
                 int x0, y0, x1, y1;
                 tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
-                const float qmax = cull ? cull_qmax(splats[g].b.y) : 0.f;
-                const float cz = cull ? splats[g].b.x : 0.f;
-                uint32_t pos = a;
-                for (int y = y0; y < y1 && pos < hi; y++) {
-                    int l = x0, h = x1;
-                    if (cull) cull_row_span(A.x, A.y, A.z, A.w, cz, qmax, y, x0, x1, &l, &h);
-                    const uint32_t c = h > l ? (uint32_t)(h - l) : 0u;
-                    if (pos + c <= lo) {  // row entirely before the window
-                        pos += c;
-                        continue;
-                    }
-                    for (int x = l; x < h && pos < hi; x++, pos++)
-                        if (pos >= lo) {
-                            s_key[pos - w0] = (K)(y * gx + x);
-                            s_val[pos - w0] = g;
+                const bool any_open =
+                    !filter || (sat[y1 * sw + x1] + sat[y0 * sw + x0] - sat[y0 * sw + x1] - sat[y1 * sw + x0]) > 0;
+                if (any_open) {
+                    const float qmax = cull ? cull_qmax(splats[g].b.y) : 0.f;
+                    const float cz = cull ? splats[g].b.x : 0.f;
+                    uint32_t pos = a;
+                    for (int y = y0; y < y1 && pos < hi; y++) {
+                        int l = x0, h = x1;
+                        if (cull) cull_row_span(A.x, A.y, A.z, A.w, cz, qmax, y, x0, x1, &l, &h);
+                        const uint32_t c = h > l ? (uint32_t)(h - l) : 0u;
+                        if (pos + c <= lo) {  // row entirely before the window
+                            pos += c;
+                            continue;
                         }
+                        for (int x = l; x < h && pos < hi; x++, pos++)
+                            if (pos >= lo) {
+                                const uint32_t tile = (uint32_t)(y * gx + x);
+                                if (!filter || is_open(tile)) {
+                                    s_key[pos - w0] = (K)tile;
+                                    s_val[pos - w0] = g;
+                                }
+                            }
+                    }
                 }
             }
         }
@@ -188,31 +273,72 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     }
     __syncthreads();
     const uint32_t mask = (uint32_t)ndig - 1u;
-    for (uint32_t j = t; j < w1 - w0; j += 256) {
-        const K k = s_key[j];
-        keys[w0 + j] = k;
-        vals[w0 + j] = s_val[j];
-        atomicAdd(&hist[(uint32_t)k & mask], 1u);
+    K* const kout = keys + (size_t)blockIdx.x * win;
+    uint32_t* const vout = vals + (size_t)blockIdx.x * win;
+    if (!filter) {
+        for (uint32_t j = t; j < wn; j += 256) {
+            const K k = s_key[j];
+            kout[j] = k;
+            vout[j] = s_val[j];
+            atomicAdd(&hist[(uint32_t)k & mask], 1u);
+        }
+    } else {
+        // order-preserving compaction in rounds of 256 slots: wave ballots give each kept pair its
+        // rank inside the round, the four wave totals the round's block offsets
+        const int lane = t & 63, wv = t >> 6;
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t carry = 0;
+        for (uint32_t r0 = 0; r0 < wn; r0 += 256) {
+            const uint32_t j = r0 + t;
+            const uint32_t v = j < wn ? s_val[j] : 0xffffffffu;
+            const bool kept = v != 0xffffffffu;
+            const uint64_t m = __ballot(kept);
+            if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t pre = carry, tot = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                pre += i < wv ? wsum[i] : 0u;
+                tot += wsum[i];
+            }
+            if (kept) {
+                const K k = s_key[j];
+                const uint32_t pos = pre + (uint32_t)__popcll(m & lt);
+                kout[pos] = k;
+                vout[pos] = v;
+                atomicAdd(&hist[(uint32_t)k & mask], 1u);
+            }
+            carry += tot;
+            __syncthreads();
+        }
+        if (t == 0) {
+            unit_len[blockIdx.x] = carry;
+            if (carry) atomicAdd(n_total, carry);
+        }
     }
     __syncthreads();
     for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + blockIdx.x] = hist[d];
 }
 
 template <typename K>
-__global__ __launch_bounds__(256) void k_ranges(int L, const K* __restrict__ keys, uint2* __restrict__ ranges) {
+__global__ __launch_bounds__(256) void k_ranges(int L, const K* __restrict__ keys, uint2* __restrict__ ranges,
+                                                uint32_t base, const uint32_t* __restrict__ n_dev) {
+    // L: host bound; n_dev (optional): the device-side count of a filtered list.  Ranges are
+    // absolute point_list indices (base + position).
+    const int n = n_dev ? (int)*n_dev : L;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L) return;
+    if (i >= n) return;
     const uint32_t cur = keys[i];
     if (i == 0) {
-        ranges[cur].x = 0;
+        ranges[cur].x = base;
     } else {
         const uint32_t prev = keys[i - 1];
         if (cur != prev) {
-            ranges[prev].y = i;
-            ranges[cur].x = i;
+            ranges[prev].y = base + i;
+            ranges[cur].x = base + i;
         }
     }
-    if (i == L - 1) ranges[cur].y = L;
+    if (i == n - 1) ranges[cur].y = base + n;
 }
 
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
@@ -244,28 +370,30 @@ void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint2* tiles, 
 }
 
 template <typename K>
-void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats, const int* radii,
-                      int gx, int gy, int cull, uint32_t* first, uint32_t win, int nwin, uint32_t L, K* keys,
-                      uint32_t* vals, int dbits, uint32_t* counts, hipStream_t st) {
-    if (P == 0 || L == 0 || win > (uint32_t)kSortMaxUnit) return;  // win comes from radix_sort_plan
-    k_window_starts<<<blocks_for(P), 256, 0, st>>>(P, offsets, win, nwin, first);
-    k_duplicate<K><<<nwin, 256, 0, st>>>(P, idx_sorted, offsets, splats, radii, gx, gy, cull, first, win, L, keys,
-                                          vals, dbits, counts, nwin);
+void launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
+    if (d.P == 0 || d.nwin == 0 || d.win > (uint32_t)kSortMaxUnit) return;  // win comes from radix_sort_plan
+    k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.P, d.offsets, d.pair0, d.win, d.nwin, d.first);
+    k_duplicate<K><<<d.nwin, 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
+                                            d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts, d.nwin,
+                                            d.sat, d.open_bits, d.unit_len, d.n_total);
 }
-template void launch_duplicate<uint16_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int, int,
-                                         uint32_t*, uint32_t, int, uint32_t, uint16_t*, uint32_t*, int, uint32_t*,
-                                         hipStream_t);
-template void launch_duplicate<uint32_t>(int, const uint32_t*, const uint2*, const Splat*, const int*, int, int, int,
-                                         uint32_t*, uint32_t, int, uint32_t, uint32_t*, uint32_t*, int, uint32_t*,
-                                         hipStream_t);
+template void launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
+template void launch_duplicate<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
+
+void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_t* open_bits, hipStream_t st) {
+    if ((size_t)(gx + 1) * (gy + 1) <= (size_t)kSatLds)
+        k_open_sat<true><<<1, 1024, 0, st>>>(gx, gy, open, sat, open_bits);
+    else
+        k_open_sat<false><<<1, 1024, 0, st>>>(gx, gy, open, sat, open_bits);
+}
 
 template <typename K>
-void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st) {
+void launch_ranges(int L, const K* keys, uint2* ranges, uint32_t base, const uint32_t* n_dev, hipStream_t st) {
     if (L == 0) return;
-    k_ranges<K><<<blocks_for(L), 256, 0, st>>>(L, keys, ranges);
+    k_ranges<K><<<blocks_for(L), 256, 0, st>>>(L, keys, ranges, base, n_dev);
 }
-template void launch_ranges<uint16_t>(int, const uint16_t*, uint2*, hipStream_t);
-template void launch_ranges<uint32_t>(int, const uint32_t*, uint2*, hipStream_t);
+template void launch_ranges<uint16_t>(int, const uint16_t*, uint2*, uint32_t, const uint32_t*, hipStream_t);
+template void launch_ranges<uint32_t>(int, const uint32_t*, uint2*, uint32_t, const uint32_t*, hipStream_t);
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;

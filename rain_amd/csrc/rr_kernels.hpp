@@ -27,6 +27,15 @@ struct PreArgs {
     const float* shs_rest;       // raw mode: f_rest [P,M-1,3] (shs = f_dc [P,1,3])
 };
 
+// Early-stop binning (rr_api.hip): the tile lists are built in two phases.  Phase A bins the
+// depth-ordered pairs [0, L_A) for every tile and blends them; a tile whose pixels have all
+// saturated is final.  Phase B bins the pairs [L_A, L) only for the tiles still open and resumes
+// their blend from the state phase A left in the image buffers.  A tile's list is then
+// A-list ++ B-list (ranges / ranges_b), which is exactly the prefix of its full depth-ordered
+// list that blending can reach.
+enum BlendPhase { kBlendSingle = 0, kBlendPhaseA = 1, kBlendPhaseB = 2 };
+constexpr uint32_t kDoneBit = 0x80000000u;  // n_contrib between the phases: pixel saturated
+
 struct BlendFwdArgs {
     int W, H, gx, gy;
     const uint2* ranges;
@@ -38,11 +47,15 @@ struct BlendFwdArgs {
     uint32_t* tile_max;
     float* out_color;
     float* out_depth;
+    const uint2* ranges_b;  // phase B lists
+    uint8_t* open;          // [T] tile still open after phase A
+    int phase;              // BlendPhase
 };
 
 struct BlendBwdArgs {
     int W, H, gx, gy;
     const uint2* ranges;
+    const uint2* ranges_b;  // phase-B lists (all {0,0} for single-phase binning)
     const uint32_t* point_list;
     const Splat* splats;
     const uint32_t* tile_max;
@@ -90,11 +103,33 @@ struct GaussBwdArgs {
 void launch_preprocess(const PreArgs& a, hipStream_t st);
 void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint2* tiles, uint2* out, hipStream_t st);
 template <typename K>
-void launch_duplicate(int P, const uint32_t* idx_sorted, const uint2* offsets, const Splat* splats, const int* radii,
-                      int gx, int gy, int cull, uint32_t* first, uint32_t win, int nwin, uint32_t L, K* keys,
-                      uint32_t* vals, int dbits, uint32_t* counts, hipStream_t st);
+struct DupArgs {
+    int P;
+    const uint32_t* idx_sorted;
+    const uint2* offsets;
+    const Splat* splats;
+    const int* radii;
+    int gx, gy, cull;
+    uint32_t* first;     // [nwin] first Gaussian of each window
+    uint32_t pair0;      // pair index of window 0
+    uint32_t win;        // pairs per window (= sort unit)
+    int nwin;
+    uint32_t L;          // end of the pair range
+    K* keys;             // window k writes [k*win, ...)
+    uint32_t* vals;
+    int dbits;           // first-pass digit width of the tile sort
+    uint32_t* counts;    // its per-window digit counts
+    // phase B (early-stop binning); all null for an unfiltered pass
+    const uint32_t* sat;
+    const uint32_t* open_bits;
+    uint32_t* unit_len;
+    uint32_t* n_total;
+};
 template <typename K>
-void launch_ranges(int L, const K* keys, uint2* ranges, hipStream_t st);
+void launch_duplicate(const DupArgs<K>& d, hipStream_t st);
+void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_t* open_bits, hipStream_t st);
+template <typename K>
+void launch_ranges(int L, const K* keys, uint2* ranges, uint32_t base, const uint32_t* n_dev, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
@@ -106,12 +141,16 @@ constexpr int kSortMaxUnit = 4096;
 
 // rr_sort.hip: stable LSD radix sort of (K key, u32 value) pairs on bits [begin_bit, end_bit).
 // vals_in == nullptr means values = input index.  keys_out may be nullptr only for a single pass.
+// n is the (host-known) capacity; unit_len (per-unit item counts of a sparse first pass, counts
+// produced by the caller) and n_dev (device-side item count after compaction) are optional.
 template <typename K>
 size_t radix_sort_temp_bytes(size_t n, int bits);
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
-                            bool first_counts_ready = false);
+                            bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
+                            const uint32_t* n_dev = nullptr);
+const char* radix_sort_last_error();  // which check failed in the last radix_sort_pairs call
 // Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
 // can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass
 // first_counts_ready = true).

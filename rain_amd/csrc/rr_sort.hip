@@ -8,7 +8,8 @@
 // one workgroup (4 wave64s) x R rounds x 64 items (R chosen per call so that small inputs still
 // spread over enough workgroups):
 //   * k_rs_count: digit histogram of the unit in LDS -> counts[digit][unit] (digit-major);
-//   * rocprim::exclusive_scan over counts gives every (digit, unit) its first output slot;
+//   * k_rs_scan_rows: per digit, exclusive scan of its counts over the units (+ digit totals);
+//     the scatter adds the digit bases, so every (digit, unit) gets its first output slot;
 //   * k_rs_scatter: (1) per-wave digit counts, (2) block-local digit starts in LDS, (3) each wave
 //     walks its rounds in order; lanes holding the same digit find each other with one ballot per
 //     digit bit (wave-wide match), rank = popcount of lower matching lanes, the group leader
@@ -16,9 +17,9 @@
 //     position, (4) the staged unit is written out in order, so consecutive threads write
 //     consecutive addresses of each digit's run (coalesced) instead of scattering single items.
 // Order inside a unit is (wave, round, lane) = input order and units are scanned in order, so
-// every pass is stable.  Passes = ceil(bits / 8) with the bits spread evenly (13 -> 7 + 6).
-#include <rocprim/device/device_scan.hpp>
-
+// every pass is stable.  A producer that filters its output (the early-stop duplicate pass) may
+// leave units sparse (unit_len[u] items each, positions kept) and only the device knows the total
+// (n_dev): the first pass then compacts, and every later pass reads the count from the device.  Passes = ceil(bits / 8) with the bits spread evenly (13 -> 7 + 6).
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
@@ -31,21 +32,36 @@ constexpr int kMaxRounds = 16;  // rounds of 64 items per wave
 constexpr int kMaxUnitItems = 64 * kWaves * kMaxRounds;  // 4096
 static_assert(kMaxUnitItems == kSortMaxUnit, "rr_kernels.hpp kSortMaxUnit");
 
+// Items of one unit: [unit * unit_items, unit * unit_items + len).  Contiguous input has
+// len = min(unit_items, n - base) with n from the host or, when only the device knows it (a
+// filtered producer), from *n_dev; a producer that leaves its units sparse passes every unit's
+// length in unit_len.
+__device__ __forceinline__ uint32_t unit_length(const uint32_t* unit_len, const uint32_t* n_dev, size_t n, int unit,
+                                                uint32_t unit_items) {
+    if (unit_len) return unit_len[unit];
+    const size_t nn = n_dev ? (size_t)*n_dev : n;
+    const size_t base = (size_t)unit * unit_items;
+    return base >= nn ? 0u : (uint32_t)min((size_t)unit_items, nn - base);
+}
+
 template <typename K>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ keys, size_t n, int shift, int dbits,
-                                                          int rounds, uint32_t* __restrict__ counts, int units) {
+                                                          int rounds, uint32_t* __restrict__ counts, int units,
+                                                          const uint32_t* __restrict__ n_dev) {
     __shared__ uint32_t hist[256];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
     for (int d = t; d < ndig; d += 64 * kWaves) hist[d] = 0;
     const int unit = blockIdx.x;
-    const size_t base = (size_t)unit * rounds * 64 * kWaves;
+    const uint32_t unit_items = (uint32_t)rounds * 64 * kWaves;
+    const size_t base = (size_t)unit * unit_items;
+    const uint32_t len = unit_length(nullptr, n_dev, n, unit, unit_items);
     const uint32_t mask = (uint32_t)ndig - 1u;
     uint32_t dr[kMaxRounds];
 #pragma unroll
     for (int r = 0; r < kMaxRounds; r++) {  // all loads in flight before the first LDS atomic
-        const size_t i = base + (size_t)r * 64 * kWaves + t;
-        dr[r] = (r < rounds && i < n) ? (((uint32_t)keys[i] >> shift) & mask) : 0xffffffffu;
+        const uint32_t li = (uint32_t)r * 64 * kWaves + t;
+        dr[r] = (r < rounds && li < len) ? (((uint32_t)keys[base + li] >> shift) & mask) : 0xffffffffu;
     }
     __syncthreads();
 #pragma unroll
@@ -55,12 +71,52 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ 
     for (int d = t; d < ndig; d += 64 * kWaves) counts[(size_t)d * units + unit] = hist[d];
 }
 
+// Exclusive scan of each digit's row of counts over the units (one workgroup per digit, rows
+// walked in tiles of 256) -> offsets[d][unit] relative to the digit, and the digit's total.  The
+// scatter adds the digit bases (exclusive scan of the <= 256 totals) itself.  Replaces a device
+// scan call and its host-side dispatch overhead.
+__global__ __launch_bounds__(256) void k_rs_scan_rows(const uint32_t* __restrict__ counts,
+                                                      uint32_t* __restrict__ offsets, int units,
+                                                      uint32_t* __restrict__ totals) {
+    __shared__ uint32_t wsum[4];
+    const int d = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t* row = counts + (size_t)d * units;
+    uint32_t* out = offsets + (size_t)d * units;
+    uint32_t carry = 0;
+    for (int base = 0; base < units; base += 256) {
+        const int u = base + t;
+        const uint32_t v = u < units ? row[u] : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t wpre = 0, tile = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            wpre += i < w ? wsum[i] : 0u;
+            tile += wsum[i];
+        }
+        if (u < units) out[u] = carry + wpre + incl - v;
+        carry += tile;
+        __syncthreads();
+    }
+    if (t == 0) totals[d] = carry;
+}
+
 template <typename K>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict__ keys_in,
                                                             const uint32_t* __restrict__ vals_in,
                                                             K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                             size_t n, int shift, int dbits, int rounds,
-                                                            const uint32_t* __restrict__ offsets, int units) {
+                                                            const uint32_t* __restrict__ offsets, int units,
+                                                            const uint32_t* __restrict__ totals,
+                                                            const uint32_t* __restrict__ unit_len,
+                                                            const uint32_t* __restrict__ n_dev) {
+    __shared__ uint32_t dbase[256];         // first output slot of each digit
     __shared__ uint32_t wcnt[kWaves][256];  // per-wave digit counts, then per-wave cursors
     __shared__ uint32_t dstart[256];        // block-local start of each digit's run
     __shared__ uint32_t goff[256];          // global slot of block-local position 0 of each digit's run
@@ -70,11 +126,35 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     const int ndig = 1 << dbits;
     const uint32_t mask = (uint32_t)ndig - 1u;
     const int unit = blockIdx.x;
-    const size_t ubase = (size_t)unit * rounds * 64 * kWaves;
-    // wave w owns the contiguous items [wbase, wbase + 64 * rounds) of the unit
-    const size_t wbase = ubase + (size_t)w * 64 * rounds;
+    const uint32_t unit_items = (uint32_t)rounds * 64 * kWaves;
+    const size_t ubase = (size_t)unit * unit_items;
+    const uint32_t len = unit_length(unit_len, n_dev, n, unit, unit_items);
+    // wave w owns the contiguous items [wl, wl + 64 * rounds) of the unit (local indices)
+    const uint32_t wl = (uint32_t)w * 64 * rounds;
+    const size_t wbase = ubase + wl;
     for (int d = lane; d < ndig; d += 64) wcnt[w][d] = 0;
     for (int d = t; d < ndig; d += 64 * kWaves) goff[d] = offsets[(size_t)d * units + unit];
+    if (w == 1) {  // digit bases: exclusive scan of the digit totals (4 per lane, then shuffles)
+        uint32_t tv[4], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int d = 4 * lane + i;
+            tv[i] = d < ndig ? totals[d] : 0u;
+            sum += tv[i];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += y;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            dbase[4 * lane + i] = run;
+            run += tv[i];
+        }
+    }
     // the wave's items go to registers once (all loads in flight together); counting, ranking
     // and staging then run from registers
     K kr[kMaxRounds];
@@ -82,15 +162,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
 #pragma unroll
     for (int r = 0; r < kMaxRounds; r++) {
         const size_t i = wbase + (size_t)r * 64 + lane;
-        const bool valid = r < rounds && i < n;
+        const bool valid = r < rounds && wl + (uint32_t)r * 64 + lane < len;
         kr[r] = valid ? keys_in[i] : (K)0;
         vr[r] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kMaxRounds; r++) {
-        const size_t i = wbase + (size_t)r * 64 + lane;
-        if (r < rounds && i < n) atomicAdd(&wcnt[w][((uint32_t)kr[r] >> shift) & mask], 1u);
+        if (r < rounds && wl + (uint32_t)r * 64 + lane < len) atomicAdd(&wcnt[w][((uint32_t)kr[r] >> shift) & mask], 1u);
     }
     __syncthreads();
     // block-local starts: digits in order, then waves in order inside each digit.  Wave 0 scans the
@@ -118,7 +197,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
             const int d = 4 * lane + i;
             if (d < ndig) {
                 dstart[d] = run;
-                goff[d] -= run;
+                goff[d] += dbase[d] - run;
                 uint32_t r2 = run;
 #pragma unroll
                 for (int v = 0; v < kWaves; v++) {
@@ -134,9 +213,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < kMaxRounds; r++) {
-        if (r >= rounds || wbase + (size_t)r * 64 >= n) continue;  // wave-uniform; keeps the loop unrollable
-        const size_t i = wbase + (size_t)r * 64 + lane;
-        const bool valid = i < n;
+        if (r >= rounds || wl + (uint32_t)r * 64 >= len) continue;  // wave-uniform; keeps the loop unrollable
+        const bool valid = wl + (uint32_t)r * 64 + lane < len;
         const K k = kr[r];
         const uint32_t v = vr[r];
         const uint32_t d = ((uint32_t)k >> shift) & mask;
@@ -157,7 +235,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
         }
     }
     __syncthreads();
-    const int nu = (int)min((size_t)rounds * 64 * kWaves, n - ubase);
+    const int nu = (int)len;
     for (int j = t; j < nu; j += 64 * kWaves) {
         const K k = s_key[j];
         const uint32_t d = ((uint32_t)k >> shift) & mask;
@@ -172,8 +250,7 @@ struct SortLayout {
     uint32_t* vals_alt;
     uint32_t* counts;
     uint32_t* offsets;
-    void* scan_temp;
-    size_t scan_bytes;
+    uint32_t* totals;  // [256] per-digit totals of the current pass
     size_t total;
 };
 
@@ -193,10 +270,6 @@ SortLayout sort_layout(void* buf, size_t n, int bits) {
     const int passes = bits <= 0 ? 0 : (bits + 7) / 8;
     const int dmax = passes ? (bits + passes - 1) / passes : 0;
     const size_t nc = std::max<size_t>(((size_t)1 << dmax) * units, 1);
-    s.scan_bytes = 0;
-    if (n > 0)
-        (void)rocprim::exclusive_scan(nullptr, s.scan_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, nc,
-                                      rocprim::plus<uint32_t>(), (hipStream_t)0);
     char* p = static_cast<char*>(buf);
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -208,7 +281,7 @@ SortLayout sort_layout(void* buf, size_t n, int bits) {
     s.vals_alt = static_cast<uint32_t*>(take(n * 4));
     s.counts = static_cast<uint32_t*>(take(nc * 4));
     s.offsets = static_cast<uint32_t*>(take(nc * 4));
-    s.scan_temp = take(s.scan_bytes);
+    s.totals = static_cast<uint32_t*>(take(256 * 4));
     s.total = off;
     return s;
 }
@@ -235,15 +308,20 @@ RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
     return p;
 }
 
+thread_local const char* g_why = "";
+const char* radix_sort_last_error() { return g_why; }
+
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
-                            bool first_counts_ready) {
+                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
-    if (n > 0xffffffffull || bits <= 0 || bits > (int)(8 * sizeof(K))) return hipErrorInvalidValue;
+    g_why = "";
+    if (n > 0xffffffffull || bits <= 0 || bits > (int)(8 * sizeof(K))) return g_why = "bad size/bits", hipErrorInvalidValue;
+    if (unit_len && !n_dev) return g_why = "sparse units without n_dev", hipErrorInvalidValue;
     const SortLayout s = sort_layout<K>(temp, n, bits);
-    if (temp_bytes < s.total) return hipErrorInvalidValue;
+    if (temp_bytes < s.total) return g_why = "temp too small", hipErrorInvalidValue;
     const int passes = (bits + 7) / 8;
     const int rounds = rounds_for(n);
     const int units = (int)((n + (size_t)64 * kWaves * rounds - 1) / ((size_t)64 * kWaves * rounds));
@@ -258,29 +336,31 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
         const bool to_out = ((passes - 1 - p) % 2) == 0;
         K* kdst = to_out ? keys_out : static_cast<K*>(s.keys_alt);
         uint32_t* vdst = to_out ? vals_out : s.vals_alt;
-        if (!last && kdst == nullptr) return hipErrorInvalidValue;  // intermediate passes need key storage
-        const size_t nc = ((size_t)1 << dbits) * (size_t)units;
-        if (!(p == 0 && first_counts_ready))
-            k_rs_count<K><<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units);
-        size_t sb = s.scan_bytes;
-        hipError_t e = rocprim::exclusive_scan(s.scan_temp, sb, s.counts, s.offsets, 0u, nc,
-                                               rocprim::plus<uint32_t>(), st);
-        if (e != hipSuccess) return e;
+        if (!last && kdst == nullptr) return g_why = "no key storage", hipErrorInvalidValue;
+        if (!(p == 0 && first_counts_ready)) {
+            if (p == 0 && unit_len) return g_why = "sparse units need producer counts", hipErrorInvalidValue;
+            k_rs_count<K><<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev);
+        }
+        k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
         k_rs_scatter<K><<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets,
-                                                       units);
+                                                       units, s.totals, p == 0 ? unit_len : nullptr, n_dev);
         ksrc = kdst;
         vsrc = vdst;
         shift += dbits;
     }
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) g_why = "kernel launch";
+    return e;
 }
 
 template size_t radix_sort_temp_bytes<uint16_t>(size_t, int);
 template size_t radix_sort_temp_bytes<uint32_t>(size_t, int);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
-                                               size_t, int, int, hipStream_t, bool);
+                                               size_t, int, int, hipStream_t, bool, const uint32_t*,
+                                               const uint32_t*);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
-                                               size_t, int, int, hipStream_t, bool);
+                                               size_t, int, int, hipStream_t, bool, const uint32_t*,
+                                               const uint32_t*);
 template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int);
 template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int);
 

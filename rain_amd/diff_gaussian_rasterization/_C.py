@@ -26,6 +26,13 @@ NUM_CHANNELS = 3
 # Exact tile culling (include/rain_raster.h RR_FLAG_NO_TILE_CULLING): identical outputs, fewer
 # (tile, Gaussian) pairs.  RAIN_TILE_CULLING=0 restores the reference's bounding-square binning.
 TILE_CULLING = os.environ.get("RAIN_TILE_CULLING", "1") != "0"
+# Early-stop binning (include/rain_raster.h RR_FLAG_FULL_BINNING): identical outputs, tile lists
+# cut past saturation.  False (or RAIN_EARLY_STOP=0) bins every pair (full per-tile lists).
+EARLY_STOP = os.environ.get("RAIN_EARLY_STOP", "1") != "0"
+
+
+def frame_flags():
+    return (0 if TILE_CULLING else N.RR_FLAG_NO_TILE_CULLING) | (0 if EARLY_STOP else N.RR_FLAG_FULL_BINNING)
 
 
 def _ptr(t):
@@ -52,7 +59,7 @@ def _require_device(means3D):
 
 
 def _frame(P, degree, M, W, H, tan_fovx, tan_fovy, scale_modifier, low_pass, prefiltered, debug):
-    flags = 0 if TILE_CULLING else N.RR_FLAG_NO_TILE_CULLING
+    flags = frame_flags()
     return N.RRFrame(int(P), int(degree), int(M), int(W), int(H), float(tan_fovx), float(tan_fovy),
                      float(scale_modifier), float(low_pass), int(bool(prefiltered)), int(bool(debug)), flags)
 
@@ -198,4 +205,4 @@ def frame_stats(geomBuffer, imageBuffer, P, W, H):
     N.check(N.raster().rr_read_frame_stats(ctypes.byref(f), _ptr(geomBuffer), _ptr(imageBuffer), ctypes.byref(st),
                                            N.stream_of(geomBuffer)), "frame_stats")
     return dict(num_rendered=st.num_rendered, num_visible=st.num_visible, l_eff=st.l_eff, tiles=st.tiles,
-                num_pairs=st.num_pairs)
+                num_pairs=st.num_pairs, num_binned=st.num_binned)

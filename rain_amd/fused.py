@@ -55,7 +55,7 @@ def forward(model, camera, bg: torch.Tensor, low_pass: float, scale_modifier: fl
     M = 1 + f_rest.shape[1]
     D = model.active_sh_degree
     L = N.raster()
-    flags = N.RR_FLAG_RAW_PARAMS | (0 if _C.TILE_CULLING else N.RR_FLAG_NO_TILE_CULLING)
+    flags = N.RR_FLAG_RAW_PARAMS | _C.frame_flags()
     frame = N.RRFrame(P, D, M, W, H, math.tan(camera.FoVx * 0.5), math.tan(camera.FoVy * 0.5),
                       float(scale_modifier), float(low_pass), 0, 0, flags)
     keep = (bg.contiguous(), camera.world_view_transform.contiguous(), camera.full_proj_transform.contiguous(),

@@ -1,0 +1,112 @@
+"""Early-stop binning (include/rain_raster.h RR_FLAG_FULL_BINNING, rr_set_binning_config): tile
+lists built in two phases, cut past saturation.  The outputs must be those of full binning —
+forward bitwise (every pixel blends the same pairs in the same order), gradients within the
+atomics-order tolerance — and of the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from tests.common import gpu_run, make_scene, oracle_run, rel_l1
+from tests.test_parity_gpu import _check_forward, _check_grads, _dpix
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def split(monkeypatch):
+    """Force the two-phase path onto small frames: phase A = L/den pairs, any frame size."""
+    from rain_amd import _native as N
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    def set_split(den):
+        N.check(N.raster().rr_set_binning_config(den, 1), "binning config")
+
+    yield set_split
+    N.check(N.raster().rr_set_binning_config(0, 0), "binning config")
+    monkeypatch.setattr(_C, "EARLY_STOP", True)
+
+
+def _stats(out, P, st):
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    geom, binning, img = out["buffers"]
+    return _C.frame_stats(geom, img, P, st["image_width"], st["image_height"])
+
+
+@pytest.mark.parametrize("den", [2, 8, 64])
+@pytest.mark.parametrize("scene", [dict(P=6000, W=192, H=144, sh_degree=3),
+                                   dict(P=3000, W=200, H=120, sh_degree=2, scale_mult=3.0),
+                                   dict(P=2500, W=128, H=96, sh_degree=3, bg=(1.0, 0.5, 0.25))])
+def test_two_phase_equals_full_binning(gpu, split, monkeypatch, scene, den):
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    inp, st = make_scene(**scene)
+    P = inp["means3D"].shape[0]
+    dpix = _dpix(st)
+    monkeypatch.setattr(_C, "EARLY_STOP", False)
+    full = gpu_run(inp, st, gpu, dL_dpix=dpix)
+    fs = _stats(full, P, st)
+    monkeypatch.setattr(_C, "EARLY_STOP", True)
+    split(den)
+    early = gpu_run(inp, st, gpu, dL_dpix=dpix)
+    es = _stats(early, P, st)
+    assert es["num_pairs"] == fs["num_pairs"] and es["num_rendered"] == fs["num_rendered"]
+    assert fs["num_binned"] == fs["num_pairs"]
+    assert es["num_binned"] <= es["num_pairs"]
+    np.testing.assert_array_equal(early["radii"], full["radii"])
+    np.testing.assert_array_equal(early["color"], full["color"])  # same pairs, same order: bitwise
+    np.testing.assert_array_equal(early["depth"], full["depth"])
+    ev = _C.debug_views(early["buffers"][0], early["buffers"][1], early["buffers"][2], early["num_rendered"], P,
+                        st["image_width"], st["image_height"])
+    fv = _C.debug_views(full["buffers"][0], full["buffers"][1], full["buffers"][2], full["num_rendered"], P,
+                        st["image_width"], st["image_height"])
+    assert torch.equal(ev["n_contrib"], fv["n_contrib"])
+    assert torch.equal(ev["final_T"], fv["final_T"])
+    assert torch.equal(ev["tile_max"], fv["tile_max"])
+    for k, a in early["grads"].items():
+        b = full["grads"][k]
+        if np.abs(b).sum() == 0:
+            assert np.abs(a).max() < 1e-8, k
+        else:
+            assert rel_l1(a, b) <= 1e-5, (k, rel_l1(a, b))
+
+
+def test_two_phase_cuts_saturated_tiles(gpu, split):
+    """Opaque, large splats saturate every tile early: phase B must bin only a small remainder."""
+    inp, st = make_scene(P=6000, W=192, H=144, sh_degree=1, scale_mult=3.0)
+    inp["opacities"] = torch.full_like(inp["opacities"], 0.95)
+    split(8)
+    out = gpu_run(inp, st, gpu)
+    s = _stats(out, inp["means3D"].shape[0], st)
+    assert s["num_binned"] < 0.5 * s["num_pairs"], s
+
+
+@pytest.mark.parametrize("case", [dict(P=3000, W=128, H=96, sh_degree=3),
+                                  dict(P=2000, W=100, H=75, sh_degree=3),
+                                  dict(P=1500, W=128, H=128, sh_degree=3, scale_mult=4.0)])
+def test_two_phase_matches_oracle(oracle, gpu, split, case):
+    inp, st = make_scene(**case)
+    dpix = _dpix(st)
+    ref = oracle_run(oracle, inp, st, dL_dpix=dpix)
+    split(4)
+    got = gpu_run(inp, st, gpu, dL_dpix=dpix)
+    _check_forward(ref, got)
+    _check_grads(ref, got)
+
+
+def test_fused_raw_path_two_phase(gpu, split):
+    """Training entry point (raw parameters, rain_amd.fused) under the two-phase path."""
+    from rain_amd import cameras, fused, synthetic
+    from rain_amd.gaussian_model import GaussianModel
+
+    g = GaussianModel(3, device="cuda")
+    g.set_params(synthetic.random_gaussians(20_000, sh_degree=3, seed=5, bench=True, device="cuda"))
+    g.active_sh_degree = 3
+    cam = cameras.fibonacci_cameras(8, 160, 120)[3].to("cuda")
+    bg = torch.zeros(3, device="cuda")
+    c_full, r_full, d_full, _ = fused.forward(g, cam, bg, 0.3)
+    split(8)
+    c, r, d, _ = fused.forward(g, cam, bg, 0.3)
+    assert torch.equal(r, r_full)
+    assert torch.equal(c, c_full)
+    assert torch.equal(d, d_full)

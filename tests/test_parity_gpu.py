@@ -81,6 +81,7 @@ def test_pair_order_and_image_state(oracle, gpu, monkeypatch):
     from rain_amd.diff_gaussian_rasterization import _C
 
     monkeypatch.setattr(_C, "TILE_CULLING", False)
+    monkeypatch.setattr(_C, "EARLY_STOP", False)  # full per-tile lists
     inp, st = make_scene(P=3000, W=128, H=96, sh_degree=3)
     ref = oracle_run(oracle, inp, st)
     got = gpu_run(inp, st, gpu)
@@ -105,11 +106,13 @@ def test_pair_order_and_image_state(oracle, gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("low_pass,scale_mult", [(0.3, 1.0), (0.3, 3.0), (50.0, 1.0)])
-def test_tile_culling_drops_only_invisible_pairs(oracle, gpu, low_pass, scale_mult):
+def test_tile_culling_drops_only_invisible_pairs(oracle, gpu, low_pass, scale_mult, monkeypatch):
     """With exact tile culling (default) each tile's list is an order-preserving subsequence of the
     reference's, every dropped pair has alpha < 1/255 (or power > 0) at every pixel of its tile
     (evaluated exactly like forward.cu:325-338), and the reference's num_rendered is returned."""
     from rain_amd.diff_gaussian_rasterization import _C
+
+    monkeypatch.setattr(_C, "EARLY_STOP", False)  # full per-tile lists
 
     inp, st = make_scene(P=2500, W=128, H=96, sh_degree=3, low_pass=low_pass, scale_mult=scale_mult)
     ref = oracle_run(oracle, inp, st)

@@ -82,8 +82,11 @@ def main():
         L = int(pl.numel())
         cuts = {}
         R0 = int(pr.min())  # culled Gaussians (no pairs) sort first
-        for frac in (1 / 32, 1 / 16, 1 / 8, 3 / 16, 1 / 4, 3 / 8):
-            R = R0 + int(frac * (P - R0))
+        # cut points in pair space: phase A bins the first f*L pairs (depth order) for every tile,
+        # phase B the rest only for tiles still open after A
+        cum = torch.cumsum(torch.bincount(pr, minlength=P), 0)
+        for frac in (1 / 64, 1 / 32, 1 / 16, 1 / 8, 1 / 4):
+            R = int(torch.searchsorted(cum, int(frac * L)))
             a_pairs = int((pr < R).sum())
             open_t = crank >= R
             b_pairs = int(((pr >= R) & open_t[tile_of]).sum())
