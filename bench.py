@@ -58,19 +58,20 @@ MODELED = ("preprocess", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd"
 
 
 def algorithmic_bytes(stage, st, P, W, H, K):
-    """SURVEY §8(d) per-launch algorithmic bytes.  L is the number of (tile, Gaussian) pairs this
-    implementation actually bins (num_pairs, after exact tile culling), not the reference's larger
-    num_rendered, so binning stages are not credited for pairs they never touch.  The tile sort is
-    priced at its minimum: read + write each u16 key and u32 value once."""
-    L, V, Le, T, N = st["num_pairs"], st["num_visible"], st["l_eff"], st["tiles"], W * H
+    """SURVEY §8(d) algorithmic bytes per frame (one training step renders one frame).  Binning
+    stages are priced on the pairs this implementation actually sorts into tile lists (num_binned:
+    after exact tile culling and early-stop binning), not on the reference's larger num_rendered, so
+    they are not credited for pairs they never write.  The tile sort is priced at its minimum: read
+    + write each key and u32 value once."""
+    Lb, V, Le, T, N = st["num_binned"], st["num_visible"], st["l_eff"], st["tiles"], W * H
     M = K
     kw = 2 if T <= 65536 else 4
     return {
         "preprocess": 20 * P + V * (99 + 12 * K),
         "scan": 8 * P,
-        "duplicate": 4 * P + 16 * V + (kw + 4) * L,
-        "tile_sort": 2 * (kw + 4) * L,
-        "ranges": kw * L + 8 * T,
+        "duplicate": 4 * P + 16 * V + (kw + 4) * Lb,
+        "tile_sort": 2 * (kw + 4) * Lb,
+        "ranges": kw * Lb + 8 * T,
         "blend_fwd": 8 * T + 44 * Le + 24 * N,
         "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
         "gauss_bwd": 4 * P * (27 + 3 * M) + 4 * P + 88 * V + 4 * P + V * (143 + 24 * K),
@@ -208,7 +209,8 @@ def main():
     kernels = {}
     for name, (ms, cnt) in breakdown.items():
         if cnt:
-            kernels[name] = {"ms_per_launch": ms / cnt, "launches": int(cnt), "total_ms": ms}
+            # per step (= per frame): early-stop binning runs the binning stages in two phases
+            kernels[name] = {"ms_per_step": ms / PW, "launches_per_step": cnt / PW, "total_ms": ms}
     if dom_timed and dom_timed[1]:
         byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2)
         dom_ms = dom_timed[0] / dom_timed[1]  # HIP events around every launch inside the timed loop
@@ -223,7 +225,7 @@ def main():
         for k in kernels:
             b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2)
             if b is not None:
-                kernels[k]["algorithmic_GBps"] = round(b / (kernels[k]["ms_per_launch"] * 1e-3) / 1e9, 1)
+                kernels[k]["algorithmic_GBps"] = round(b / (kernels[k]["ms_per_step"] * 1e-3) / 1e9, 1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -132,16 +132,16 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     la[q] = alpha;
                     dL_dalpha += tfbg[q] * inv;
                     const float dL_dG = Bv.y * dL_dalpha;
-                    const float gdx = G * dx, gdy = G * dy;
-                    const float dG_ddelx = -gdx * A.z - gdy * A.w;
-                    const float dG_ddely = -gdy * Bv.x - gdx * A.w;
-                    // the constant factors (0.5 W, 0.5 H, -0.5) are applied once per (tile,
-                    // Gaussian, component) at the flush below, not per pixel
-                    g0 += dL_dG * dG_ddelx;
-                    g1 += dL_dG * dG_ddely;
-                    g2 += gdx * dx * dL_dG;
-                    g3 += gdx * dy * dL_dG;
-                    g4 += gdy * dy * dL_dG;
+                    // dG/d(delta) = -G (conic . delta): the conic is the same for every pixel of
+                    // the pair, so only Sx = sum dL_dG G dx and Sy = sum dL_dG G dy are summed per
+                    // pixel, and the flush forms -(conic . S) once per (tile, Gaussian); it also
+                    // applies the constant factors (0.5 W, 0.5 H, -0.5)
+                    const float tx = dL_dG * (G * dx), ty = dL_dG * (G * dy);
+                    g0 += tx;
+                    g1 += ty;
+                    g2 += tx * dx;
+                    g3 += tx * dy;
+                    g4 += ty * dy;
                     g5 += G * dL_dalpha;
                 }
             }
@@ -161,7 +161,18 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
 #pragma unroll
                 for (int i = 1; i < NW; i++) v += s_g[i][e];
                 const int comp = e - pair * NGRAD;
-                v *= comp == 0 ? ddelx_dx : comp == 1 ? ddely_dy : comp <= 4 ? -0.5f : 1.f;
+                if (comp <= 1) {  // dL/dmean2D from (Sx, Sy): -(conic . S), then the NDC factor
+                    float sx = s_g[0][pair * NGRAD], sy = s_g[0][pair * NGRAD + 1];
+#pragma unroll
+                    for (int i = 1; i < NW; i++) {
+                        sx += s_g[i][pair * NGRAD];
+                        sy += s_g[i][pair * NGRAD + 1];
+                    }
+                    const float cw = s_a[pair].w;
+                    v = comp == 0 ? -(s_a[pair].z * sx + cw * sy) * ddelx_dx : -(s_b[pair].x * sy + cw * sx) * ddely_dy;
+                } else {
+                    v *= comp <= 4 ? -0.5f : 1.f;
+                }
                 if (v != 0.f) atomicAdd(a.gacc + (size_t)s_id[pair] * GACC_STRIDE + comp, v);
             }
         }
