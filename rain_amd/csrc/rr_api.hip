@@ -4,6 +4,8 @@
 // Replaces CudaRasterizer::Rasterizer::{forward,backward,markVisible}
 // (rasterizer_impl.cu:130-142,187-430) and the pybind wrappers (rasterize_points.cu:24-212).
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -68,12 +70,29 @@ struct SatAdd2 {
         return make_uint2(x < a.x ? 0xffffffffu : x, y < a.y ? 0xffffffffu : y);
     }
 };
+// The scan reads tiles[] through idx_sorted (depth order) on the fly: no gathered copy.
+struct GatherTiles {
+    const uint32_t* idx_sorted;
+    const uint2* tiles;
+    __host__ __device__ uint2 operator()(uint32_t s) const { return tiles[idx_sorted[s]]; }
+};
+using TilesInDepthOrder = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, GatherTiles, uint2>;
+TilesInDepthOrder tiles_in_depth_order(const uint32_t* idx_sorted, const uint2* tiles) {
+    return TilesInDepthOrder(rocprim::counting_iterator<uint32_t>(0u), GatherTiles{idx_sorted, tiles});
+}
+
 size_t depth_sort_temp(int P) { return P > 0 ? radix_sort_temp_bytes<uint32_t>((size_t)P, 32) : 0; }
 size_t scan_temp(int P) {
+    // memoized: queried by every carve (forward, render, backward) with the same P
+    static thread_local int last_p = -1;
+    static thread_local size_t last_bytes = 0;
+    if (P == last_p) return last_bytes;
     size_t bytes = 0;
     if (P > 0)
-        (void)rocprim::inclusive_scan(nullptr, bytes, (const uint2*)nullptr, (uint2*)nullptr, (size_t)P, SatAdd2(),
-                                      (hipStream_t)0);
+        (void)rocprim::inclusive_scan(nullptr, bytes, tiles_in_depth_order(nullptr, nullptr), (uint2*)nullptr,
+                                      (size_t)P, SatAdd2(), (hipStream_t)0);
+    last_p = P;
+    last_bytes = bytes;
     return bytes;
 }
 template <typename K>
@@ -88,8 +107,7 @@ struct Geom {
     uint32_t* depth_keys;
     uint32_t* depth_keys_sorted;
     uint32_t* idx_sorted;
-    uint2* tiles_sorted;  // tiles[] in depth order
-    uint2* offsets;       // inclusive prefix sum of tiles_sorted; .y of the last = reference num_rendered
+    uint2* offsets;       // inclusive prefix sum of tiles[] in depth order; .y of the last = num_rendered
     void* temp;
     size_t temp_bytes;
     size_t total;
@@ -103,7 +121,6 @@ Geom carve_geom(void* buf, int P) {
     g.depth_keys = c.take<uint32_t>(n);
     g.depth_keys_sorted = c.take<uint32_t>(n);
     g.idx_sorted = c.take<uint32_t>(n);
-    g.tiles_sorted = c.take<uint2>(n);
     g.offsets = c.take<uint2>(n);
     g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
@@ -355,10 +372,9 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     RR_STAGE_CHECK("depth sort");
     {
         StageTimer tm(RR_STAGE_SCAN, st);
-        launch_gather_tiles(P, gm.idx_sorted, gm.tiles, gm.tiles_sorted, st);
         size_t tb = gm.temp_bytes;
-        RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, gm.tiles_sorted, gm.offsets, (size_t)P,
-                                         SatAdd2(), st),
+        RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, tiles_in_depth_order(gm.idx_sorted, gm.tiles), gm.offsets,
+                                         (size_t)P, SatAdd2(), st),
                  "tile-count scan");
     }
     RR_STAGE_CHECK("scan");

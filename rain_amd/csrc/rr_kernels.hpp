@@ -101,7 +101,6 @@ struct GaussBwdArgs {
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);
-void launch_gather_tiles(int P, const uint32_t* idx_sorted, const uint2* tiles, uint2* out, hipStream_t st);
 template <typename K>
 struct DupArgs {
     int P;

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Build an A/B variant of librain_raster.so with extra compile definitions, into
+gpurun_variants/<name>.so (git-ignored; travels to the GPU box with the snapshot).
+
+    python tools/build_variant.py nostage -DRR_STAGE_SH=0
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from rain_amd import _build as B  # noqa: E402
+
+
+def main():
+    name, flags = sys.argv[1], sys.argv[2:]
+    out = os.path.join(ROOT, "gpurun_variants")
+    objdir = os.path.join(out, name + "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    srcs = B.LIBS["librain_raster.so"]
+
+    def cc(s):
+        src = os.path.join(B.CSRC, s)
+        obj = os.path.join(objdir, s.replace(".hip", ".o"))
+        cmd = [B.HIPCC, *B.CXXFLAGS, *B.EXTRA.get(s, []), *flags, "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode:
+            raise SystemExit(r.stderr)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=6) as ex:
+        objs = list(ex.map(cc, srcs))
+    target = os.path.join(out, name + ".so")
+    r = subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", target, *objs],
+                       capture_output=True, text=True)
+    if r.returncode:
+        raise SystemExit(r.stderr)
+    print(target)
+
+
+if __name__ == "__main__":
+    main()

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--points", type=int, default=1_000_000)
     ap.add_argument("--binning-split", type=int, default=0)
     ap.add_argument("--no-cprofile", action="store_true")
+    ap.add_argument("--raster-lib", default=None, help="alternative librain_raster.so (A/B of builds)")
     a = ap.parse_args()
     import torch
 
@@ -31,6 +32,8 @@ def main():
 
     from rain_amd import _native
 
+    if a.raster_lib:
+        _native.RASTER_LIB = os.path.abspath(a.raster_lib)
     dev = torch.device("cuda:0")
     if a.binning_split:
         _native.check(_native.raster().rr_set_binning_config(a.binning_split, 0), "binning config")
@@ -65,7 +68,7 @@ def main():
     pr.disable()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    print(f"split {a.binning_split} ms/step {1e3 * (t1 - t0) / a.steps:.3f}")
+    print(f"lib {a.raster_lib} split {a.binning_split} ms/step {1e3 * (t1 - t0) / a.steps:.3f}")
     if a.no_cprofile:
         return
     s = io.StringIO()

@@ -26,7 +26,6 @@ STAGES = [  # kernel-name pattern -> bench.py stage name
     (r"k_gauss_bwd", "gauss_bwd"),
     (r"k_duplicate", "duplicate"),
     (r"k_ranges", "ranges"),
-    (r"k_gather_tiles", "gather_tiles"),
 ]
 
 
