@@ -173,6 +173,10 @@ def main():
     iters_per_s = world * K / elapsed
     ms_per_step = 1000.0 * elapsed / K
 
+    # the reference's own timing bracket (train.py:71-117: iter_start before render, iter_end after
+    # loss.backward()): render forward + L1/SSIM + backward, no optimizer step, no densification
+    bracket_ms = _bracket(trainer, cams, gts, K if K < 50 else 50, world, dev)
+
     # forward-only throughput (preprocess -> blend incl. sorts and the L read-back), no autograd
     Pn = gauss.get_xyz.shape[0]
     with torch.no_grad():
@@ -216,6 +220,7 @@ def main():
         dom_ms = dom_timed[0] / dom_timed[1]  # HIP events around every launch inside the timed loop
         gbs = byts / (dom_ms * 1e-3) / 1e9
         roofline = {"kernel": dom, "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "measured_copy_GBps": _copy_peak(dev),
                     "ms_per_launch": round(dom_ms, 5), "launches": int(dom_timed[1]),
                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(dom),
                     "algorithmic_bytes_per_launch": int(byts),
@@ -251,6 +256,9 @@ def main():
                    "parallelism": f"dp{world} (view-sharded, RCCL all-reduce)" if world > 1 else "dp1",
                    "iterations": [start_iter + Wm + PW, end_iter]},
         "forward_mpix_per_s": round(fwd_mpix, 2),
+        "views_per_s": round(iters_per_s, 3),  # one view per rank per step: = value
+        "bracket_iters_per_s": round(world * 1000.0 / bracket_ms, 3),
+        "bracket_ms": round(bracket_ms, 4),
         "gaussians_after": int(Pn),
         "frame_stats": {k: int(v) for k, v in mean_stats.items()},
         "roofline": roofline,
@@ -262,6 +270,68 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _bracket(trainer, cams, gts, n, world, dev):
+    """ms per render-forward + loss + backward (the reference's iter_start..iter_end bracket,
+    train.py:71-117), max over ranks.  Gradients go to the parameters' .grad buffers; no Adam."""
+    import torch
+    import torch.distributed as dist
+
+    from rain_amd import fused
+    from rain_amd.loss import l1_ssim_backward, l1_ssim_forward
+
+    g, lam = trainer.g, trainer.opt.lambda_dssim
+    g.bind_flat_grad(extra=0, zero=False)
+    cache = fused.BinningCache()
+    grads = None
+
+    def one(i):
+        nonlocal grads
+        cam = cams[i % len(cams)]
+        image, _r, _d, st = fused.forward(g, cam, trainer.background, trainer.low_pass, cache=cache)
+        loss, _p, lws = l1_ssim_forward(image, gts[i % len(cams)], lam)
+        dimg = l1_ssim_backward(image, gts[i % len(cams)], lam, lws)
+        grads = dict(xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad,
+                     opacity=g._opacity.grad, scaling=g._scaling.grad, rotation=g._rotation.grad)
+        fused.backward(st, dimg, grads, None, None)
+
+    with torch.no_grad():
+        for i in range(3):
+            one(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(n):
+            one(i)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+    g.optimizer.zero_grad(set_to_none=True)
+    if world > 1:
+        e = torch.tensor([t], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        t = float(e.item())
+    return 1000.0 * t / n
+
+
+def _copy_peak(dev):
+    """Measured device-to-device copy bandwidth (read + write bytes / time), 1 GiB buffers."""
+    import torch
+
+    a = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    for _ in range(2):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    del a, b
+    return round(2 * (1 << 30) / (ms * 1e-3) / 1e9, 1)
 
 
 def _settings(cam, gauss, bg):
@@ -291,7 +361,7 @@ def _pmc_traffic(kernel):
         return None
 
 
-def _cpu_baseline(gauss, cam, bg, D, threads):
+def _cpu_baseline(gauss, cam, bg, D, threads, views=3):
     """The oracle (test infrastructure, `port` of the reference algorithm) on the same frame."""
     import numpy as np
     import torch
@@ -312,16 +382,20 @@ def _cpu_baseline(gauss, cam, bg, D, threads):
                     projmatrix=s.projmatrix.cpu().numpy(), sh_degree=D, campos=s.campos.cpu().numpy(),
                     low_pass=0.3)
     dpix = np.random.default_rng(0).standard_normal((3, s.image_height, s.image_width)).astype(np.float32)
-    t0 = time.perf_counter()
-    nr, color, radii, depth, state = O.forward(st, m, op, shs=sh, scales=sc, rotations=ro, nthreads=nthr)
-    t1 = time.perf_counter()
-    O.backward(state, st, m, radii, dpix, shs=sh, scales=sc, rotations=ro, nthreads=nthr)
-    t2 = time.perf_counter()
-    return {"value": round(1.0 / (t2 - t0), 4), "unit": "render fwd+bwd iters/s", "cores": int(O.lib().orc_threads()),
+    tf = tb = 0.0
+    for _ in range(views):  # the same frame `views` times: a bounded sample of ~10 s
+        t0 = time.perf_counter()
+        nr, color, radii, depth, state = O.forward(st, m, op, shs=sh, scales=sc, rotations=ro, nthreads=nthr)
+        t1 = time.perf_counter()
+        O.backward(state, st, m, radii, dpix, shs=sh, scales=sc, rotations=ro, nthreads=nthr)
+        t2 = time.perf_counter()
+        tf += t1 - t0
+        tb += t2 - t1
+    return {"value": round(views / (tf + tb), 4), "unit": "render fwd+bwd iters/s", "cores": int(O.lib().orc_threads()),
             "kind": "port",
-            "sample": f"1 full {s.image_width}x{s.image_height} view, {m.shape[0]} Gaussians, SH {D}: forward "
-                      f"{t1 - t0:.2f}s + backward {t2 - t1:.2f}s (rasterizer only; loss/Adam not included)",
-            "forward_mpix_per_s": round(s.image_width * s.image_height / (t1 - t0) / 1e6, 4)}
+            "sample": f"{views} x 1 full {s.image_width}x{s.image_height} view, {m.shape[0]} Gaussians, SH {D}: forward "
+                      f"{tf / views:.2f}s + backward {tb / views:.2f}s per view (rasterizer only; loss/Adam not included)",
+            "forward_mpix_per_s": round(views * s.image_width * s.image_height / tf / 1e6, 4)}
 
 
 if __name__ == "__main__":

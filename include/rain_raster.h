@@ -125,6 +125,20 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
                       void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
                       int num_pairs, float* out_color, float* out_depth, void* stream);
 
+/*
+ * Both forward stages in one call, for callers that keep a reusable binning buffer (the training
+ * loop): stage 1, the pair-count read-back, then stage 2 straight away if `binning_bytes` is at
+ * least rr_binning_bytes(*num_pairs, W, H) -- no return to the caller between the sync and the
+ * binning launches, so the device idles only for the read-back itself.  If the buffer is too
+ * small, *binning_needed receives the required size and RR_INCOMPLETE is returned with stage 1
+ * done: the caller grows its buffer and finishes with rr_forward_render.
+ */
+#define RR_INCOMPLETE 4
+int rr_forward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii, void* geom_buffer,
+               size_t geom_bytes, void* image_buffer, size_t image_bytes, void* binning_buffer, size_t binning_bytes,
+               int* num_rendered, int* num_pairs, size_t* binning_needed, float* out_color, float* out_depth,
+               void* stream);
+
 /* Optional fused optimizer step for RR_FLAG_RAW_PARAMS backwards (rr_grads.adam): Adam over the six
  * GaussianModel parameter groups (gaussian_model.py:144-153), applied in the same pass that forms
  * the gradients, so the gradients never travel through HBM.  Same arithmetic as rain_train.h's

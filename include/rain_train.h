@@ -37,6 +37,13 @@ typedef struct rt_adam_group {
 
 int rt_adam_step(const rt_adam_group* groups, int n_groups, double beta1, double beta2, double eps, void* stream);
 
+/* The same step on gradient SUMS: every gradient element is multiplied by grad_scale (fp32) before
+ * the update -- bitwise the reference's grad.mul_(1/N) followed by step().  Used by the view-sharded
+ * step, where each rank updates only its 1/N slice of the flat parameter buffer after a
+ * reduce-scatter of the gradient sums (rain_amd/train.py ShardedAdam). */
+int rt_adam_step_scaled(const rt_adam_group* groups, int n_groups, double beta1, double beta2, double eps,
+                        float grad_scale, void* stream);
+
 const char* rt_last_error(void);
 
 #ifdef __cplusplus

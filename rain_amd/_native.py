@@ -32,6 +32,7 @@ class RRFrame(ctypes.Structure):
 RR_FLAG_NO_TILE_CULLING = 1
 RR_FLAG_RAW_PARAMS = 2
 RR_FLAG_FULL_BINNING = 4
+RR_INCOMPLETE = 4  # rr_forward: stage 1 done, binning buffer too small
 
 
 class RRCamera(ctypes.Structure):
@@ -75,7 +76,7 @@ class RRDebugViews(ctypes.Structure):
 
 # every symbol include/rain_raster.h declares (tests check the .so exports all of them)
 RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
-                  "rr_forward_geometry", "rr_forward_render", "rr_backward", "rr_mark_visible", "rr_last_error",
+                  "rr_forward_geometry", "rr_forward_render", "rr_forward", "rr_backward", "rr_mark_visible", "rr_last_error",
                   "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
                   "rr_set_binning_config", "rr_profile_enable",
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name"]
@@ -110,6 +111,9 @@ def raster():
         L.rr_forward_geometry.argtypes = [fp, cp, gp, vp, vp, sz, vp, sz, ctypes.POINTER(ci), ctypes.POINTER(ci), vp]
         L.rr_forward_render.restype = ci
         L.rr_forward_render.argtypes = [fp, cp, gp, vp, vp, vp, vp, sz, ci, vp, vp, vp]
+        L.rr_forward.restype = ci
+        L.rr_forward.argtypes = [fp, cp, gp, vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(ci), ctypes.POINTER(ci),
+                                 ctypes.POINTER(sz), vp, vp, vp]
         L.rr_backward.restype = ci
         L.rr_backward.argtypes = [fp, cp, gp, vp, vp, vp, vp, ci, vp, vp, sz, ctypes.POINTER(RRGrads), vp]
         L.rr_mark_visible.restype = ci
@@ -158,7 +162,7 @@ def loss_lib():
 
 
 TRAIN_LIB = os.path.join(LIB_DIR, "librain_train.so")
-TRAIN_SYMBOLS = ["rt_adam_step", "rt_last_error"]
+TRAIN_SYMBOLS = ["rt_adam_step", "rt_adam_step_scaled", "rt_last_error"]
 RT_MAX_GROUPS = 8
 _train = None
 
@@ -176,6 +180,9 @@ def train_lib():
         L.rt_adam_step.restype = ctypes.c_int
         L.rt_adam_step.argtypes = [ctypes.POINTER(RTAdamGroup), ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                    ctypes.c_double, ctypes.c_void_p]
+        L.rt_adam_step_scaled.argtypes = [ctypes.POINTER(RTAdamGroup), ctypes.c_int, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_double, ctypes.c_float, ctypes.c_void_p]
+        L.rt_adam_step_scaled.restype = ctypes.c_int
         L.rt_last_error.restype = ctypes.c_char_p
         _train = L
     return _train

@@ -502,6 +502,22 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
                    : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
 }
 
+int rr_forward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii, void* geom_buffer,
+               size_t geom_bytes, void* image_buffer, size_t image_bytes, void* binning_buffer, size_t binning_bytes,
+               int* num_rendered, int* num_pairs, size_t* binning_needed, float* out_color, float* out_depth,
+               void* stream) {
+    if (!binning_needed) return fail(RR_ERR_ARG, "binning_needed is null");
+    *binning_needed = 0;
+    int rc = rr_forward_geometry(f, cam, g, radii, geom_buffer, geom_bytes, image_buffer, image_bytes, num_rendered,
+                                 num_pairs, stream);
+    if (rc != RR_OK || f->P == 0) return rc;
+    const size_t need = *num_pairs > 0 ? carve_bin(nullptr, *num_pairs, f->width, f->height).total : 0;
+    *binning_needed = need;
+    if (binning_bytes < need) return RR_INCOMPLETE;
+    return rr_forward_render(f, cam, g, radii, geom_buffer, image_buffer, binning_buffer, binning_bytes, *num_pairs,
+                             out_color, out_depth, stream);
+}
+
 int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                 const void* geom_buffer, const void* image_buffer, const void* binning_buffer, int num_rendered,
                 const float* dL_dpix, void* workspace, size_t workspace_bytes, const rr_grads* out, void* stream) {

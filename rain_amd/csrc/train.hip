@@ -43,6 +43,7 @@ struct AdamArgs {
     AdamGroupDev grp[RT_MAX_GROUPS];
     int n_groups;
     double beta1, beta2, eps;
+    float grad_scale;  // applied to every gradient element first (1/N for an N-rank gradient sum)
 };
 
 __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
@@ -56,7 +57,8 @@ __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
     if (e0 >= G.n) return;
     if (G.vec && e0 + kPerThread <= G.n) {
         float4 p = *reinterpret_cast<const float4*>(G.p + e0);
-        const float4 g = *reinterpret_cast<const float4*>(G.g + e0);
+        float4 g = *reinterpret_cast<const float4*>(G.g + e0);
+        g.x *= a.grad_scale; g.y *= a.grad_scale; g.z *= a.grad_scale; g.w *= a.grad_scale;
         float4 m = *reinterpret_cast<const float4*>(G.m + e0);
         float4 v = *reinterpret_cast<const float4*>(G.v + e0);
         adam_elem(p.x, g.x, m.x, v.x, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
         for (int k = 0; k < kPerThread && e0 + k < G.n; k++) {
             const int64_t e = e0 + k;
             float p = G.p[e], m = G.m[e], v = G.v[e];
-            adam_elem(p, G.g[e], m, v, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
+            adam_elem(p, G.g[e] * a.grad_scale, m, v, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
             G.p[e] = p;
             G.m[e] = m;
             G.v[e] = v;
@@ -87,6 +89,11 @@ extern "C" {
 const char* rt_last_error(void) { return g_err.c_str(); }
 
 int rt_adam_step(const rt_adam_group* groups, int n_groups, double beta1, double beta2, double eps, void* stream) {
+    return rt_adam_step_scaled(groups, n_groups, beta1, beta2, eps, 1.0f, stream);
+}
+
+int rt_adam_step_scaled(const rt_adam_group* groups, int n_groups, double beta1, double beta2, double eps,
+                        float grad_scale, void* stream) {
     if (n_groups < 0 || n_groups > RT_MAX_GROUPS) return fail("n_groups must be 0..RT_MAX_GROUPS");
     if (n_groups > 0 && !groups) return fail("groups is null");
     AdamArgs a{};
@@ -94,6 +101,7 @@ int rt_adam_step(const rt_adam_group* groups, int n_groups, double beta1, double
     a.beta1 = beta1;
     a.beta2 = beta2;
     a.eps = eps;
+    a.grad_scale = grad_scale;
     int64_t blocks = 0;
     for (int i = 0; i < n_groups; i++) {
         const rt_adam_group& s = groups[i];

@@ -42,9 +42,28 @@ class RawFrame:
     M: int
 
 
-def forward(model, camera, bg: torch.Tensor, low_pass: float, scale_modifier: float = 1.0):
+class BinningCache:
+    """A grow-only binning buffer reused frame after frame (the training loop renders one frame,
+    runs its backward, then renders the next, all on one stream, so frame s+1's binning never
+    overwrites a list frame s's backward still reads).  With it the forward is one native call
+    (rr_forward): the device waits only for the pair-count read-back, not for a return to Python."""
+
+    def __init__(self, headroom: float = 1.25):
+        self.buf = None
+        self.headroom = headroom
+
+    def get(self, nbytes: int, dev) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != dev:
+            self.buf = torch.empty((int(nbytes * self.headroom) + 4096,), dtype=torch.uint8, device=dev)
+        return self.buf
+
+
+def forward(model, camera, bg: torch.Tensor, low_pass: float, scale_modifier: float = 1.0,
+            cache: BinningCache | None = None):
     """Render `camera` from `model` (a GaussianModel) in raw-parameter mode.
-    Returns (color [3,H,W], radii [P] int32, depth [1,H,W], RawFrame)."""
+    Returns (color [3,H,W], radii [P] int32, depth [1,H,W], RawFrame).  With `cache` the binning
+    buffer is reused (see BinningCache) and must not be needed by an earlier frame's pending
+    backward."""
     xyz = model._xyz
     dev = xyz.device
     if dev.type != "cuda":
@@ -76,6 +95,20 @@ def forward(model, camera, bg: torch.Tensor, low_pass: float, scale_modifier: fl
     img = torch.empty((L.rr_image_bytes(W, H),), **u8)
     stream = N.stream_of(xyz)
     nr, npairs = ctypes.c_int(0), ctypes.c_int(0)
+    if P > 0 and cache is not None:
+        binning = cache.buf if cache.buf is not None and cache.buf.device == dev else torch.empty((0,), **u8)
+        need = ctypes.c_size_t(0)
+        rc = L.rr_forward(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii), _p(geom), geom.numel(),
+                          _p(img), img.numel(), _p(binning), binning.numel(), ctypes.byref(nr), ctypes.byref(npairs),
+                          ctypes.byref(need), _p(color), _p(depth), stream)
+        if rc == N.RR_INCOMPLETE:  # the pairs outgrew the buffer: grow it and run stage 2
+            binning = cache.get(need.value, dev)
+            rc = L.rr_forward_render(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii), _p(geom),
+                                     _p(img), _p(binning), binning.numel(), npairs.value, _p(color), _p(depth),
+                                     stream)
+        N.check(rc, "fused forward")
+        st = RawFrame(frame, cam, gs, (keep, params), radii, geom, img, binning, nr.value, P, M)
+        return color, radii, depth, st
     if P > 0:
         N.check(L.rr_forward_geometry(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii), _p(geom),
                                       geom.numel(), _p(img), img.numel(), ctypes.byref(nr), ctypes.byref(npairs),

@@ -115,6 +115,7 @@ class GaussianModel:
         self.spatial_lr_scale = 0
         self.divide_ratio = divide_ratio
         self.flat_grad = None
+        self._packed = None
         self.scaling_activation = torch.exp
         self.scaling_inverse_activation = torch.log
         self.opacity_activation = torch.sigmoid
@@ -266,6 +267,7 @@ class GaussianModel:
             lr_final=training_args.position_lr_final * self.spatial_lr_scale,
             lr_delay_mult=training_args.position_lr_delay_mult, max_steps=training_args.position_lr_max_steps)
         self.flat_grad = None
+        self._packed = None
 
     def update_learning_rate(self, iteration):
         for param_group in self.optimizer.param_groups:
@@ -280,25 +282,63 @@ class GaussianModel:
 
     FLAT_ALIGN = 64  # floats: every parameter's gradient view starts on a 256-B boundary
 
-    def bind_flat_grad(self, extra: int = 0, zero: bool = True):
-        """Make every parameter's .grad a view into one fp32 buffer (segments padded to 256 B, plus
-        `extra` trailing floats for densification statistics) and return the buffer.  The whole
-        buffer is zeroed if `zero`, otherwise only the trailing `extra` floats (for writers that
-        overwrite every gradient, e.g. the fused raw-parameter backward)."""
-        ps = self.params()
+    def flat_layout(self, pad_to: int = 1):
+        """Segment offsets of the six parameters in the flat buffers (each padded to FLAT_ALIGN
+        floats) and the total length, padded to a multiple of FLAT_ALIGN * pad_to so that it splits
+        into pad_to equal, 256-B aligned shards."""
         a = self.FLAT_ALIGN
-        n = sum((p.numel() + a - 1) // a * a for p in ps)
+        offs, off = [], 0
+        for p in self.params():
+            offs.append(off)
+            off += (p.numel() + a - 1) // a * a
+        unit = a * max(int(pad_to), 1)
+        return offs, (off + unit - 1) // unit * unit
+
+    def bind_flat_grad(self, extra: int = 0, zero: bool = True, pad_to: int = 1):
+        """Make every parameter's .grad a view into one fp32 buffer (flat_layout(pad_to), plus
+        `extra` trailing floats) and return the buffer.  The whole buffer is zeroed if `zero`,
+        otherwise only the trailing `extra` floats (for writers that overwrite every gradient, e.g.
+        the fused raw-parameter backward)."""
+        ps = self.params()
+        offs, n = self.flat_layout(pad_to)
         if self.flat_grad is None or self.flat_grad.numel() != n + extra:
             self.flat_grad = torch.zeros(n + extra, device=self.device)
         elif zero:
             self.flat_grad.zero_()
         elif extra:
             self.flat_grad[n:].zero_()
-        off = 0
-        for p in ps:
+        for p, off in zip(ps, offs):
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
-            off += (p.numel() + a - 1) // a * a
         return self.flat_grad
+
+    def pack_flat_state(self, pad_to: int = 1):
+        """Move the six parameters and their Adam moments into three flat fp32 buffers with the
+        flat-gradient layout (flat_layout(pad_to)); parameters keep their identity (only .data is
+        re-pointed), so param_groups and optimizer.state stay valid.  Used by the view-sharded step:
+        a rank updates the slice [r*n/N, (r+1)*n/N) of all three buffers, then all-gathers the
+        parameter buffer.  Re-packs only after densification / opacity reset replaced tensors.
+        Returns (params, exp_avg, exp_avg_sq, offsets, n)."""
+        ps = self.params()
+        key = (pad_to,) + tuple(id(p) for p in ps) + tuple(p.data_ptr() for p in ps)
+        if self._packed is not None and self._packed[0] == key:
+            return self._packed[1]
+        offs, n = self.flat_layout(pad_to)
+        fp, fm, fv = (torch.zeros(n, device=self.device) for _ in range(3))
+        for p, off in zip(ps, offs):
+            k = p.numel()
+            fp[off:off + k].copy_(p.data.reshape(-1))
+            st = self.optimizer.state[p]
+            if len(st) == 0:  # the state torch's Adam creates on its first step
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+            else:
+                fm[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                fv[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+            p.data = fp[off:off + k].view_as(p)
+            st["exp_avg"] = fm[off:off + k].view_as(p)
+            st["exp_avg_sq"] = fv[off:off + k].view_as(p)
+        out = (fp, fm, fv, offs, n)
+        self._packed = ((pad_to,) + tuple(id(p) for p in ps) + tuple(p.data_ptr() for p in ps), out)
+        return out
 
     # ---- densification (gaussian_model.py:200-421) ----
     def reset_opacity(self):

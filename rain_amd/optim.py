@@ -112,3 +112,52 @@ class FusedAdam(torch.optim.Optimizer):
                 if rc != 0:
                     raise RuntimeError(f"rt_adam_step: {L.rt_last_error().decode(errors='replace')}")
         return loss
+
+
+@torch.no_grad()
+def sharded_adam_step(optimizer, params, offsets, shard_grad: torch.Tensor, lo: int, grad_scale: float):
+    """One Adam step restricted to the slice [lo, lo + S) of the flat parameter / moment buffers
+    (GaussianModel.pack_flat_state), S = shard_grad.numel(), with shard_grad = that slice of the
+    gradient SUM over ranks (reduce-scatter output).  Every element is updated exactly as
+    optimizer.step() after grad.mul_(grad_scale) would update it; every group's step count advances
+    on every rank (also when its segment misses the slice), so all ranks keep identical counts.
+    FusedAdam: one launch (rt_adam_step_scaled); torch.optim.Adam (CPU replicas in the gloo tests):
+    torch's own single-tensor Adam on the slices."""
+    hi = lo + shard_grad.numel()
+    items = []
+    for p, off in zip(params, offsets):
+        group = next(g for g in optimizer.param_groups if any(q is p for q in g["params"]))
+        st = optimizer.state[p]
+        if len(st) == 0:
+            raise RuntimeError("sharded_adam_step: pack the optimizer state first (GaussianModel.pack_flat_state)")
+        st["step"] += 1.0
+        a, b = max(off, lo), min(off + p.numel(), hi)
+        if a < b:
+            items.append((group, p, st, a - off, a - lo, b - a))
+    if isinstance(optimizer, FusedAdam):
+        if not items:
+            return
+        groups = []
+        b1 = b2 = eps = None
+        for group, p, st, po, go, n in items:
+            gb1, gb2 = group["betas"]
+            b1, b2, eps = float(gb1), float(gb2), float(group["eps"])
+            k = float(st["step"].item())
+            groups.append(N.RTAdamGroup(p.data_ptr() + 4 * po, shard_grad.data_ptr() + 4 * go,
+                                        st["exp_avg"].data_ptr() + 4 * po, st["exp_avg_sq"].data_ptr() + 4 * po, n,
+                                        float(group["lr"]), 1.0 - math.pow(gb1, k), math.sqrt(1.0 - math.pow(gb2, k))))
+        arr = (N.RTAdamGroup * len(groups))(*groups)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(shard_grad.device).cuda_stream)
+        rc = N.train_lib().rt_adam_step_scaled(arr, len(groups), b1, b2, eps, float(grad_scale), stream)
+        if rc != 0:
+            raise RuntimeError(f"rt_adam_step_scaled: {N.train_lib().rt_last_error().decode(errors='replace')}")
+        return
+    from torch.optim.adam import adam as adam_functional
+
+    for group, p, st, po, go, n in items:
+        b1, b2 = group["betas"]
+        g = shard_grad[go:go + n] * grad_scale
+        step = (st["step"] - 1.0).clone()  # the functional form advances its own copy
+        adam_functional([p.data.view(-1)[po:po + n]], [g], [st["exp_avg"].view(-1)[po:po + n]],
+                        [st["exp_avg_sq"].view(-1)[po:po + n]], [], [step], foreach=False, amsgrad=False,
+                        beta1=b1, beta2=b2, lr=group["lr"], weight_decay=0.0, eps=group["eps"], maximize=False)

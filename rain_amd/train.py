@@ -8,11 +8,14 @@ data-parallel group:
 * every rank holds the full Gaussian set and Adam state (replicas);
 * at step s rank r renders view ``perm[s*N + r]`` of a permutation shared by all ranks (the
   reference's pop-random-without-replacement, train.py:87-89, done globally);
-* after backward ONE all-reduce (SUM) covers every parameter gradient (they are views into one
-  flat buffer) plus the per-view densification increments; gradients are then averaged, the
-  increments summed (N views add their norms exactly like N sequential iterations would); a second,
-  small all-reduce (MAX) merges max_radii2D;
-* Adam / densify then run identically on every rank (same RNG seed), so replicas stay equal.
+* after backward the gradients (views into one flat buffer) are reduce-scattered (SUM); each rank
+  applies Adam, scaled by 1/N, to its 1/N slice of the flat parameter / moment buffers and the
+  parameter buffer is all-gathered — the bytes of one all-reduce, 1/N of the optimizer work
+  (Trainer._finish);
+* densification statistics accumulate per rank and are merged (SUM, and MAX for max_radii2D) only
+  on densify iterations, where the Adam moments are all-gathered too; densify / prune / opacity
+  reset then run identically on every rank (same RNG seed), so replicas stay equal (N views add
+  their norms exactly like N sequential iterations would).
 
 With world_size 1 there is no collective and the step is the reference's iteration.
 """
@@ -27,6 +30,7 @@ import torch.distributed as dist
 
 from .gaussian_model import GaussianModel, OptimizationParams, low_pass_schedule
 from .loss import fused_l1_ssim_loss
+from .optim import sharded_adam_step
 from .renderer import PipelineParams, render
 
 
@@ -99,6 +103,9 @@ class Trainer:
         plain_pipe = not (self.pipe.convert_SHs_python or self.pipe.compute_cov3D_python)
         auto = dev.type == "cuda" and loss_fn is None and plain_pipe
         self.fused = auto if fused is None else bool(fused)
+        self._bin_cache = None
+        self.reuse_binning = True  # fused step: one native forward call over a reused binning buffer
+        self._shard = None
         if self.fused and not (dev.type == "cuda" and loss_fn is None and plain_pipe):
             raise ValueError("fused step needs a HIP device, the default loss and the default pipeline")
 
@@ -160,55 +167,93 @@ class Trainer:
         from . import fused
         from .loss import l1_ssim_backward, l1_ssim_forward
 
+        if self._bin_cache is None:
+            self._bin_cache = fused.BinningCache()
         g, opt = self.g, self.opt
         vidx, cam = self._low_pass_and_view(iteration)
-        P = g.get_xyz.shape[0]
         densify_phase = iteration < opt.densify_until_iter
+        densify_now, reset_now = self._events(iteration)
         # Single GPU, and no densify/prune or opacity reset this iteration (they replace parameter
         # tensors before the reference's optimizer.step()): the Adam step runs inside the backward
         # kernel and the gradients never exist in HBM.
-        densify_now, reset_now = self._events(iteration)
         fuse_adam = (self.world == 1 and iteration < opt.iterations and not densify_now and not reset_now
                      and hasattr(g.optimizer, "fused_step"))
-        extra = 2 * P if (self.world > 1 and densify_phase) else 0
-        flat = None if fuse_adam else g.bind_flat_grad(extra=extra, zero=False)  # backward overwrites all grads
+        if self.world > 1:
+            g.pack_flat_state(self.world)
+        flat = None if fuse_adam else g.bind_flat_grad(zero=False, pad_to=self.world)  # backward overwrites all
         with torch.no_grad():
-            image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass)
+            image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass,
+                                                     cache=self._bin_cache if self.reuse_binning else None)
             gt = self.gt[vidx]
             loss, _parts, lws = l1_ssim_forward(image, gt, opt.lambda_dssim)
             dimg = l1_ssim_backward(image, gt, opt.lambda_dssim, lws)
             grads = None if fuse_adam else dict(
                 xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad, opacity=g._opacity.grad,
                 scaling=g._scaling.grad, rotation=g._rotation.grad)
-            nparam = None if flat is None else flat.numel() - extra
-            stats = None
-            local_max = None
-            if densify_phase:
-                if self.world > 1:
-                    local_max = g.max_radii2D.clone()
-                    stats = (flat[nparam:nparam + P], flat[nparam + P:], local_max)
-                else:
-                    stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D)
+            # densification statistics accumulate per rank; ranks merge them only when densify
+            # consumes them (_finish)
+            stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D) if densify_phase else None
             fused.backward(st, dimg, grads, stats, adam=g.optimizer.fused_step(g) if fuse_adam else None)
-            if self.world > 1:
-                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-                flat[:nparam].mul_(1.0 / self.world)
-                if densify_phase:
-                    dist.all_reduce(local_max, op=dist.ReduceOp.MAX, group=self.group)
-                    g.max_radii2D = local_max
-                    g.xyz_gradient_accum += flat[nparam:nparam + P].unsqueeze(1)
-                    g.denom += flat[nparam + P:].unsqueeze(1)
-            densified = self._densify_and_adam(iteration, adam_done=fuse_adam)
+            densified = self._finish(iteration, flat, densify_now, reset_now, adam_done=fuse_adam)
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
                         view=vidx, low_pass=self.low_pass, densified=densified)
+
+    def _finish(self, iteration, flat, densify_now, reset_now, adam_done=False):
+        """Gradient exchange + optimizer step + densification (train.py:132-147) after the backward.
+
+        N = 1: densify / reset, then Adam (unless the backward kernel already applied it).
+        N > 1, ordinary iteration (no densify / reset): reduce-scatter the flat gradient SUM, each
+        rank runs Adam (scaled by 1/N) on its 1/N slice of the flat parameter / moment buffers, then
+        all-gathers the parameter buffer — the bytes of one all-reduce, 1/N of the optimizer work.
+        N > 1, densify / reset iteration (1 in 100): all-gather the Adam moments (each rank kept only
+        its slice current), merge the per-rank densification statistics (SUM / MAX) when densify
+        runs, all-reduce the gradients if an optimizer step follows (reset only: the reference
+        steps every group but the replaced opacity), then the N = 1 logic on identical replicas."""
+        g, opt = self.g, self.opt
+        if self.world == 1:
+            return self._densify_and_adam(iteration, adam_done=adam_done)
+        fp, fm, fv, _offs, n = g.pack_flat_state(self.world)
+        S = n // self.world
+        lo = self.rank * S
+        if not (densify_now or reset_now):
+            if iteration < opt.iterations:
+                if self._shard is None or self._shard.numel() != S or self._shard.device != flat.device:
+                    self._shard = torch.empty(S, dtype=flat.dtype, device=flat.device)
+                dist.reduce_scatter_tensor(self._shard, flat[:n], op=dist.ReduceOp.SUM, group=self.group)
+                sharded_adam_step(g.optimizer, g.params(), _offs, self._shard, lo, 1.0 / self.world)
+                dist.all_gather_into_tensor(fp, fp[lo:lo + S], group=self.group)
+                for p in g.params():
+                    p.grad = None
+            return False
+        dist.all_gather_into_tensor(fm, fm[lo:lo + S], group=self.group)
+        dist.all_gather_into_tensor(fv, fv[lo:lo + S], group=self.group)
+        if densify_now:
+            self.sync_densify_stats()
+        elif iteration < opt.iterations:
+            dist.all_reduce(flat[:n], op=dist.ReduceOp.SUM, group=self.group)
+            flat[:n].mul_(1.0 / self.world)
+        return self._densify_and_adam(iteration)
+
+    def sync_densify_stats(self):
+        """Merge the per-rank densification statistics in place: gradient-norm sums and view
+        counts add (SUM), max_radii2D takes the MAX — what N sequential views would have left.
+        Ranks then hold the merged values, so call it only where they are consumed and reset
+        (densify), or on copies."""
+        g = self.g
+        if self.world > 1:
+            dist.all_reduce(g.xyz_gradient_accum, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(g.denom, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(g.max_radii2D, op=dist.ReduceOp.MAX, group=self.group)
 
     def _step_autograd(self, iteration: int, sync_loss: bool = False) -> StepInfo:
         """The reference-API step: render() through GaussianRasterizer + autograd (train.py:109-147)."""
         g, opt = self.g, self.opt
         vidx, cam = self._low_pass_and_view(iteration)
-        P = g.get_xyz.shape[0]
         densify_phase = iteration < opt.densify_until_iter
-        flat = g.bind_flat_grad(extra=2 * P if (self.world > 1 and densify_phase) else 0)
+        densify_now, reset_now = self._events(iteration)
+        if self.world > 1:
+            g.pack_flat_state(self.world)
+        flat = g.bind_flat_grad(pad_to=self.world)
 
         pkg = render(cam, g, self.pipe, self.background, low_pass=self.low_pass)
         image, vsp, vis, radii = pkg["render"], pkg["viewspace_points"], pkg["visibility_filter"], pkg["radii"]
@@ -218,26 +263,9 @@ class Trainer:
         loss.backward()
 
         with torch.no_grad():
-            nparam = flat.numel() - (2 * P if (self.world > 1 and densify_phase) else 0)
-            if self.world > 1:
-                if densify_phase:
-                    acc = flat[nparam:nparam + P]
-                    den = flat[nparam + P:]
-                    acc[vis] = torch.norm(vsp.grad[vis, :2], dim=-1)
-                    den[vis] = 1.0
-                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-                flat[:nparam].mul_(1.0 / self.world)
-            if densify_phase:
-                if self.world > 1:
-                    local = g.max_radii2D.clone()
-                    local[vis] = torch.max(local[vis], radii[vis].float())
-                    dist.all_reduce(local, op=dist.ReduceOp.MAX, group=self.group)
-                    g.max_radii2D = local
-                    g.xyz_gradient_accum += flat[nparam:nparam + P].unsqueeze(1)
-                    g.denom += flat[nparam + P:].unsqueeze(1)
-                else:
-                    g.max_radii2D[vis] = torch.max(g.max_radii2D[vis], radii[vis].float())
-                    g.add_densification_stats(vsp, vis)
-            densified = self._densify_and_adam(iteration)
+            if densify_phase:  # train.py:132-134, per rank (merged by _finish when densify runs)
+                g.max_radii2D[vis] = torch.max(g.max_radii2D[vis], radii[vis].float())
+                g.add_densification_stats(vsp, vis)
+            densified = self._finish(iteration, flat, densify_now, reset_now)
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
                         view=vidx, low_pass=self.low_pass, densified=densified)

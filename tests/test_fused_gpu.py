@@ -178,3 +178,38 @@ def test_adam_fused_into_backward_matches_separate_step(gpu):
             scale = max(float(y.abs().max()), 1e-30)
             assert float((x - y).abs().max()) <= 1e-4 * scale, (m, float((x - y).abs().max()), scale)
             assert rel_l1(x, y) < 1e-4, (m, rel_l1(x, y))
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_adam_equals_full_step(world):
+    """rain_amd.optim.sharded_adam_step over every rank's slice (run here one after another in one
+    process) == FusedAdam.step on the mean gradient, bitwise: the view-sharded step's optimizer."""
+    from rain_amd.optim import sharded_adam_step
+
+    torch.manual_seed(0)
+    ga, gb = _model(3001, 3, 3, seed=4), _model(3001, 3, 3, seed=4)
+    for g in (ga, gb):
+        g.training_setup(OptimizationParams())
+    gsum = [torch.randn_like(p) * 1e-3 for p in ga.params()]
+    for it in range(3):  # a few steps so the moments and bias corrections are non-trivial
+        # reference: grads = sum / N, one full step
+        for p, s in zip(ga.params(), gsum):
+            p.grad = s * (1.0 / world)
+        ga.optimizer.step()
+        # sharded: packed flat state, flat gradient sum, every rank's slice
+        fp, fm, fv, offs, n = gb.pack_flat_state(world)
+        flat = torch.zeros(n, device="cuda")
+        for off, s in zip(offs, gsum):
+            flat[off:off + s.numel()] = s.reshape(-1)
+        S = n // world
+        for r in range(world):
+            if r > 0:  # only rank 0 advances the step counts once per step; the others reuse them
+                for p in gb.params():
+                    gb.optimizer.state[p]["step"] -= 1.0
+            sharded_adam_step(gb.optimizer, gb.params(), offs, flat[r * S:(r + 1) * S].clone(), r * S, 1.0 / world)
+        torch.cuda.synchronize()
+        for (na, pa), pb in zip(_params(ga).items(), gb.params()):
+            assert torch.equal(pa.detach(), pb.detach()), f"step {it}: {na} differs"
+            sa, sb = ga.optimizer.state[pa], gb.optimizer.state[pb]
+            assert torch.equal(sa["exp_avg"], sb["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sb["exp_avg_sq"])
+            assert float(sa["step"]) == float(sb["step"])

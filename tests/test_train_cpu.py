@@ -126,6 +126,7 @@ def _worker(rank, world, port, out_path):
                  loss_fn=_ref_loss)
     for it in (1, 2, 3):
         tr.step(it)
+    tr.sync_densify_stats()  # statistics stay per rank until densify consumes them
     torch.save({n: p.detach().clone() for n, p in zip(("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"),
                                                      g.params())} | {"accum": g.xyz_gradient_accum.clone(),
                                                                     "denom": g.denom.clone(),
@@ -187,3 +188,80 @@ def test_view_sharded_step_gloo_world2(oracle, tmp_path, monkeypatch):
     torch.testing.assert_close(r0["accum"], g.xyz_gradient_accum, rtol=1e-5, atol=1e-8)
     torch.testing.assert_close(r0["denom"], g.denom)
     torch.testing.assert_close(r0["maxr"], g.max_radii2D)
+
+
+def _event_opt():
+    opt = OptimizationParams()
+    opt.densify_from_iter, opt.densification_interval, opt.opacity_reset_interval = 1, 2, 3
+    return opt
+
+
+def _worker_events(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    dgr._C = oracle_c
+    cams, gts = _scene()
+    g = _model(800, 1, seed=3)
+    opt = _event_opt()
+    g.training_setup(opt)
+    tr = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(c2f=False, seed=5), scene_extent=4.4,
+                 loss_fn=_ref_loss)
+    flags = [tr.step(it).densified for it in range(1, 7)]
+    out = {n: p.detach().clone() for n, p in zip(("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"),
+                                                  g.params())}
+    for n, p in zip(("xyz", "opacity", "f_rest"), (g._xyz, g._opacity, g._features_rest)):
+        out["m_" + n] = g.optimizer.state[p]["exp_avg"].clone()
+        out["v_" + n] = g.optimizer.state[p]["exp_avg_sq"].clone()
+    out["densified"] = torch.tensor(flags)
+    torch.save(out, f"{out_path}.{rank}")
+    torch.distributed.destroy_process_group()
+
+
+def test_view_sharded_densify_and_reset_gloo_world2(oracle, tmp_path, monkeypatch):
+    """Iterations with densify/prune (2, 4, 6) and opacity reset (3, 6) in the sharded step: Adam
+    moments gathered, statistics merged, the replaced opacity skipped; replicas stay identical and
+    equal one process running the reference schedule on the mean of the same two views' gradients."""
+    out = str(tmp_path / "e")
+    mp.start_processes(_worker_events, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    r0, r1 = torch.load(out + ".0", weights_only=True), torch.load(out + ".1", weights_only=True)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), f"replicas diverged on {k}"
+    assert r0["densified"].tolist() == [False, True, False, True, False, True]
+
+    monkeypatch.setattr(dgr, "_C", oracle_c)
+    from rain_amd.train import ViewSampler
+
+    cams, gts = _scene()
+    g = _model(800, 1, seed=3)
+    opt = _event_opt()
+    g.training_setup(opt)
+    tr1 = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(c2f=False, seed=5), scene_extent=4.4,
+                  loss_fn=_ref_loss)
+    sampler = ViewSampler(len(cams), 2, seed=5)
+    bg = torch.zeros(3)
+    for it in range(1, 7):
+        g.update_learning_rate(it)
+        grads = [torch.zeros_like(p) for p in g.params()]
+        for v in sampler.next_group():
+            for p in g.params():
+                p.grad = None
+            pkg = render(cams[v], g, PipelineParams(), bg)
+            _ref_loss(pkg["render"], gts[v], opt.lambda_dssim).backward()
+            for acc, p in zip(grads, g.params()):
+                acc += p.grad
+            with torch.no_grad():
+                vis = pkg["visibility_filter"]
+                g.max_radii2D[vis] = torch.max(g.max_radii2D[vis], pkg["radii"][vis].float())
+                g.add_densification_stats(pkg["viewspace_points"], vis)
+        with torch.no_grad():
+            for acc, p in zip(grads, g.params()):
+                p.grad = acc / 2.0
+            tr1._densify_and_adam(it)
+            g.optimizer.zero_grad(set_to_none=True)
+    ref = dict(zip(("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"), g.params()))
+    for k, v in ref.items():
+        assert r0[k].shape == v.shape, k
+        torch.testing.assert_close(r0[k], v.detach(), rtol=1e-5, atol=1e-7)
+    for n, p in zip(("xyz", "opacity", "f_rest"), (g._xyz, g._opacity, g._features_rest)):
+        torch.testing.assert_close(r0["m_" + n], g.optimizer.state[p]["exp_avg"], rtol=1e-5, atol=1e-9)
+        torch.testing.assert_close(r0["v_" + n], g.optimizer.state[p]["exp_avg_sq"], rtol=1e-5, atol=1e-12)
