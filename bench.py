@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-profile", action="store_true", help="skip HIP-event stage timing in the timed region")
+    p.add_argument("--aux-normal", action="store_true",
+                   help="forward-only leg renders the aux depth + normal outputs (BASELINE configs[4] stress)")
     p.add_argument("--binning-split", type=int, default=0,
                    help="early-stop binning: phase A = 1/N of the pairs (1 = one phase; 0 = library default)")
     return p.parse_args()
@@ -74,8 +76,19 @@ def algorithmic_bytes(stage, st, P, W, H, K):
         "ranges": kw * Lb + 8 * T,
         "blend_fwd": 8 * T + 44 * Le + 24 * N,
         "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
-        "gauss_bwd": 4 * P * (27 + 3 * M) + 4 * P + 88 * V + 4 * P + V * (143 + 24 * K),
+        "gauss_bwd": gauss_bwd_bytes(P, V, K, M),
     }.get(stage)
+
+
+def gauss_bwd_bytes(P, V, K, M, fused_adam=True):
+    """Per-Gaussian backward.  In the training step (fused_adam) it reads the 64-B gradient
+    accumulator line and applies Adam in place: read + write of parameter, exp_avg and exp_avg_sq
+    (n_par = 11 + 3M floats each: xyz 3, f_dc 3, f_rest 3(M-1), opacity 1, scaling 3, rotation 4),
+    plus the densification statistics of visible Gaussians (read + write of 3 floats).  The
+    reference-API backward instead zero-fills and writes its gradient tensors."""
+    if fused_adam:
+        return 64 * P + 24 * (11 + 3 * M) * P + 24 * V
+    return 4 * P * (27 + 3 * M) + 4 * P + 88 * V + 4 * P + V * (143 + 24 * K)
 
 
 def main():
@@ -98,7 +111,7 @@ def main():
     from rain_amd.cameras import fibonacci_cameras
     from rain_amd.diff_gaussian_rasterization import _C
     from rain_amd.gaussian_model import GaussianModel, OptimizationParams
-    from rain_amd.renderer import PipelineParams, render
+    from rain_amd.renderer import PipelineParams, render, render_depth_normal
     from rain_amd.train import TrainConfig, Trainer
 
     P, W, H, D = args.points, args.width, args.height, args.sh_degree
@@ -187,7 +200,10 @@ def main():
             dist.barrier()
         tf0 = time.perf_counter()
         for i in range(args.fwd_frames):
-            render(cams[(rank * 7 + i) % len(cams)], gauss, pipe, bg)
+            if args.aux_normal:
+                render_depth_normal(cams[(rank * 7 + i) % len(cams)], gauss, bg)
+            else:
+                render(cams[(rank * 7 + i) % len(cams)], gauss, pipe, bg)
         torch.cuda.synchronize()
         tf = time.perf_counter() - tf0
     if world > 1:
@@ -222,11 +238,13 @@ def main():
         roofline = {"kernel": dom, "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "measured_copy_GBps": _copy_peak(dev),
                     "ms_per_launch": round(dom_ms, 5), "launches": int(dom_timed[1]),
-                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(dom),
+                    "frac": round(gbs / HBM_PEAK_GBS, 4),
+                    # PMC passes are committed for the headline workload only (tools/pmc_workload.py)
+                    "traffic": _pmc_traffic(dom) if (P, W, H) == (1_000_000, 1920, 1080) else None,
                     "algorithmic_bytes_per_launch": int(byts),
                     # the blend kernels are VALU-issue bound, not HBM bound: fraction of SIMD
                     # cycles issuing a VALU op, from the committed SQ counter pass
-                    "valu_busy": _pmc_field(dom, "valu_busy")}
+                    "valu_busy": _pmc_field(dom, "valu_busy") if (P, W, H) == (1_000_000, 1920, 1080) else None}
         for k in kernels:
             b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2)
             if b is not None:
@@ -256,6 +274,7 @@ def main():
                    "parallelism": f"dp{world} (view-sharded, RCCL all-reduce)" if world > 1 else "dp1",
                    "iterations": [start_iter + Wm + PW, end_iter]},
         "forward_mpix_per_s": round(fwd_mpix, 2),
+        "forward_outputs": "color+depth+normal" if args.aux_normal else "color+depth",
         "views_per_s": round(iters_per_s, 3),  # one view per rank per step: = value
         "bracket_iters_per_s": round(world * 1000.0 / bracket_ms, 3),
         "bracket_ms": round(bracket_ms, 4),

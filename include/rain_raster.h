@@ -75,6 +75,15 @@ typedef struct rr_frame {
  * every pair in one phase (the pair-order tests compare full lists with the reference's). */
 #define RR_FLAG_FULL_BINNING 4
 
+/* Auxiliary normal map (BASELINE configs[4]: depth + normal aux outputs; the reference has no
+ * normal output, so this has no reference counterpart -- parity is against oracle/raster_oracle.c).
+ * Each visible Gaussian's normal is the world axis of its smallest scale, rotated into view space,
+ * flipped to face the camera, unit length; the map is sum_i alpha_i T_i n_i per pixel (like depth:
+ * no background term, not normalised by 1 - T).  Forward only (no gradient, like depth).  Needs
+ * scales/rotations; set the flag on both forward stages and pass out_normal to
+ * rr_forward_render_aux. */
+#define RR_FLAG_AUX_NORMAL 8
+
 /* Camera / per-frame device arrays (reference args of the same names). */
 typedef struct rr_camera {
     const float* background; /* [3] */
@@ -124,6 +133,11 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
 int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                       void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
                       int num_pairs, float* out_color, float* out_depth, void* stream);
+
+/* rr_forward_render plus the aux normal map out_normal [3,H,W] (RR_FLAG_AUX_NORMAL; NULL otherwise). */
+int rr_forward_render_aux(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
+                          void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
+                          int num_pairs, float* out_color, float* out_depth, float* out_normal, void* stream);
 
 /*
  * Both forward stages in one call, for callers that keep a reusable binning buffer (the training

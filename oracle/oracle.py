@@ -47,7 +47,7 @@ def lib():
             ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f32p,
             _f32p, _f32p, _f32p, _f32p, ctypes.c_float, _f32p, _f32p,
             _f32p, _f32p, _f32p, ctypes.c_float, ctypes.c_float,
-            ctypes.c_int, ctypes.c_float, _f32p, _f32p, _i32p, _i32p, ctypes.c_int]
+            ctypes.c_int, ctypes.c_float, _f32p, _f32p, _i32p, _i32p, ctypes.c_int, _f32p]
         L.orc_backward.restype = ctypes.c_int
         L.orc_backward.argtypes = [
             ctypes.c_void_p, _f32p, _f32p, _i32p, _f32p, _f32p, ctypes.c_float, _f32p, _f32p,
@@ -163,8 +163,10 @@ class State:
 
 
 def forward(s: Settings, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-            cov3D_precomp=None, nthreads: int = 0):
-    """≙ _C.rasterize_gaussians: returns (num_rendered, color[3,H,W], radii[P], depth[1,H,W], State)."""
+            cov3D_precomp=None, nthreads: int = 0, normal: bool = False):
+    """≙ _C.rasterize_gaussians: returns (num_rendered, color[3,H,W], radii[P], depth[1,H,W], State),
+    plus the aux normal map [3,H,W] as a 6th element when `normal` (include/rain_raster.h
+    RR_FLAG_AUX_NORMAL; no reference counterpart)."""
     L = lib()
     means3D = _f32(means3D).reshape(-1, 3)
     P = means3D.shape[0]
@@ -178,12 +180,17 @@ def forward(s: Settings, means3D, opacities, shs=None, colors_precomp=None, scal
     color = np.zeros((3, H, W), np.float32)
     depth = np.zeros((1, H, W), np.float32)
     radii = np.zeros(P, np.int32)
+    if normal and (scales is None or rotations is None):
+        raise ValueError("the aux normal map needs scales/rotations")
+    nmap = np.zeros((3, H, W), np.float32) if normal else None
     nr = ctypes.c_int(0)
     h = L.orc_forward(P, int(s.sh_degree), M, _p(bg), W, H, _p(means3D), _p(shs), _p(colors_precomp), _p(opac),
                       _p(scales), float(s.scale_modifier), _p(rotations), _p(cov3D_precomp), _p(view), _p(proj),
                       _p(campos), float(s.tanfovx), float(s.tanfovy), int(bool(s.prefiltered)), float(s.low_pass),
-                      _p(color), _p(depth), _p(radii, _i32p), ctypes.byref(nr), int(nthreads))
+                      _p(color), _p(depth), _p(radii, _i32p), ctypes.byref(nr), int(nthreads), _p(nmap))
     st = State(h, P, W, H)
+    if normal:
+        return nr.value, color, radii, depth, st, nmap
     return nr.value, color, radii, depth, st
 
 

@@ -129,6 +129,25 @@ static void compute_cov3d(const float* scale, float mod, const float* rot, float
     cov3D[3] = Sg[1][1]; cov3D[4] = Sg[1][2]; cov3D[5] = Sg[2][2];
 }
 
+/* Auxiliary normal (BASELINE configs[4] "depth+normal aux outputs"; the reference renders no
+ * normals, so this follows the build's own definition in include/rain_raster.h RR_FLAG_AUX_NORMAL):
+ * the world axis of the smallest scale (column k of Rs), rotated into view space by R_w2c
+ * (transformVec4x3, auxiliary.h:68-76), flipped to face the camera, unit length. */
+static f3 gaussian_normal(const float* scale, const float* rot, const float* view, f3 p_view) {
+    float Rs[3][3];
+    quat_to_rot(rot, Rs);
+    int k = 0;
+    if (scale[1] < scale[k]) k = 1;
+    if (scale[2] < scale[k]) k = 2;
+    f3 n = mk3(Rs[0][k], Rs[1][k], Rs[2][k]);
+    f3 nv = mk3(view[0] * n.x + view[4] * n.y + view[8] * n.z, view[1] * n.x + view[5] * n.y + view[9] * n.z,
+                view[2] * n.x + view[6] * n.y + view[10] * n.z);
+    if (dot3(nv, p_view) > 0.f) nv = mk3(-nv.x, -nv.y, -nv.z);
+    float len = sqrtf(dot3(nv, nv));
+    if (!(len > 0.f)) return mk3(0.f, 0.f, 0.f);
+    return mk3(nv.x / len, nv.y / len, nv.z / len);
+}
+
 /* Shared between forward.cu:63-102 and backward.cu:156-189: the clamped view-space mean,
  * the 2x3 block A = J·W (glm's T is A laid out so that glm T[i][j] == A[i][j]), and the
  * un-dilated 2D covariance A V A^T. */
@@ -331,7 +350,7 @@ orc_state* orc_forward(int P, int D, int M, const float* bg, int W, int H, const
                        float scale_modifier, const float* rotations, const float* cov3D_precomp,
                        const float* view, const float* proj, const float* campos, float tanfovx, float tanfovy,
                        int prefiltered, float low_pass, float* out_color, float* out_depth, int* radii_out,
-                       int* num_rendered_out, int nthreads) {
+                       int* num_rendered_out, int nthreads, float* out_normal) {
     (void)prefiltered;
     set_threads(nthreads);
     orc_state* s = (orc_state*)calloc(1, sizeof(orc_state));
@@ -354,6 +373,7 @@ orc_state* orc_forward(int P, int D, int M, const float* bg, int W, int H, const
     s->ranges = (uint32_t*)calloc(2 * (size_t)T, sizeof(uint32_t));
     s->final_T = (float*)calloc((size_t)W * H, sizeof(float));
     s->n_contrib = (uint32_t*)calloc((size_t)W * H, sizeof(uint32_t));
+    float* normals = out_normal ? (float*)calloc(3 * Pz, sizeof(float)) : NULL;
 
     /* ---- preprocess: forward.cu:144-246 ---- */
 #pragma omp parallel for schedule(static)
@@ -405,6 +425,10 @@ orc_state* orc_forward(int P, int D, int M, const float* bg, int W, int H, const
         s->conic_opacity[4 * idx + 2] = conic[2];
         s->conic_opacity[4 * idx + 3] = opacities[idx];
         s->tiles_touched[idx] = (uint32_t)((rmaxy - rminy) * (rmaxx - rminx));
+        if (normals) {
+            f3 nv = gaussian_normal(scales + 3 * (size_t)idx, rotations + 4 * (size_t)idx, view, p_view);
+            normals[3 * idx] = nv.x; normals[3 * idx + 1] = nv.y; normals[3 * idx + 2] = nv.z;
+        }
     }
     if (radii_out) memcpy(radii_out, s->radii, sizeof(int) * (size_t)P);
 
@@ -473,7 +497,7 @@ orc_state* orc_forward(int P, int D, int M, const float* bg, int W, int H, const
                 float pfx = (float)px, pfy = (float)py;
                 float Tr = 1.0f;
                 uint32_t contributor = 0, last_contributor = 0;
-                float C[3] = {0, 0, 0}, Dp = 0;
+                float C[3] = {0, 0, 0}, Dp = 0, Nm[3] = {0, 0, 0};
                 for (uint32_t k = rs; k < re; k++) {
                     contributor++;
                     uint32_t g = s->point_list[k];
@@ -487,6 +511,8 @@ orc_state* orc_forward(int P, int D, int M, const float* bg, int W, int H, const
                     if (test_T < 0.0001f) break; /* done = true */
                     for (int ch = 0; ch < 3; ch++) C[ch] += features[3 * (size_t)g + ch] * alpha * Tr;
                     Dp += s->depths[g] * alpha * Tr;
+                    if (normals)
+                        for (int ch = 0; ch < 3; ch++) Nm[ch] += normals[3 * (size_t)g + ch] * alpha * Tr;
                     Tr = test_T;
                     last_contributor = contributor;
                 }
@@ -494,8 +520,11 @@ orc_state* orc_forward(int P, int D, int M, const float* bg, int W, int H, const
                 s->n_contrib[pix_id] = last_contributor;
                 for (int ch = 0; ch < 3; ch++) out_color[(size_t)ch * H * W + pix_id] = C[ch] + Tr * bg[ch];
                 out_depth[pix_id] = Dp;
+                if (out_normal)
+                    for (int ch = 0; ch < 3; ch++) out_normal[(size_t)ch * H * W + pix_id] = Nm[ch];
             }
     }
+    free(normals);
     return s;
 }
 

@@ -32,6 +32,7 @@ class RRFrame(ctypes.Structure):
 RR_FLAG_NO_TILE_CULLING = 1
 RR_FLAG_RAW_PARAMS = 2
 RR_FLAG_FULL_BINNING = 4
+RR_FLAG_AUX_NORMAL = 8
 RR_INCOMPLETE = 4  # rr_forward: stage 1 done, binning buffer too small
 
 
@@ -76,7 +77,7 @@ class RRDebugViews(ctypes.Structure):
 
 # every symbol include/rain_raster.h declares (tests check the .so exports all of them)
 RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
-                  "rr_forward_geometry", "rr_forward_render", "rr_forward", "rr_backward", "rr_mark_visible", "rr_last_error",
+                  "rr_forward_geometry", "rr_forward_render", "rr_forward_render_aux", "rr_forward", "rr_backward", "rr_mark_visible", "rr_last_error",
                   "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
                   "rr_set_binning_config", "rr_profile_enable",
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name"]
@@ -111,6 +112,8 @@ def raster():
         L.rr_forward_geometry.argtypes = [fp, cp, gp, vp, vp, sz, vp, sz, ctypes.POINTER(ci), ctypes.POINTER(ci), vp]
         L.rr_forward_render.restype = ci
         L.rr_forward_render.argtypes = [fp, cp, gp, vp, vp, vp, vp, sz, ci, vp, vp, vp]
+        L.rr_forward_render_aux.restype = ci
+        L.rr_forward_render_aux.argtypes = [fp, cp, gp, vp, vp, vp, vp, sz, ci, vp, vp, vp, vp]
         L.rr_forward.restype = ci
         L.rr_forward.argtypes = [fp, cp, gp, vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(ci), ctypes.POINTER(ci),
                                  ctypes.POINTER(sz), vp, vp, vp]

@@ -108,6 +108,7 @@ struct Geom {
     uint32_t* depth_keys_sorted;
     uint32_t* idx_sorted;
     uint2* offsets;       // inclusive prefix sum of tiles[] in depth order; .y of the last = num_rendered
+    float4* normals;      // RR_FLAG_AUX_NORMAL: view-space normal per visible Gaussian
     void* temp;
     size_t temp_bytes;
     size_t total;
@@ -122,6 +123,7 @@ Geom carve_geom(void* buf, int P) {
     g.depth_keys_sorted = c.take<uint32_t>(n);
     g.idx_sorted = c.take<uint32_t>(n);
     g.offsets = c.take<uint2>(n);
+    g.normals = c.take<float4>(n);
     g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
@@ -304,6 +306,8 @@ int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, boo
     if (g->shs && (f->D < 0 || f->D > 3 || f->M < (f->D + 1) * (f->D + 1)))
         return fail(RR_ERR_ARG, "sh_degree must be 0..3 and sh.size(1) >= (degree+1)^2");
     if (f->M > 16) return fail(RR_ERR_ARG, "sh.size(1) > 16 is not supported (SH degree <= 3, forward.cu:9-60)");
+    if ((f->flags & RR_FLAG_AUX_NORMAL) && !sr)
+        return fail(RR_ERR_ARG, "the aux normal output needs scales/rotations (not cov3D_precomp)");
     if (f->flags & RR_FLAG_RAW_PARAMS) {
         if (!g->shs || !sr || !g->opacities)
             return fail(RR_ERR_ARG, "raw-parameter mode needs SH, scales/rotations and opacities");
@@ -356,6 +360,7 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     a.cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
     a.raw = (f->flags & RR_FLAG_RAW_PARAMS) ? 1 : 0;
     a.shs_rest = g->shs_rest;
+    a.normals = (f->flags & RR_FLAG_AUX_NORMAL) ? gm.normals : nullptr;
 
     {
         StageTimer tm(RR_STAGE_PREPROCESS, st);
@@ -474,8 +479,18 @@ extern "C" {
 int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                       void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
                       int num_pairs, float* out_color, float* out_depth, void* stream) {
+    if (f && (f->flags & RR_FLAG_AUX_NORMAL)) return fail(RR_ERR_ARG, "RR_FLAG_AUX_NORMAL: use rr_forward_render_aux");
+    return rr_forward_render_aux(f, cam, g, radii, geom_buffer, image_buffer, binning_buffer, binning_bytes, num_pairs,
+                                 out_color, out_depth, nullptr, stream);
+}
+
+int rr_forward_render_aux(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
+                          void* geom_buffer, void* image_buffer, void* binning_buffer, size_t binning_bytes,
+                          int num_pairs, float* out_color, float* out_depth, float* out_normal, void* stream) {
     int rc = validate(f, cam, g, true);
     if (rc) return rc;
+    if (((f->flags & RR_FLAG_AUX_NORMAL) != 0) != (out_normal != nullptr))
+        return fail(RR_ERR_ARG, "out_normal must be given exactly when RR_FLAG_AUX_NORMAL is set");
     const int P = f->P, W = f->width, H = f->height, L = num_pairs;
     const int cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
     if (P == 0) return RR_OK;
@@ -498,6 +513,7 @@ int rr_forward_render(const rr_frame* f, const rr_camera* cam, const rr_gaussian
     b.point_list = bn.point_list; b.splats = gm.splats; b.bg = cam->background;
     b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
     b.out_color = out_color; b.out_depth = out_depth;
+    b.normals = out_normal ? gm.normals : nullptr; b.out_normal = out_normal;
     return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
                    : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
 }

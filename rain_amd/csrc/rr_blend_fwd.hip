@@ -24,7 +24,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-template <int NW>
+// AUX: also blend the per-Gaussian view-space normals into out_normal (RR_FLAG_AUX_NORMAL).
+template <int NW, bool AUX>
 __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
 #pragma clang fp contract(off)  // exactly blend_power's rounding: every fma below is explicit
     constexpr int PAIRS = 2 / NW;  // pixel pairs per lane
@@ -41,11 +42,13 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
     __shared__ float4 s_a[B];
     __shared__ float4 s_b[B];
     __shared__ float4 s_c[B];
+    __shared__ float4 s_n[AUX ? B : 1];
 
     // per pixel pair: T (transmittance), om (1 while the pixel is open, 0 once saturated: it zeroes
     // alpha, so a closed pixel neither blends nor changes T), colour / depth accumulators
     int py[PAIRS][2];
     f2 pfy[PAIRS], T[PAIRS], om[PAIRS], C0[PAIRS], C1[PAIRS], C2[PAIRS], Dp[PAIRS];
+    f2 N0[PAIRS], N1[PAIRS], N2[PAIRS];  // AUX only
     uint32_t last[PAIRS][2];
 #pragma unroll
     for (int p = 0; p < PAIRS; p++) {
@@ -56,6 +59,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
         T[p] = f2{1.f, 1.f};
         om[p] = f2{(px < a.W && row0 < a.H) ? 1.f : 0.f, (px < a.W && row0 + 4 < a.H) ? 1.f : 0.f};
         C0[p] = C1[p] = C2[p] = Dp[p] = f2{0.f, 0.f};
+        N0[p] = N1[p] = N2[p] = f2{0.f, 0.f};
         last[p][0] = last[p][1] = 0;
     }
     const size_t HW = (size_t)a.H * a.W;
@@ -82,6 +86,11 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
                         T[p].x = tv; C0[p].x = c0; C1[p].x = c1; C2[p].x = c2; Dp[p].x = dv;
                         om[p].x = (nc & kDoneBit) ? 0.f : 1.f;
                     }
+                    if (AUX) {
+                        const float n0 = a.out_normal[pix], n1 = a.out_normal[HW + pix], n2 = a.out_normal[2 * HW + pix];
+                        if (k) { N0[p].y = n0; N1[p].y = n1; N2[p].y = n2; }
+                        else { N0[p].x = n0; N1[p].x = n1; N2[p].x = n2; }
+                    }
                     last[p][k] = nc & ~kDoneBit;
                 }
             }
@@ -94,17 +103,26 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
         return c;
     };
 
-    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
-    if (t < n) load_splat(a.splats, a.point_list[range.x + t], na, nb, nc);
+    float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na, nn = na;
+    if (t < n) {
+        const uint32_t id = a.point_list[range.x + t];
+        load_splat(a.splats, id, na, nb, nc);
+        if (AUX) nn = a.normals[id];
+    }
     for (int base = 0; base < n; base += B) {
         if (__syncthreads_count(all_closed()) == B) break;
         if (base + t < n) {
             s_a[t] = na;
             s_b[t] = nb;
             s_c[t] = nc;
+            if (AUX) s_n[t] = nn;
         }
         __syncthreads();
-        if (base + B + t < n) load_splat(a.splats, a.point_list[range.x + base + B + t], na, nb, nc);
+        if (base + B + t < n) {
+            const uint32_t id = a.point_list[range.x + base + B + t];
+            load_splat(a.splats, id, na, nb, nc);
+            if (AUX) nn = a.normals[id];
+        }
         const int cnt = min(B, n - base);
         for (int j = 0; j < cnt; j++) {
             if ((j & 3) == 0 && __all(all_closed())) break;
@@ -138,6 +156,12 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
                 C1[p] = fma2(f2{Cc.y, Cc.y}, wgt, C1[p]);
                 C2[p] = fma2(f2{Cc.z, Cc.z}, wgt, C2[p]);
                 Dp[p] = fma2(f2{Bv.z, Bv.z}, wgt, Dp[p]);
+                if (AUX) {
+                    const float4 Nv = s_n[j];
+                    N0[p] = fma2(f2{Nv.x, Nv.x}, wgt, N0[p]);
+                    N1[p] = fma2(f2{Nv.y, Nv.y}, wgt, N1[p]);
+                    N2[p] = fma2(f2{Nv.z, Nv.z}, wgt, N2[p]);
+                }
                 T[p].x = sat0 ? T[p].x : testT.x;
                 T[p].y = sat1 ? T[p].y : testT.y;
                 om[p].x = sat0 ? 0.f : om[p].x;
@@ -167,6 +191,11 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
                         a.out_color[HW + pix] = k ? C1[p].y : C1[p].x;
                         a.out_color[2 * HW + pix] = k ? C2[p].y : C2[p].x;
                         a.out_depth[pix] = k ? Dp[p].y : Dp[p].x;
+                        if (AUX) {
+                            a.out_normal[pix] = k ? N0[p].y : N0[p].x;
+                            a.out_normal[HW + pix] = k ? N1[p].y : N1[p].x;
+                            a.out_normal[2 * HW + pix] = k ? N2[p].y : N2[p].x;
+                        }
                     }
                 }
             return;
@@ -187,6 +216,11 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
                 a.out_color[HW + pix] = (k ? C1[p].y : C1[p].x) + Tk * a.bg[1];
                 a.out_color[2 * HW + pix] = (k ? C2[p].y : C2[p].x) + Tk * a.bg[2];
                 a.out_depth[pix] = k ? Dp[p].y : Dp[p].x;
+                if (AUX) {
+                    a.out_normal[pix] = k ? N0[p].y : N0[p].x;
+                    a.out_normal[HW + pix] = k ? N1[p].y : N1[p].x;
+                    a.out_normal[2 * HW + pix] = k ? N2[p].y : N2[p].x;
+                }
             }
         }
 #pragma unroll
@@ -209,8 +243,14 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
-    if (blend_fwd_waves() == 1) k_blend_fwd<1><<<T, 64, 0, st>>>(a);
-    else k_blend_fwd<2><<<T, 128, 0, st>>>(a);
+    const bool aux = a.out_normal != nullptr;
+    if (blend_fwd_waves() == 1) {
+        if (aux) k_blend_fwd<1, true><<<T, 64, 0, st>>>(a);
+        else k_blend_fwd<1, false><<<T, 64, 0, st>>>(a);
+    } else {
+        if (aux) k_blend_fwd<2, true><<<T, 128, 0, st>>>(a);
+        else k_blend_fwd<2, false><<<T, 128, 0, st>>>(a);
+    }
 }
 
 }  // namespace rr

@@ -162,6 +162,25 @@ __device__ __forceinline__ void quat_rot(float4 q, float R[3][3]) {
     R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
 }
 
+// Auxiliary surface normal (BASELINE configs[4] depth + normal outputs; the reference renders no
+// normals): the world axis of the Gaussian's smallest scale (a column of R), rotated into view
+// space, flipped to face the camera, unit length.  Same op order as gaussian_normal in
+// oracle/raster_oracle.c.
+__device__ __forceinline__ float4 gaussian_normal(v3 sc, float4 q, const float* view, v3 p_view) {
+    float R[3][3];
+    quat_rot(q, R);
+    int k = 0;
+    if (sc.y < (k == 0 ? sc.x : sc.y)) k = 1;
+    if (sc.z < (k == 0 ? sc.x : sc.y)) k = 2;
+    const v3 n = k == 0 ? mk(R[0][0], R[1][0], R[2][0]) : k == 1 ? mk(R[0][1], R[1][1], R[2][1])
+                                                                 : mk(R[0][2], R[1][2], R[2][2]);
+    v3 nv = mk(view[0] * n.x + view[4] * n.y + view[8] * n.z, view[1] * n.x + view[5] * n.y + view[9] * n.z,
+               view[2] * n.x + view[6] * n.y + view[10] * n.z);
+    if (dot(nv, p_view) > 0.f) nv = mk(-nv.x, -nv.y, -nv.z);
+    const float len = sqrtf(dot(nv, nv));
+    return len > 0.f ? make_float4(nv.x / len, nv.y / len, nv.z / len, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // Sigma = M^T M with M[i][j] = s_i R[j][i]  (forward.cu:129-140).  Used by the forward
 // preprocess AND recomputed by the backward (no cov3D round trip through HBM).
 __device__ __forceinline__ void cov3d_from_scale_rot(v3 scale, float mod, float4 q, float cov[6]) {

@@ -36,13 +36,15 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     const float ppx = p_hom.x * p_w, ppy = p_hom.y * p_w;
 
     float cov[6];
+    float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+    v3 sc = mk(0.f, 0.f, 0.f);
     if (a.cov3D_precomp) {
         const float* c = a.cov3D_precomp + 6 * (size_t)idx;
 #pragma unroll
         for (int i = 0; i < 6; i++) cov[i] = c[i];
     } else {
-        float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
-        v3 sc = load3(a.scales + 3 * (size_t)idx);
+        q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        sc = load3(a.scales + 3 * (size_t)idx);
         if (a.raw) {
             q = act_rot(q);
             sc = act_scale(sc);
@@ -90,6 +92,7 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     s.b = make_float4(cz, opacity, p_view.z, 0.f);
     s.c = rgb;
     a.splats[idx] = s;
+    if (a.normals) a.normals[idx] = gaussian_normal(sc, q, a.view, p_view);
     a.radii[idx] = radius;
     uint32_t n = (uint32_t)area;
     if (a.cull) {

@@ -25,6 +25,7 @@ struct PreArgs {
     int cull;                    // exact tile culling on/off
     int raw;                     // RR_FLAG_RAW_PARAMS: apply the GaussianModel getters in-kernel
     const float* shs_rest;       // raw mode: f_rest [P,M-1,3] (shs = f_dc [P,1,3])
+    float4* normals;             // RR_FLAG_AUX_NORMAL: view-space unit normal per visible Gaussian, else null
 };
 
 // Early-stop binning (rr_api.hip): the tile lists are built in two phases.  Phase A bins the
@@ -50,6 +51,8 @@ struct BlendFwdArgs {
     const uint2* ranges_b;  // phase B lists
     uint8_t* open;          // [T] tile still open after phase A
     int phase;              // BlendPhase
+    const float4* normals;  // aux normal output (RR_FLAG_AUX_NORMAL): per-Gaussian normals and
+    float* out_normal;      // the blended normal map [3,H,W]; both null otherwise
 };
 
 struct BlendBwdArgs {

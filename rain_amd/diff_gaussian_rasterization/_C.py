@@ -67,6 +67,26 @@ def _frame(P, degree, M, W, H, tan_fovx, tan_fovy, scale_modifier, low_pass, pre
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
                         prefiltered, debug, low_pass):
+    out = _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                     viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                     prefiltered, debug, low_pass, False)
+    return out[:4] + out[5:]
+
+
+def rasterize_gaussians_aux(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                            viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                            prefiltered, debug, low_pass):
+    """rasterize_gaussians plus the aux normal map (include/rain_raster.h RR_FLAG_AUX_NORMAL; no
+    reference counterpart): returns (num_rendered, color, radii, depth, normal [3,H,W], geomBuffer,
+    binningBuffer, imgBuffer).  The buffers are valid for rasterize_gaussians_backward."""
+    return _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                      viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                      prefiltered, debug, low_pass, True)
+
+
+def _rasterize(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+               viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+               prefiltered, debug, low_pass, normal):
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     P = means3D.size(0)
@@ -76,8 +96,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     u8 = dict(dtype=torch.uint8, device=device)
     if P == 0:
         return (0, torch.zeros((NUM_CHANNELS, H, W), **fopts), torch.zeros((0,), dtype=torch.int32, device=device),
-                torch.zeros((1, H, W), **fopts), torch.empty((0,), **u8), torch.empty((0,), **u8),
-                torch.empty((0,), **u8))
+                torch.zeros((1, H, W), **fopts), torch.zeros((3, H, W), **fopts) if normal else None,
+                torch.empty((0,), **u8), torch.empty((0,), **u8), torch.empty((0,), **u8))
     L = N.raster()
     M = sh.size(1) if sh.size(0) != 0 else 0
     keep = dict(
@@ -88,11 +108,14 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         proj=_dev_f32(projmatrix, device, "projmatrix"), sh=_dev_f32(sh, device, "sh"),
         campos=_dev_f32(campos, device, "campos"))
     frame = _frame(P, degree, M, W, H, tan_fovx, tan_fovy, scale_modifier, low_pass, prefiltered, debug)
+    if normal:
+        frame.flags |= N.RR_FLAG_AUX_NORMAL
     cam = N.RRCamera(_ptr(keep["bg"]), _ptr(keep["view"]), _ptr(keep["proj"]), _ptr(keep["campos"]))
     gs = N.RRGaussians(_ptr(keep["means3D"]), _ptr(keep["sh"]), _ptr(keep["colors"]), _ptr(keep["opacity"]),
                        _ptr(keep["scales"]), _ptr(keep["rotations"]), _ptr(keep["cov3D"]))
     out_color = torch.empty((NUM_CHANNELS, H, W), **fopts)
     out_depth = torch.empty((1, H, W), **fopts)
+    out_normal = torch.empty((3, H, W), **fopts) if normal else None
     radii = torch.empty((P,), dtype=torch.int32, device=device)
     geom = torch.empty((L.rr_geometry_bytes(P),), **u8)
     img = torch.empty((L.rr_image_bytes(W, H),), **u8)
@@ -105,12 +128,12 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             "rasterize_gaussians")
     num_rendered, num_pairs = nr.value, npairs.value
     binning = torch.empty((L.rr_binning_bytes(num_pairs, W, H) if num_pairs > 0 else 0,), **u8)
-    N.check(L.rr_forward_render(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _ptr(radii), _ptr(geom),
-                                _ptr(img), _ptr(binning), binning.numel(), num_pairs, _ptr(out_color),
-                                _ptr(out_depth), stream),
+    N.check(L.rr_forward_render_aux(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _ptr(radii),
+                                    _ptr(geom), _ptr(img), _ptr(binning), binning.numel(), num_pairs,
+                                    _ptr(out_color), _ptr(out_depth), _ptr(out_normal), stream),
             "rasterize_gaussians")
     # num_rendered is the reference's value (sum of bounding-square tile counts)
-    return num_rendered, out_color, radii, out_depth, geom, binning, img
+    return num_rendered, out_color, radii, out_depth, out_normal, geom, binning, img
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,

@@ -134,6 +134,25 @@ class GaussianRasterizer(nn.Module):
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations,
                                    cov3D_precomp, raster_settings)
 
+    @torch.no_grad()
+    def render_depth_normal(self, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None):
+        """Forward only, with the auxiliary outputs of BASELINE configs[4]: returns (color [3,H,W],
+        radii [P], depth [1,H,W], normal [3,H,W]).  The normal map (no reference counterpart) blends
+        each Gaussian's view-space smallest-scale axis, facing the camera, like depth: sum of
+        alpha*T*n, no background (include/rain_raster.h RR_FLAG_AUX_NORMAL).  Needs scales/rotations."""
+        s = self.raster_settings
+        if (shs is None) == (colors_precomp is None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if scales is None or rotations is None:
+            raise Exception('render_depth_normal needs the scale/rotation pair (normals come from the scale axes)')
+        e = torch.Tensor([])
+        out = _C.rasterize_gaussians_aux(s.bg, means3D, e if colors_precomp is None else colors_precomp, opacities,
+                                         scales, rotations, s.scale_modifier, e, s.viewmatrix, s.projmatrix,
+                                         s.tanfovx, s.tanfovy, s.image_height, s.image_width,
+                                         e if shs is None else shs, s.sh_degree, s.campos, s.prefiltered, s.debug,
+                                         s.low_pass)
+        return out[1], out[2], out[3], out[4]
+
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians",
            "_C"]

@@ -70,3 +70,18 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=
                                               rotations=rotations, cov3D_precomp=cov3D_precomp)
     return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
             "radii": radii, "depth": depth}
+
+
+@torch.no_grad()
+def render_depth_normal(viewpoint_camera, pc, bg_color: torch.Tensor, scaling_modifier=1.0, low_pass=0.3):
+    """Evaluation-time render with the auxiliary outputs of BASELINE configs[4] (depth + normal):
+    {render [3,H,W], depth [1,H,W], normal [3,H,W], radii, visibility_filter}.  No autograd graph."""
+    settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5), bg=bg_color,
+        scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform,
+        projmatrix=viewpoint_camera.full_proj_transform, sh_degree=pc.active_sh_degree,
+        campos=viewpoint_camera.camera_center, prefiltered=False, debug=False, low_pass=low_pass)
+    color, radii, depth, normal = GaussianRasterizer(settings).render_depth_normal(
+        pc.get_xyz, pc.get_opacity, shs=pc.get_features, scales=pc.get_scaling, rotations=pc.get_rotation)
+    return {"render": color, "depth": depth, "normal": normal, "radii": radii, "visibility_filter": radii > 0}
