@@ -27,6 +27,23 @@ def _np(t):
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
                         prefiltered, debug, low_pass):
+    out = _forward(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                   viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                   prefiltered, debug, low_pass, False)
+    return out[:4] + out[5:]
+
+
+def rasterize_gaussians_aux(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                            viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                            prefiltered, debug, low_pass):
+    return _forward(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                    viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                    prefiltered, debug, low_pass, True)
+
+
+def _forward(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+             viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+             prefiltered, debug, low_pass, normal):
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     s = O.Settings(image_height=int(image_height), image_width=int(image_width), tanfovx=float(tan_fovx),
@@ -37,15 +54,17 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     H, W = int(image_height), int(image_width)
     if P == 0:
         z = torch.zeros((0,), dtype=torch.uint8)
-        return 0, torch.zeros((3, H, W)), torch.zeros((0,), dtype=torch.int32), torch.zeros((1, H, W)), z, z, z
-    nr, color, radii, depth, st = O.forward(s, _np(means3D), _np(opacity), shs=_np(sh), colors_precomp=_np(colors),
-                                            scales=_np(scales), rotations=_np(rotations),
-                                            cov3D_precomp=_np(cov3D_precomp), nthreads=1)
+        return (0, torch.zeros((3, H, W)), torch.zeros((0,), dtype=torch.int32), torch.zeros((1, H, W)),
+                torch.zeros((3, H, W)) if normal else None, z, z, z)
+    res = O.forward(s, _np(means3D), _np(opacity), shs=_np(sh), colors_precomp=_np(colors), scales=_np(scales),
+                    rotations=_np(rotations), cov3D_precomp=_np(cov3D_precomp), nthreads=1, normal=normal)
+    nr, color, radii, depth, st = res[:5]
+    nmap = torch.from_numpy(res[5]) if normal else None
     key = next(_ids)
     _states[key] = (st, s)
     geom = torch.tensor([key], dtype=torch.int64)
     empty = torch.zeros((0,), dtype=torch.uint8)
-    return nr, torch.from_numpy(color), torch.from_numpy(radii), torch.from_numpy(depth), geom, empty, empty
+    return nr, torch.from_numpy(color), torch.from_numpy(radii), torch.from_numpy(depth), nmap, geom, empty, empty
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
