@@ -44,6 +44,62 @@ int rt_adam_step(const rt_adam_group* groups, int n_groups, double beta1, double
 int rt_adam_step_scaled(const rt_adam_group* groups, int n_groups, double beta1, double beta2, double eps,
                         float grad_scale, void* stream);
 
+/*
+ * Densification as stream compaction (replaces GaussianModel.densify_and_prune's boolean-mask
+ * cat / index chain, gaussian_model.py:339-415 via train.py:136-140).
+ *
+ * With g = xyz_gradient_accum / denom (NaN -> 0) and s = exp(scaling):
+ *   clone  = |g| >= grad_threshold && max(s) <= clone_split_scale          (densify_and_clone)
+ *   split  =  g  >= grad_threshold && max(s) >  clone_split_scale          (densify_and_split)
+ *   prune(x) = sigmoid(opacity_x) < min_opacity || (prune_big_world && max(s_x) > big_world_scale)
+ * (max_radii2D never prunes: densification_postfix has zeroed it before the prune, as in the
+ * reference).  The result is, in the reference's order: the originals that are neither split nor
+ * pruned, then the clones not pruned, then for n = 0..n_split-1 the n-th child of every split
+ * Gaussian not pruned.  A child of Gaussian i has xyz = R(q_i) (z * s_i) + xyz_i, with z the i-th
+ * row (in split order) of block n of standard normals drawn by the caller exactly as torch.normal
+ * draws them, scaling = log(s_i * (1 / split_scale_div)) (torch divides by a scalar through its
+ * reciprocal), and the parameters of i otherwise; clones and children get zero Adam moments.
+ *
+ * rt_densify_plan: flags + offsets into the workspace and the four counts (host, after a sync):
+ *   counts[0] = originals kept, [1] = clones kept, [2] = split Gaussians whose children are kept,
+ *   [3] = split Gaussians (rows of standard normals per child block).
+ * rt_densify_apply: writes every group's parameter / exp_avg / exp_avg_sq rows for the new set of
+ *   counts[0] + counts[1] + n_split * counts[2] Gaussians.
+ */
+typedef struct rt_densify_params {
+    int P;                    /* Gaussians before densification */
+    int n_split;              /* children per split Gaussian (N = 2) */
+    float grad_threshold;     /* max_grad */
+    float clone_split_scale;  /* percent_dense * scene_extent */
+    float min_opacity;
+    float big_world_scale;    /* 0.1 * extent */
+    int prune_big_world;      /* max_screen_size given */
+    float split_scale_div;    /* divide_ratio * N */
+} rt_densify_params;
+
+typedef struct rt_densify_group {
+    const float* param;       /* [P, width] */
+    const float* exp_avg;     /* [P, width] or NULL (no optimizer state yet) */
+    const float* exp_avg_sq;
+    float* out_param;         /* [P_new, width] */
+    float* out_exp_avg;       /* NULL when exp_avg is NULL */
+    float* out_exp_avg_sq;
+    int width;                /* floats per Gaussian: xyz 3, f_dc 3, f_rest 3(M-1), opacity 1, scaling 3, rotation 4 */
+    int kind;                 /* RT_GROUP_* */
+} rt_densify_group;
+
+#define RT_GROUP_OTHER 0
+#define RT_GROUP_XYZ 1
+#define RT_GROUP_SCALING 2
+
+size_t rt_densify_workspace_bytes(int P);
+int rt_densify_plan(const rt_densify_params* p, const float* xyz_gradient_accum, const float* denom,
+                    const float* scaling, const float* opacity, void* workspace, size_t workspace_bytes,
+                    int64_t counts[4], void* stream);
+int rt_densify_apply(const rt_densify_params* p, const float* scaling, const float* rotation, const float* normals,
+                     const void* workspace, const rt_densify_group* groups, int n_groups, const int64_t counts[4],
+                     void* stream);
+
 const char* rt_last_error(void);
 
 #ifdef __cplusplus

@@ -28,7 +28,7 @@ LIBS = {
                           "rr_api.hip"],
     "librain_loss.so": ["loss.hip"],
     "librain_knn.so": ["knn.hip"],
-    "librain_train.so": ["train.hip"],
+    "librain_train.so": ["train.hip", "densify.hip"],
 }
 
 

@@ -165,9 +165,25 @@ def loss_lib():
 
 
 TRAIN_LIB = os.path.join(LIB_DIR, "librain_train.so")
-TRAIN_SYMBOLS = ["rt_adam_step", "rt_adam_step_scaled", "rt_last_error"]
+TRAIN_SYMBOLS = ["rt_adam_step", "rt_adam_step_scaled", "rt_densify_workspace_bytes", "rt_densify_plan",
+                 "rt_densify_apply", "rt_last_error"]
 RT_MAX_GROUPS = 8
 _train = None
+
+
+class RTDensifyParams(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_int), ("n_split", ctypes.c_int), ("grad_threshold", ctypes.c_float),
+                ("clone_split_scale", ctypes.c_float), ("min_opacity", ctypes.c_float),
+                ("big_world_scale", ctypes.c_float), ("prune_big_world", ctypes.c_int),
+                ("split_scale_div", ctypes.c_float)]
+
+
+class RTDensifyGroup(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("param", "exp_avg", "exp_avg_sq", "out_param", "out_exp_avg",
+                                                "out_exp_avg_sq")] + [("width", ctypes.c_int), ("kind", ctypes.c_int)]
+
+
+RT_GROUP_OTHER, RT_GROUP_XYZ, RT_GROUP_SCALING = 0, 1, 2
 
 
 class RTAdamGroup(ctypes.Structure):
@@ -186,6 +202,16 @@ def train_lib():
         L.rt_adam_step_scaled.argtypes = [ctypes.POINTER(RTAdamGroup), ctypes.c_int, ctypes.c_double,
                                           ctypes.c_double, ctypes.c_double, ctypes.c_float, ctypes.c_void_p]
         L.rt_adam_step_scaled.restype = ctypes.c_int
+        vp = ctypes.c_void_p
+        L.rt_densify_workspace_bytes.restype = ctypes.c_size_t
+        L.rt_densify_workspace_bytes.argtypes = [ctypes.c_int]
+        L.rt_densify_plan.restype = ctypes.c_int
+        L.rt_densify_plan.argtypes = [ctypes.POINTER(RTDensifyParams), vp, vp, vp, vp, vp, ctypes.c_size_t,
+                                      ctypes.POINTER(ctypes.c_int64), vp]
+        L.rt_densify_apply.restype = ctypes.c_int
+        L.rt_densify_apply.argtypes = [ctypes.POINTER(RTDensifyParams), vp, vp, vp, vp,
+                                       ctypes.POINTER(RTDensifyGroup), ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                       vp]
         L.rt_last_error.restype = ctypes.c_char_p
         _train = L
     return _train

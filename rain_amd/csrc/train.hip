@@ -84,6 +84,10 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 
 }  // namespace
 
+namespace rt_internal {
+void set_error(const std::string& m) { g_err = m; }  // densify.hip reports through rt_last_error too
+}  // namespace rt_internal
+
 extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }

@@ -471,8 +471,14 @@ class GaussianModel:
                                    self._features_rest[selected_pts_mask], self._opacity[selected_pts_mask],
                                    self._scaling[selected_pts_mask], self._rotation[selected_pts_mask])
 
+    # HIP devices densify with the stream-compaction kernels (include/rain_train.h rt_densify_*);
+    # False selects the torch restatement below (tests compare the two)
+    native_densify = True
+
     def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, N=2, abe_split=False,
                           generator=None):
+        if self.native_densify and self.device.type == "cuda" and not abe_split and self._xyz.shape[0] > 0:
+            return self._densify_and_prune_native(max_grad, min_opacity, extent, max_screen_size, N, generator)
         grads = self.xyz_gradient_accum / self.denom
         grads[grads.isnan()] = 0.0
         self.densify_and_clone(grads, max_grad, extent)
@@ -483,6 +489,76 @@ class GaussianModel:
             big_points_ws = self.get_scaling.max(dim=1).values > 0.1 * extent
             prune_mask = torch.logical_or(torch.logical_or(prune_mask, big_points_vs), big_points_ws)
         self.prune_points(prune_mask)
+
+    def _densify_and_prune_native(self, max_grad, min_opacity, extent, max_screen_size, N, generator):
+        """densify_and_clone + densify_and_split + prune (gaussian_model.py:366-415) as one stream
+        compaction on the device: the same decisions, the survivors in the same order, the same values
+        (the split children's xyz up to the rounding of the reference's bmm) and the same
+        optimizer-state surgery (new Parameters, zero moments for the new Gaussians)."""
+        import ctypes
+
+        from . import _native as NV
+
+        L = NV.train_lib()
+        dev = self.device
+        P = self._xyz.shape[0]
+
+        def ptr(t):
+            return None if t is None or t.numel() == 0 else ctypes.c_void_p(t.data_ptr())
+
+        def check(rc, what):
+            if rc != 0:
+                raise RuntimeError(f"{what}: {L.rt_last_error().decode(errors='replace')}")
+
+        prm = NV.RTDensifyParams(P, int(N), float(max_grad), float(self.percent_dense * extent), float(min_opacity),
+                                 float(0.1 * extent), int(bool(max_screen_size)), float(self.divide_ratio * N))
+        ws = torch.empty((L.rt_densify_workspace_bytes(P),), dtype=torch.uint8, device=dev)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        acc, den = self.xyz_gradient_accum.contiguous(), self.denom.contiguous()
+        sc, op, rot = (t.detach().contiguous() for t in (self._scaling, self._opacity, self._rotation))
+        counts = (ctypes.c_int64 * 4)()
+        check(L.rt_densify_plan(ctypes.byref(prm), ptr(acc), ptr(den), ptr(sc), ptr(op), ptr(ws), ws.numel(), counts,
+                                stream), "rt_densify_plan")
+        A, B, C, S = (int(c) for c in counts)
+        # torch.normal(mean=0, std) draws normal_(0, 1) into its output first: same draws, same generator
+        z = torch.empty((N * S, 3), device=dev).normal_(0.0, 1.0, generator=generator) if S else None
+        Pn = A + B + N * C
+        kinds = {"xyz": NV.RT_GROUP_XYZ, "scaling": NV.RT_GROUP_SCALING}
+        plans, structs = [], []
+        for group in self.optimizer.param_groups:
+            p = group["params"][0]
+            st = self.optimizer.state.get(p, None)
+            has = st is not None and "exp_avg" in st
+            width = math.prod(p.shape[1:])
+            out = torch.empty((Pn,) + tuple(p.shape[1:]), device=dev)
+            om = torch.empty_like(out) if has else None
+            ov = torch.empty_like(out) if has else None
+            src = p.detach().contiguous()
+            m = st["exp_avg"].contiguous() if has else None
+            v = st["exp_avg_sq"].contiguous() if has else None
+            if width > 0:
+                structs.append(NV.RTDensifyGroup(ptr(src), ptr(m), ptr(v), ptr(out), ptr(om), ptr(ov), width,
+                                                 kinds.get(group["name"], NV.RT_GROUP_OTHER)))
+            plans.append((group, p, st, out, om, ov, (src, m, v)))
+        arr = (NV.RTDensifyGroup * max(len(structs), 1))(*structs)
+        check(L.rt_densify_apply(ctypes.byref(prm), ptr(sc), ptr(rot), ptr(z), ptr(ws), arr, len(structs), counts,
+                                 stream), "rt_densify_apply")
+        new = {}
+        for group, p, st, out, om, ov, _keep in plans:
+            param = nn.Parameter(out.requires_grad_(True))
+            if st is not None:
+                del self.optimizer.state[p]
+                if om is not None:
+                    st["exp_avg"], st["exp_avg_sq"] = om, ov
+                self.optimizer.state[param] = st
+            group["params"][0] = param
+            new[group["name"]] = param
+        self._xyz, self._features_dc, self._features_rest = new["xyz"], new["f_dc"], new["f_rest"]
+        self._opacity, self._scaling, self._rotation = new["opacity"], new["scaling"], new["rotation"]
+        self.xyz_gradient_accum = torch.zeros((Pn, 1), device=dev)
+        self.denom = torch.zeros((Pn, 1), device=dev)
+        self.max_radii2D = torch.zeros((Pn,), device=dev)
+        self.flat_grad = None
 
     def add_densification_stats(self, viewspace_point_tensor, update_filter):
         """gaussian_model.py:419-421 (consumes the NDC-space dL/dmeans2D the rasterizer returns)."""

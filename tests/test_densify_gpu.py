@@ -1,0 +1,90 @@
+"""Native densification (include/rain_train.h rt_densify_*) against the torch
+restatement of densify_and_prune (GaussianModel.native_densify = False: gaussian_model.py:339-415 op
+for op): the same survivors in the same order, the same values (split children's xyz within the
+rounding of the reference's bmm) and the same optimizer-state surgery."""
+import math
+
+import pytest
+import torch
+
+from rain_amd import synthetic
+from rain_amd.gaussian_model import PARAM_NAMES, GaussianModel, OptimizationParams
+
+pytestmark = pytest.mark.gpu
+EXTENT = 4.4
+
+
+def _model(P, seed):
+    g = GaussianModel(3, divide_ratio=0.8, device="cuda")
+    p = synthetic.random_gaussians(P, sh_degree=3, seed=seed, bench=True, device="cuda")
+    gen = torch.Generator().manual_seed(seed + 1)
+    # scales across the clone/split boundary (percent_dense * extent = 0.044), 1% past the
+    # world-size prune (0.1 * extent); 5% of the opacities below min_opacity
+    s = torch.empty((P, 3)).uniform_(math.log(0.005), math.log(0.2), generator=gen)
+    s[: P // 100] = math.log(0.6)
+    p["scaling"] = s.to("cuda")
+    o = p["opacity"].clone()
+    o[P // 100: P // 100 + P // 20] = -6.0
+    p["opacity"] = o
+    g.set_params(p)
+    g.active_sh_degree = 3
+    g.spatial_lr_scale = EXTENT
+    g.training_setup(OptimizationParams())
+    return g
+
+
+def _prime(g, seed):
+    """Non-trivial Adam moments and densification statistics (identical for identical seeds)."""
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    for p in g.params():
+        p.grad = torch.randn(p.shape, device="cuda", generator=gen) * 1e-3
+    g.optimizer.step()
+    g.optimizer.zero_grad(set_to_none=True)
+    P = g.get_xyz.shape[0]
+    g.denom = torch.randint(0, 4, (P, 1), device="cuda", generator=gen).float()
+    g.xyz_gradient_accum = torch.rand((P, 1), device="cuda", generator=gen) * 6e-4 * g.denom
+    g.max_radii2D = torch.rand((P,), device="cuda", generator=gen) * 40
+
+
+@pytest.mark.parametrize("max_screen_size", [None, 20])
+def test_native_densify_matches_torch(max_screen_size):
+    P = 40_000
+    a, b = _model(P, 3), _model(P, 3)
+    _prime(a, 5)
+    _prime(b, 5)
+    a.native_densify = False
+    a.densify_and_prune(0.0002, 0.005, EXTENT, max_screen_size,
+                        generator=torch.Generator(device="cuda").manual_seed(11))
+    b.densify_and_prune(0.0002, 0.005, EXTENT, max_screen_size,
+                        generator=torch.Generator(device="cuda").manual_seed(11))
+    Pn = a.get_xyz.shape[0]
+    assert b.get_xyz.shape[0] == Pn and Pn != P
+    for name, pa, pb in zip(PARAM_NAMES, a.params(), b.params()):
+        assert pa.shape == pb.shape, name
+        if name == "xyz":
+            torch.testing.assert_close(pb.detach(), pa.detach(), rtol=1e-6, atol=1e-6)
+        else:
+            assert torch.equal(pa.detach(), pb.detach()), name
+        sa, sb = a.optimizer.state[pa], b.optimizer.state[pb]
+        assert torch.equal(sa["exp_avg"], sb["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sb["exp_avg_sq"]), name
+        assert float(sa["step"]) == float(sb["step"])
+        assert any(pb is grp["params"][0] for grp in b.optimizer.param_groups)
+    for t in (b.xyz_gradient_accum, b.denom, b.max_radii2D):
+        assert t.shape[0] == Pn and float(t.abs().sum()) == 0.0
+
+
+def test_native_densify_without_optimizer_state():
+    """Groups with no Adam state yet (no step taken): only the parameters are rebuilt."""
+    a, b = _model(5000, 7), _model(5000, 7)
+    for g in (a, b):
+        P = g.get_xyz.shape[0]
+        g.denom = torch.ones((P, 1), device="cuda")
+        g.xyz_gradient_accum = torch.full((P, 1), 1e-3, device="cuda")
+    a.native_densify = False
+    a.densify_and_prune(0.0002, 0.005, EXTENT, None, generator=torch.Generator(device="cuda").manual_seed(1))
+    b.densify_and_prune(0.0002, 0.005, EXTENT, None, generator=torch.Generator(device="cuda").manual_seed(1))
+    for name, pa, pb in zip(PARAM_NAMES, a.params(), b.params()):
+        assert pa.shape == pb.shape, name
+        if name != "xyz":
+            assert torch.equal(pa.detach(), pb.detach()), name
+        assert len(b.optimizer.state.get(pb, {})) == len(a.optimizer.state.get(pa, {}))
