@@ -13,10 +13,12 @@
 // One host sync (the counts, to size the outputs and draw the split samples).
 //
 // Arithmetic is written as torch evaluates the reference's expressions (one rounding per op: fp
-// contraction off) — exp / log / sigmoid / sqrt / division as ATen's float kernels, division by a
-// Python scalar as a multiplication by its float reciprocal, build_rotation (general_utils.py:52-73)
-// op by op — so decisions and new values are bitwise those of the torch path, except the split
-// children's xyz, whose 3x3 bmm (a BLAS batched GEMM there) accumulates in a fixed fma order here.
+// contraction off) — division by a Python scalar as a multiplication by its float reciprocal (as
+// ATen does; checked on the device), build_rotation (general_utils.py:52-73) op by op — so
+// survivors, clones and the children's other parameters are bitwise those of the torch path; the
+// children's xyz differ by the rounding of the reference's 3x3 bmm (a BLAS batched GEMM there, a
+// fixed fma order here) and their log-scales by up to an ulp of expf/logf (the device library here,
+// ATen's kernels there).
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
     constexpr int PPL = 4 / NW;
     constexpr int B = 64 * NW;
     const int ntiles = a.gx * a.gy;
-    const int tile = xcd_tile(blockIdx.x, ntiles);
+    const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     const int nmax = (int)a.tile_max[tile];  // pairs past this index were blended by no pixel
     if (nmax == 0) return;
     const int tx = tile % a.gx, ty = tile / a.gx;

@@ -66,7 +66,8 @@ struct BlendBwdArgs {
     const uint32_t* n_contrib;
     const float* bg;
     const float* dL_dpix;
-    float* gacc;  // [P][GACC_STRIDE]
+    float* gacc;      // [P][GACC_STRIDE]
+    uint32_t* order;  // [T] scratch: tile of each workgroup, heaviest first (k_tile_order); null: XCD order
 };
 
 struct GaussBwdArgs {
@@ -170,4 +171,6 @@ namespace rr {
 // Tuning knob: waves per tile (1, 2, 4) of the blend kernels; 0 = default / env override.
 void set_blend_config(int fwd_waves, int bwd_waves);
 int blend_fwd_waves();  // 1 or 2 (forward blend, rr_blend_fwd.hip)
+bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_set_tuning "bwd_tile_order")
+int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
 }  // namespace rr
