@@ -264,6 +264,12 @@ int rr_profile_select(unsigned stage_mask);
  * blend kernels (1, 2 or 4; 0 restores the default).  Results are identical for every choice. */
 int rr_set_blend_config(int fwd_waves, int bwd_waves);
 
+/* Runtime tuning knobs (A/B tests; defaults are the measured best):
+ *   "bwd_tile_order" 0/1  backward blend dispatches tiles heaviest first (default 1;
+ *                         env RAIN_BWD_TILE_ORDER), "fwd_waves" / "bwd_waves" as rr_set_blend_config.
+ * Unknown keys return RR_ERR_ARG. */
+int rr_set_tuning(const char* key, int value);
+
 /* Tuning knob (diagnostics / tests): early-stop binning bins L / split_denominator pairs in phase A
  * (1 = one phase) for frames of at least min_pairs pairs; 0 restores a default (4, 2^16).  Results
  * are identical for every choice.  Applies to frames rendered after the call (a backward finds its

@@ -141,6 +141,7 @@ struct Img {
     uint8_t* open;      // [T] tile still open after phase A
     uint32_t* sat;      // [(gy+1)*(gx+1)] 2-D prefix sum of open
     uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask
+    uint32_t* order;      // [T] backward blend dispatch order (heaviest tiles first)
     size_t total;
 };
 Img carve_img(void* buf, int W, int H) {
@@ -158,6 +159,7 @@ Img carve_img(void* buf, int W, int H) {
     m.open = c.take<uint8_t>(T);
     m.sat = c.take<uint32_t>((size_t)(grid_x(W) + 1) * (grid_y(H) + 1));
     m.open_bits = c.take<uint32_t>((T + 31) / 32);
+    m.order = c.take<uint32_t>(T);
     m.total = align_up(c.off);
     return m;
 }
@@ -585,6 +587,7 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
         b.tile_max = im.tile_max;
         b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.bg = cam->background; b.dL_dpix = dL_dpix;
         b.gacc = gacc;
+        b.order = bwd_tile_order() ? im.order : nullptr;
         launch_blend_bwd(b, st);
     }
     RR_STAGE_CHECK("blend backward");
@@ -679,6 +682,11 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves) {
     if (!ok(fwd_waves) || !(ok(bwd_waves) || bwd_waves == 3))
         return fail(RR_ERR_ARG, "waves per tile must be 0, 1, 2 or 4");
     set_blend_config(fwd_waves, bwd_waves);
+    return RR_OK;
+}
+
+int rr_set_tuning(const char* key, int value) {
+    if (set_tuning(key, value) != 0) return fail(RR_ERR_ARG, std::string("unknown tuning key: ") + (key ? key : "(null)"));
     return RR_OK;
 }
 

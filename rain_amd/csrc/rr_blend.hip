@@ -20,6 +20,7 @@
 //   * Tiles are assigned XCD-contiguously (the dispatcher sends block b to XCD b % 8), so tiles
 //     sharing Gaussians share an L2.
 #include <cstdlib>
+#include <string>
 
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
@@ -180,9 +181,40 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
     }
 }
 
+// Heaviest tiles first ("longest processing time" order) for the backward blend: a tile costs
+// tile_max pairs, which varies by more than 10x across a frame, and in XCD order a dense tile
+// dispatched late runs alone on its SIMD after the rest of the grid has drained.  One workgroup:
+// counting sort of the tiles by descending min(tile_max / 4, 1023) (order inside a bucket free).
+__global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __restrict__ cost,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[1024];
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    auto bucket = [&](int i) { return 1023u - min(cost[i] >> 2, 1023u); };
+    hist[t] = 0;
+    __syncthreads();
+    for (int i = t; i < T; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
+    __syncthreads();
+    const uint32_t v = hist[t];
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int i = 0; i < w; i++) pre += wsum[i];
+    hist[t] = pre + incl - v;
+    __syncthreads();
+    for (int i = t; i < T; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
+}
+
 namespace {
 int g_fwd_waves = 0;
 int g_bwd_waves = 0;
+int g_bwd_order = -1;  // -1: RAIN_BWD_TILE_ORDER or the default (on)
 int env_waves(const char* name, int dflt) {
     const char* s = std::getenv(name);
     if (!s) return dflt;
@@ -206,9 +238,28 @@ int blend_fwd_waves() {
     return nw == 1 ? 1 : 2;
 }
 
+bool bwd_tile_order() {
+    if (g_bwd_order < 0) {
+        const char* s = std::getenv("RAIN_BWD_TILE_ORDER");
+        g_bwd_order = s ? (std::atoi(s) != 0) : 1;
+    }
+    return g_bwd_order != 0;
+}
+
+int set_tuning(const char* key, int value) {
+    if (!key) return 1;
+    const std::string k(key);
+    if (k == "bwd_tile_order") g_bwd_order = value != 0;
+    else if (k == "fwd_waves") g_fwd_waves = value;
+    else if (k == "bwd_waves") g_bwd_waves = value;
+    else return 1;
+    return 0;
+}
+
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
+    if (a.order) k_tile_order<<<1, 1024, 0, st>>>(T, a.tile_max, a.order);
     const int nw = g_bwd_waves ? g_bwd_waves : env_waves("RAIN_BLEND_BWD_WAVES", kBwdWavesDefault);
     switch (nw) {
         case 2: k_blend_bwd<2, 1><<<T, 128, 0, st>>>(a); break;

@@ -18,13 +18,14 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--option", default="reuse_binning", help="boolean Trainer attribute to toggle")
+    ap.add_argument("--knob", default=None, help="native tuning key toggled 0/1 instead (rr_set_tuning)")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--points", type=int, default=1_000_000)
     a = ap.parse_args()
     import torch
 
-    from rain_amd import synthetic
+    from rain_amd import _native, synthetic
     from rain_amd.cameras import fibonacci_cameras
     from rain_amd.gaussian_model import GaussianModel, OptimizationParams
     from rain_amd.renderer import PipelineParams, render
@@ -54,7 +55,10 @@ def main():
     res = {False: [], True: []}
     for b in range(2 * a.blocks):
         val = bool(b % 2)
-        setattr(tr, a.option, val)
+        if a.knob:
+            _native.check(_native.raster().rr_set_tuning(a.knob.encode(), int(val)), "tuning")
+        else:
+            setattr(tr, a.option, val)
         tr.step(it)
         it += 1
         torch.cuda.synchronize()
@@ -65,7 +69,7 @@ def main():
         torch.cuda.synchronize()
         res[val].append(1000 * (time.perf_counter() - t0) / a.steps)
     for v in (False, True):
-        print(f"{a.option}={v}: median {statistics.median(res[v]):.4f} ms/step  blocks {[round(x, 4) for x in res[v]]}")
+        print(f"{a.knob or a.option}={v}: median {statistics.median(res[v]):.4f} ms/step  blocks {[round(x, 4) for x in res[v]]}")
 
 
 if __name__ == "__main__":
