@@ -266,7 +266,10 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
 
 /* Runtime tuning knobs (A/B tests; defaults are the measured best):
  *   "bwd_tile_order" 0/1  backward blend dispatches tiles heaviest first (default 1;
- *                         env RAIN_BWD_TILE_ORDER), "fwd_waves" / "bwd_waves" as rr_set_blend_config.
+ *                         env RAIN_BWD_TILE_ORDER),
+ *   "fwd_tile_order" 0/1  forward blends dispatch tiles longest list first (default 0;
+ *                         env RAIN_FWD_TILE_ORDER),
+ *   "fwd_waves" / "bwd_waves" as rr_set_blend_config.
  * Unknown keys return RR_ERR_ARG. */
 int rr_set_tuning(const char* key, int value);
 

@@ -438,6 +438,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = early ? kBlendPhaseA : kBlendSingle;
+        b.order = fwd_tile_order() ? im.order : nullptr;
+        if (b.order) launch_tile_order_by_length(gx * gy, im.ranges, im.order, st);
         launch_blend_fwd(b, st);
     }
     RR_STAGE_CHECK("blend forward");
@@ -468,6 +470,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = kBlendPhaseB;
+        if (b.order) launch_tile_order_by_length(gx * gy, im.ranges_b, im.order, st);
         launch_blend_fwd(b, st);
     }
     RR_STAGE_CHECK("blend forward (phase B)");

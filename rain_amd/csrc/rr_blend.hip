@@ -185,12 +185,17 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
 // tile_max pairs, which varies by more than 10x across a frame, and in XCD order a dense tile
 // dispatched late runs alone on its SIMD after the rest of the grid has drained.  One workgroup:
 // counting sort of the tiles by descending min(tile_max / 4, 1023) (order inside a bucket free).
+// The forward blends use the same order with the tile's list length as its cost (ranges != null).
 __global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __restrict__ cost,
+                                                     const uint2* __restrict__ ranges,
                                                      uint32_t* __restrict__ order) {
     __shared__ uint32_t hist[1024];
     __shared__ uint32_t wsum[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    auto bucket = [&](int i) { return 1023u - min(cost[i] >> 2, 1023u); };
+    auto bucket = [&](int i) {
+        const uint32_t c = ranges ? ranges[i].y - ranges[i].x : cost[i];
+        return 1023u - min(c >> 2, 1023u);
+    };
     hist[t] = 0;
     __syncthreads();
     for (int i = t; i < T; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
@@ -215,6 +220,7 @@ namespace {
 int g_fwd_waves = 0;
 int g_bwd_waves = 0;
 int g_bwd_order = -1;  // -1: RAIN_BWD_TILE_ORDER or the default (on)
+int g_fwd_order = -1;  // -1: RAIN_FWD_TILE_ORDER or the default (off)
 int env_waves(const char* name, int dflt) {
     const char* s = std::getenv(name);
     if (!s) return dflt;
@@ -246,10 +252,25 @@ bool bwd_tile_order() {
     return g_bwd_order != 0;
 }
 
+bool fwd_tile_order() {
+    if (g_fwd_order < 0) {
+        // default off: list length is not what a forward tile costs (saturation is); measured
+        // 1.585 vs 1.581 ms per training step with / without
+        const char* s = std::getenv("RAIN_FWD_TILE_ORDER");
+        g_fwd_order = s ? (std::atoi(s) != 0) : 0;
+    }
+    return g_fwd_order != 0;
+}
+
+void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st) {
+    if (T > 0) k_tile_order<<<1, 1024, 0, st>>>(T, nullptr, ranges, order);
+}
+
 int set_tuning(const char* key, int value) {
     if (!key) return 1;
     const std::string k(key);
     if (k == "bwd_tile_order") g_bwd_order = value != 0;
+    else if (k == "fwd_tile_order") g_fwd_order = value != 0;
     else if (k == "fwd_waves") g_fwd_waves = value;
     else if (k == "bwd_waves") g_bwd_waves = value;
     else return 1;
@@ -259,7 +280,7 @@ int set_tuning(const char* key, int value) {
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
-    if (a.order) k_tile_order<<<1, 1024, 0, st>>>(T, a.tile_max, a.order);
+    if (a.order) k_tile_order<<<1, 1024, 0, st>>>(T, a.tile_max, nullptr, a.order);
     const int nw = g_bwd_waves ? g_bwd_waves : env_waves("RAIN_BLEND_BWD_WAVES", kBwdWavesDefault);
     switch (nw) {
         case 2: k_blend_bwd<2, 1><<<T, 128, 0, st>>>(a); break;

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
     constexpr int PAIRS = 2 / NW;  // pixel pairs per lane
     constexpr int B = 64 * NW;     // records per round
     const int ntiles = a.gx * a.gy;
-    const int tile = xcd_tile(blockIdx.x, ntiles);
+    const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int t = threadIdx.x;

@@ -53,6 +53,7 @@ struct BlendFwdArgs {
     int phase;              // BlendPhase
     const float4* normals;  // aux normal output (RR_FLAG_AUX_NORMAL): per-Gaussian normals and
     float* out_normal;      // the blended normal map [3,H,W]; both null otherwise
+    const uint32_t* order;  // [T] tile of each workgroup, longest list first; null: XCD order
 };
 
 struct BlendBwdArgs {
@@ -172,5 +173,7 @@ namespace rr {
 void set_blend_config(int fwd_waves, int bwd_waves);
 int blend_fwd_waves();  // 1 or 2 (forward blend, rr_blend_fwd.hip)
 bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_set_tuning "bwd_tile_order")
+bool fwd_tile_order();  // forward blends dispatch tiles longest list first (rr_set_tuning "fwd_tile_order")
+void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
 }  // namespace rr
