@@ -83,11 +83,41 @@ def _valu_busy(dirname):
     return {st: statistics.median(v) for st, v in out.items()}
 
 
+def _inst_mix(dirname):
+    """Per kernel (median over launches): wave-level VALU / SALU / LDS instruction counts and the
+    VALU issue fraction = SQ_INSTS_VALU x 2 cycles (a wave64 VALU op occupies a SIMD-32 for two
+    cycles; transcendentals longer, so this is a lower bound) / (duration x 1024 SIMDs x clock)."""
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
+    acc = {}
+    for fn in files:
+        per = {}
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                st = _stage(row.get("Kernel_Name", ""))
+                if st is None:
+                    continue
+                d = per.setdefault((st, row.get("Dispatch_Id")), {"dur": None})
+                d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                if row.get("End_Timestamp") and row.get("Start_Timestamp"):
+                    d["dur"] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+        for (st, _), d in per.items():
+            if not d.get("dur") or "SQ_INSTS_VALU" not in d:
+                continue
+            r = acc.setdefault(st, {})
+            for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
+                if k in d:
+                    r.setdefault(k, []).append(d[k])
+            r.setdefault("valu_issue_frac", []).append(2.0 * d["SQ_INSTS_VALU"] / (d["dur"] * CLOCK_GHZ * SIMDS))
+    return {st: {k.lower(): round(statistics.median(v), 4 if k == "valu_issue_frac" else 0) for k, v in r.items()}
+            for st, r in acc.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--sq-dir", default=None, help="a third pass with SQ_ACTIVE_INST_VALU (VALU busy)")
+    ap.add_argument("--inst-dir", default=None, help="a pass with SQ_INSTS_VALU/SALU/LDS and SQ_WAVES")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
@@ -109,6 +139,11 @@ def main():
                                  f"{CLOCK_GHZ} GHz): fraction of SIMD cycles issuing a VALU op")
         for st, v in _valu_busy(a.sq_dir).items():
             out["kernels"].setdefault(st, {})["valu_busy"] = round(v, 3)
+    if a.inst_dir:
+        out["inst_note"] = ("wave-level instruction counts per launch (SQ_INSTS_*); valu_issue_frac = "
+                            f"SQ_INSTS_VALU x 2 cycles / (duration x 1024 SIMDs x {CLOCK_GHZ} GHz)")
+        for st, v in _inst_mix(a.inst_dir).items():
+            out["kernels"].setdefault(st, {}).update(v)
     with open(a.out, "w") as fo:
         json.dump(out, fo, indent=1)
     print(json.dumps(out, indent=1))

@@ -17,6 +17,8 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" 
     -- python3 tools/pmc_workload.py > "$OUT/write.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/pmc_sq" -o run \
     --output-format csv -- python3 tools/pmc_workload.py > "$OUT/sq.log" 2>&1
-python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --sq-dir "$OUT/pmc_sq" \
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --kernel-trace \
+    -d "$OUT/pmc_inst" -o run --output-format csv -- python3 tools/pmc_workload.py > "$OUT/inst.log" 2>&1
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --sq-dir "$OUT/pmc_sq" --inst-dir "$OUT/pmc_inst" \
     --out "$OUT/pmc_traffic.json" > /dev/null
 echo "profile passes done: $OUT"
