@@ -52,8 +52,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
 
     const size_t HW = (size_t)a.H * a.W;
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
-    float T[PPL], tfbg[PPL], dp0[PPL], dp1[PPL], dp2[PPL];
-    float ar0[PPL], ar1[PPL], ar2[PPL], lc0[PPL], lc1[PPL], lc2[PPL], la[PPL];
+    // The reference keeps accum_rec per channel (backward.cu:497-507) and only ever uses its dot
+    // product with dL/dpix; by linearity the same convex-combination recurrence runs on the scalar
+    // R = accum_rec . dL/dpix, with lcdp = last_color . dL/dpix (8 fewer VALU ops and 4 fewer VGPRs
+    // per pixel and pair, and as well conditioned as the per-channel form).
+    float T[PPL], tfbg[PPL], dp0[PPL], dp1[PPL], dp2[PPL], R[PPL], lcdp[PPL], la[PPL];
     int last[PPL];
 #pragma unroll
     for (int q = 0; q < PPL; q++) {
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
         dp2[q] = inside ? a.dL_dpix[2 * HW + pix] : 0.f;
         // -T_final * (bg . dL/dpixel): numerator of the background term (backward.cu:521-524)
         tfbg[q] = -Tf * (bg0 * dp0[q] + bg1 * dp1[q] + bg2 * dp2[q]);
-        ar0[q] = ar1[q] = ar2[q] = lc0[q] = lc1[q] = lc2[q] = la[q] = 0.f;
+        R[q] = lcdp[q] = la[q] = 0.f;
     }
     const uint2 range = a.ranges[tile];
     const uint2 range_b = a.ranges_b[tile];
@@ -116,22 +119,18 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     any = true;
                     const float one_m = 1.f - alpha;
                     const float inv = rcp_nr(one_m);  // both divisions by (1 - alpha) share one reciprocal
-                    T[q] = T[q] * inv;
+                    T[q] = T[q] * inv;                // T_i, the transmittance in front of this Gaussian
                     const float dchannel_dcolor = alpha * T[q];
                     const float4 Cc = s_c[j];
-                    ar0[q] = la[q] * lc0[q] + (1.f - la[q]) * ar0[q];
-                    ar1[q] = la[q] * lc1[q] + (1.f - la[q]) * ar1[q];
-                    ar2[q] = la[q] * lc2[q] + (1.f - la[q]) * ar2[q];
-                    lc0[q] = Cc.x;
-                    lc1[q] = Cc.y;
-                    lc2[q] = Cc.z;
-                    float dL_dalpha = (Cc.x - ar0[q]) * dp0[q] + (Cc.y - ar1[q]) * dp1[q] + (Cc.z - ar2[q]) * dp2[q];
+                    const float cdp = Cc.x * dp0[q] + Cc.y * dp1[q] + Cc.z * dp2[q];
                     g6 += dchannel_dcolor * dp0[q];
                     g7 += dchannel_dcolor * dp1[q];
                     g8 += dchannel_dcolor * dp2[q];
-                    dL_dalpha *= T[q];
+                    R[q] = la[q] * lcdp[q] + (1.f - la[q]) * R[q];
+                    lcdp[q] = cdp;
                     la[q] = alpha;
-                    dL_dalpha += tfbg[q] * inv;
+                    // dL/dalpha = T_i (c - accum_rec) . dL/dpix - T_final (bg . dL/dpix) / (1 - alpha)
+                    const float dL_dalpha = (cdp - R[q]) * T[q] + tfbg[q] * inv;
                     const float dL_dG = Bv.y * dL_dalpha;
                     // dG/d(delta) = -G (conic . delta): the conic is the same for every pixel of
                     // the pair, so only Sx = sum dL_dG G dx and Sy = sum dL_dG G dy are summed per
