@@ -244,7 +244,11 @@ def main():
                     "algorithmic_bytes_per_launch": int(byts),
                     # the blend kernels are VALU-issue bound, not HBM bound: fraction of SIMD
                     # cycles issuing a VALU op, from the committed SQ counter pass
-                    "valu_busy": _pmc_field(dom, "valu_busy") if (P, W, H) == (1_000_000, 1920, 1080) else None}
+                    "valu_busy": _pmc_field(dom, "valu_busy") if (P, W, H) == (1_000_000, 1920, 1080) else None,
+                    # VALU issue roofline from the SQ_INSTS_VALU pass: wave instructions x 2 cycles
+                    # over (duration x 1024 SIMDs x 2.4 GHz) -- the bound the blend kernels sit on
+                    "valu_issue_frac": (_pmc_field(dom, "valu_issue_frac")
+                                        if (P, W, H) == (1_000_000, 1920, 1080) else None)}
         for k in kernels:
             b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2)
             if b is not None:
