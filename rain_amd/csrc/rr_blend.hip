@@ -195,9 +195,18 @@ __global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __re
         const uint32_t c = ranges ? ranges[i].y - ranges[i].x : cost[i];
         return 1023u - min(c >> 2, 1023u);
     };
+    // up to kReg tiles per thread stay in registers between the two passes (one read of the costs,
+    // all loads in flight together); larger grids fall back to re-reading
+    constexpr int kReg = 16;
+    uint32_t bk[kReg];
+#pragma unroll
+    for (int r = 0; r < kReg; r++) bk[r] = (t + r * 1024 < T) ? bucket(t + r * 1024) : 0u;
     hist[t] = 0;
     __syncthreads();
-    for (int i = t; i < T; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
+#pragma unroll
+    for (int r = 0; r < kReg; r++)
+        if (t + r * 1024 < T) atomicAdd(&hist[bk[r]], 1u);
+    for (int i = t + kReg * 1024; i < T; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
     __syncthreads();
     const uint32_t v = hist[t];
     uint32_t incl = v;
@@ -212,13 +221,17 @@ __global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __re
     for (int i = 0; i < w; i++) pre += wsum[i];
     hist[t] = pre + incl - v;
     __syncthreads();
-    for (int i = t; i < T; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
+#pragma unroll
+    for (int r = 0; r < kReg; r++)
+        if (t + r * 1024 < T) order[atomicAdd(&hist[bk[r]], 1u)] = (uint32_t)(t + r * 1024);
+    for (int i = t + kReg * 1024; i < T; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
 }
 
 namespace {
 int g_fwd_waves = 0;
 int g_bwd_waves = 0;
 int g_bwd_order = -1;  // -1: RAIN_BWD_TILE_ORDER or the default (on)
+int g_fwd_b_waves = -1;  // -1: RAIN_BLEND_FWD_B_WAVES or the default
 int g_fwd_order = -1;  // -1: RAIN_FWD_TILE_ORDER or the default (off)
 int env_waves(const char* name, int dflt) {
     const char* s = std::getenv(name);
@@ -232,6 +245,7 @@ int env_waves(const char* name, int dflt) {
 // (rr_blend_fwd.hip) runs 1 or 2 waves per tile (4 or 2 pixels per lane, packed in pairs).
 constexpr int kFwdWavesDefault = 2;
 constexpr int kBwdWavesDefault = 1;
+constexpr int kFwdBWavesDefault = 4;
 
 void set_blend_config(int fwd_waves, int bwd_waves) {
     g_fwd_waves = fwd_waves;
@@ -249,6 +263,14 @@ bool bwd_tile_order() {
         g_bwd_order = s ? (std::atoi(s) != 0) : 1;
     }
     return g_bwd_order != 0;
+}
+
+int blend_fwd_b_waves() {
+    if (g_fwd_b_waves < 0) {
+        const char* s = std::getenv("RAIN_BLEND_FWD_B_WAVES");
+        g_fwd_b_waves = s ? std::atoi(s) : kFwdBWavesDefault;
+    }
+    return g_fwd_b_waves == 4 ? 4 : 0;
 }
 
 bool fwd_tile_order() {
@@ -270,6 +292,7 @@ int set_tuning(const char* key, int value) {
     const std::string k(key);
     if (k == "bwd_tile_order") g_bwd_order = value != 0;
     else if (k == "fwd_tile_order") g_fwd_order = value != 0;
+    else if (k == "fwd_b_waves") g_fwd_b_waves = value ? 4 : 0;
     else if (k == "fwd_waves") g_fwd_waves = value;
     else if (k == "bwd_waves") g_bwd_waves = value;
     else return 1;

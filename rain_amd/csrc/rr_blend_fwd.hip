@@ -28,8 +28,11 @@ __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementw
 template <int NW, bool AUX>
 __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
 #pragma clang fp contract(off)  // exactly blend_power's rounding: every fma below is explicit
-    constexpr int PAIRS = 2 / NW;  // pixel pairs per lane
-    constexpr int B = 64 * NW;     // records per round
+    // NW = 4 (phase B of early-stop binning: few open tiles with long lists, so per-tile latency
+    // rules): each lane owns ONE pixel, the packed pair's second half is a masked dummy
+    constexpr bool HALF = NW == 4;
+    constexpr int PAIRS = HALF ? 1 : 2 / NW;  // pixel pairs per lane
+    constexpr int B = 64 * NW;                // records per round
     const int ntiles = a.gx * a.gy;
     const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
@@ -52,12 +55,12 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
     uint32_t last[PAIRS][2];
 #pragma unroll
     for (int p = 0; p < PAIRS; p++) {
-        const int row0 = ty * TILE_Y + (lane >> 4) + 8 * (w * PAIRS + p);
+        const int row0 = ty * TILE_Y + (lane >> 4) + (HALF ? 4 * w : 8 * (w * PAIRS + p));
         py[p][0] = row0;
-        py[p][1] = row0 + 4;
-        pfy[p] = f2{(float)row0, (float)(row0 + 4)};
+        py[p][1] = HALF ? 0x3fffffff : row0 + 4;  // HALF: never inside the image
+        pfy[p] = f2{(float)row0, (float)(HALF ? row0 : row0 + 4)};
         T[p] = f2{1.f, 1.f};
-        om[p] = f2{(px < a.W && row0 < a.H) ? 1.f : 0.f, (px < a.W && row0 + 4 < a.H) ? 1.f : 0.f};
+        om[p] = f2{(px < a.W && row0 < a.H) ? 1.f : 0.f, (px < a.W && py[p][1] < a.H) ? 1.f : 0.f};
         C0[p] = C1[p] = C2[p] = Dp[p] = f2{0.f, 0.f};
         N0[p] = N1[p] = N2[p] = f2{0.f, 0.f};
         last[p][0] = last[p][1] = 0;
@@ -244,7 +247,10 @@ void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
     const bool aux = a.out_normal != nullptr;
-    if (blend_fwd_waves() == 1) {
+    if (a.phase == kBlendPhaseB && blend_fwd_b_waves() == 4) {
+        if (aux) k_blend_fwd<4, true><<<T, 256, 0, st>>>(a);
+        else k_blend_fwd<4, false><<<T, 256, 0, st>>>(a);
+    } else if (blend_fwd_waves() == 1) {
         if (aux) k_blend_fwd<1, true><<<T, 64, 0, st>>>(a);
         else k_blend_fwd<1, false><<<T, 64, 0, st>>>(a);
     } else {

@@ -171,7 +171,8 @@ void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
 namespace rr {
 // Tuning knob: waves per tile (1, 2, 4) of the blend kernels; 0 = default / env override.
 void set_blend_config(int fwd_waves, int bwd_waves);
-int blend_fwd_waves();  // 1 or 2 (forward blend, rr_blend_fwd.hip)
+int blend_fwd_waves();    // 1 or 2 (forward blend, rr_blend_fwd.hip)
+int blend_fwd_b_waves();  // phase B of early-stop binning: 4 (one pixel per lane) or as phase A
 bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_set_tuning "bwd_tile_order")
 bool fwd_tile_order();  // forward blends dispatch tiles longest list first (rr_set_tuning "fwd_tile_order")
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
