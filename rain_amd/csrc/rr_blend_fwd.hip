@@ -127,28 +127,45 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
             if (AUX) nn = a.normals[id];
         }
         const int cnt = min(B, n - base);
-        for (int j = 0; j < cnt; j++) {
-            if ((j & 3) == 0 && __all(all_closed())) break;
-            const float4 A = s_a[j];
+        for (int j0 = 0; j0 < cnt; j0 += 4) {
+            if (__all(all_closed())) break;
+            // groups of 4 pairs: the falloff / alpha of the 4 pairs (independent of T) are formed
+            // first, so their exp / compare chains overlap; only the blend below is sequential.
+            // A slot past cnt (stale / uninitialised LDS, j < B still) is computed but never blended.
+            f2 alq[4][PAIRS];
+#pragma unroll
+            for (int uu = 0; uu < 4; uu++) {
+                const int j = j0 + uu;
+                const float4 A = s_a[j];
+                const float4 Bv = s_b[j];
+                // x-terms shared by both pixels of a pair (blend_power's op sequence)
+                const float dx = A.x - pfx;
+                const float cxdx2 = (A.z * dx) * dx;
+                const float wdx = A.w * dx;
+#pragma unroll
+                for (int p = 0; p < PAIRS; p++) {
+                    const f2 dy = f2{A.y, A.y} - pfy[p];
+                    const f2 tq = fma2(f2{Bv.x, Bv.x} * dy, dy, f2{cxdx2, cxdx2});
+                    const f2 u = f2{wdx, wdx} * dy;
+                    const f2 power = fma2(f2{-0.5f, -0.5f}, tq, -u);
+                    const f2 pl = power * f2{kLog2e, kLog2e};
+                    f2 al = f2{Bv.y, Bv.y} * f2{__builtin_amdgcn_exp2f(pl.x), __builtin_amdgcn_exp2f(pl.y)};
+                    // forward.cu:333-336: skip power > 0 and alpha < 1/255 (alpha := 0)
+                    al.x = (power.x <= 0.0f && fminf(0.99f, al.x) >= 1.0f / 255.0f) ? fminf(0.99f, al.x) : 0.f;
+                    al.y = (power.y <= 0.0f && fminf(0.99f, al.y) >= 1.0f / 255.0f) ? fminf(0.99f, al.y) : 0.f;
+                    alq[uu][p] = al;
+                }
+            }
+#pragma unroll
+            for (int uu = 0; uu < 4; uu++) {
+            const int j = j0 + uu;
+            if (j >= cnt) break;
             const float4 Bv = s_b[j];
             const float4 Cc = s_c[j];
             const uint32_t k1 = koff + (uint32_t)(base + j + 1);
-            // x-terms shared by both pixels of a pair (blend_power's op sequence)
-            const float dx = A.x - pfx;
-            const float cxdx2 = (A.z * dx) * dx;
-            const float wdx = A.w * dx;
 #pragma unroll
             for (int p = 0; p < PAIRS; p++) {
-                const f2 dy = f2{A.y, A.y} - pfy[p];
-                const f2 tq = fma2(f2{Bv.x, Bv.x} * dy, dy, f2{cxdx2, cxdx2});
-                const f2 u = f2{wdx, wdx} * dy;
-                const f2 power = fma2(f2{-0.5f, -0.5f}, tq, -u);
-                const f2 pl = power * f2{kLog2e, kLog2e};
-                f2 al = f2{Bv.y, Bv.y} * f2{__builtin_amdgcn_exp2f(pl.x), __builtin_amdgcn_exp2f(pl.y)};
-                // forward.cu:333-336: skip power > 0 and alpha < 1/255 (alpha := 0)
-                al.x = (power.x <= 0.0f && fminf(0.99f, al.x) >= 1.0f / 255.0f) ? fminf(0.99f, al.x) : 0.f;
-                al.y = (power.y <= 0.0f && fminf(0.99f, al.y) >= 1.0f / 255.0f) ? fminf(0.99f, al.y) : 0.f;
-                al = al * om[p];
+                const f2 al = alq[uu][p] * om[p];
                 const f2 testT = T[p] * (f2{1.f, 1.f} - al);
                 // forward.cu:337-341: saturation closes the pixel without blending this Gaussian
                 const bool sat0 = testT.x < 0.0001f, sat1 = testT.y < 0.0001f;
@@ -171,6 +188,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
                 om[p].y = sat1 ? 0.f : om[p].y;
                 last[p][0] = wgt.x > 0.f ? k1 : last[p][0];
                 last[p][1] = wgt.y > 0.f ? k1 : last[p][1];
+            }
             }
         }
         __syncthreads();
