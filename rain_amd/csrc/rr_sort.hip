@@ -71,36 +71,66 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ 
     for (int d = t; d < ndig; d += 64 * kWaves) counts[(size_t)d * units + unit] = hist[d];
 }
 
-// Exclusive scan of each digit's row of counts over the units (one workgroup per digit, rows
-// walked in tiles of 256) -> offsets[d][unit] relative to the digit, and the digit's total.  The
-// scatter adds the digit bases (exclusive scan of the <= 256 totals) itself.  Replaces a device
-// scan call and its host-side dispatch overhead.
+// Exclusive scan of each digit's row of counts over the units (one workgroup per digit) ->
+// offsets[d][unit] relative to the digit, and the digit's total.  The scatter adds the digit bases
+// (exclusive scan of the <= 256 totals) itself.  Replaces a device scan call and its host-side
+// dispatch overhead.  Rows of up to 256 * kScanReg units are read into registers in one go (thread
+// t owns a contiguous run of units), so the scan waits for one load latency instead of one per
+// 256 units; longer rows are walked in tiles of 256.
+constexpr int kScanReg = 16;
+__device__ __forceinline__ uint32_t block_exclusive_scan256(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t wpre = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        wpre += i < w ? wsum[i] : 0u;
+        total += wsum[i];
+    }
+    return wpre + incl - v;
+}
+
 __global__ __launch_bounds__(256) void k_rs_scan_rows(const uint32_t* __restrict__ counts,
                                                       uint32_t* __restrict__ offsets, int units,
                                                       uint32_t* __restrict__ totals) {
     __shared__ uint32_t wsum[4];
-    const int d = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int d = blockIdx.x, t = threadIdx.x;
     const uint32_t* row = counts + (size_t)d * units;
     uint32_t* out = offsets + (size_t)d * units;
+    if (units <= 256 * kScanReg) {
+        const int c = (units + 255) / 256;  // units per thread
+        const int u0 = t * c;
+        uint32_t v[kScanReg], sum = 0;
+#pragma unroll
+        for (int i = 0; i < kScanReg; i++) {
+            v[i] = (i < c && u0 + i < units) ? row[u0 + i] : 0u;
+            sum += v[i];
+        }
+        uint32_t total;
+        uint32_t run = block_exclusive_scan256(sum, wsum, total);
+#pragma unroll
+        for (int i = 0; i < kScanReg; i++) {
+            if (i < c && u0 + i < units) out[u0 + i] = run;
+            run += v[i];
+        }
+        if (t == 0) totals[d] = total;
+        return;
+    }
     uint32_t carry = 0;
     for (int base = 0; base < units; base += 256) {
         const int u = base + t;
         const uint32_t v = u < units ? row[u] : 0u;
-        uint32_t incl = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint32_t wpre = 0, tile = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            wpre += i < w ? wsum[i] : 0u;
-            tile += wsum[i];
-        }
-        if (u < units) out[u] = carry + wpre + incl - v;
+        uint32_t tile;
+        const uint32_t ex = block_exclusive_scan256(v, wsum, tile);
+        if (u < units) out[u] = carry + ex;
         carry += tile;
         __syncthreads();
     }
