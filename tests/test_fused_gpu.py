@@ -170,9 +170,12 @@ def test_adam_fused_into_backward_matches_separate_step(gpu):
                 g.optimizer.step()
         models.append(g)
     a, b = models
+    # the two runs' backward atomics sum in different orders; Adam divides by sqrt(v), which turns
+    # last-bit gradient differences of a nearly-cancelling Gaussian into ~1e-6-relative parameter
+    # differences (observed 3.6e-6 on opacity, lr 0.05): 1e-5 of the parameter scale
     for k in NAMES:
         x, y = _params(a)[k].detach(), _params(b)[k].detach()
-        assert (x - y).abs().max() <= 1e-6 * max(1.0, float(y.abs().max())), (k, float((x - y).abs().max()))
+        assert (x - y).abs().max() <= 1e-5 * max(1.0, float(y.abs().max())), (k, float((x - y).abs().max()))
     for pa, pb in zip(a.params(), b.params()):
         sa, sb = a.optimizer.state[pa], b.optimizer.state[pb]
         assert float(sa["step"]) == float(sb["step"]) == 3.0
