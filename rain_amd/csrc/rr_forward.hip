@@ -188,7 +188,7 @@ __global__ __launch_bounds__(1024) void k_open_sat(int gx, int gy, const uint8_t
 // A Gaussian whose tile rectangle holds no open tile (2-D prefix-sum test) is skipped without
 // enumerating its rows; the kept pairs of the window are compacted (order preserved) and the
 // window's length goes to unit_len[k] (a sparse sort unit) and into *n_total.
-template <typename K>
+template <typename K, bool FILTER>
 __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __restrict__ idx_sorted,
                                                    const uint2* __restrict__ offsets,
                                                    const Splat* __restrict__ splats, const int* __restrict__ radii,
@@ -200,7 +200,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                                                    const uint32_t* __restrict__ open_bits,
                                                    uint32_t* __restrict__ unit_len, uint32_t* __restrict__ n_total) {
     // open-tile bitmask in LDS for 16-bit tile ids (T <= 65536); wider grids read open[] directly
-    constexpr bool kMaskLds = sizeof(K) == 2;
+    // (FILTER: phase B; the unfiltered kernel does without the mask's 8 KiB of LDS)
+    constexpr bool kMaskLds = sizeof(K) == 2 && FILTER;
     __shared__ K s_key[kSortMaxUnit];
     __shared__ uint32_t s_val[kSortMaxUnit];
     __shared__ uint32_t hist[256];
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
-    const bool filter = sat != nullptr;
+    constexpr bool filter = FILTER;
     for (int d = t; d < ndig; d += 256) hist[d] = 0;
     const uint32_t w0 = pair0 + blockIdx.x * win, w1 = min(w0 + win, L);
     const uint32_t wn = w1 - w0;
@@ -317,22 +318,23 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
 template <typename K>
 __global__ __launch_bounds__(256) void k_ranges(int L, const K* __restrict__ keys, uint2* __restrict__ ranges,
                                                 uint32_t base, const uint32_t* __restrict__ n_dev) {
-    // L: host bound; n_dev (optional): the device-side count of a filtered list.  Ranges are
-    // absolute point_list indices (base + position).
+    // L: host bound; n_dev (optional): the device-side count of a filtered list (grid-stride, so a
+    // short filtered list does not pay for a grid sized by its bound).  Ranges are absolute
+    // point_list indices (base + position).
     const int n = n_dev ? (int)*n_dev : L;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t cur = keys[i];
-    if (i == 0) {
-        ranges[cur].x = base;
-    } else {
-        const uint32_t prev = keys[i - 1];
-        if (cur != prev) {
-            ranges[prev].y = base + i;
-            ranges[cur].x = base + i;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t cur = keys[i];
+        if (i == 0) {
+            ranges[cur].x = base;
+        } else {
+            const uint32_t prev = keys[i - 1];
+            if (cur != prev) {
+                ranges[prev].y = base + i;
+                ranges[cur].x = base + i;
+            }
         }
+        if (i == n - 1) ranges[cur].y = base + n;
     }
-    if (i == n - 1) ranges[cur].y = base + n;
 }
 
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
@@ -363,7 +365,8 @@ template <typename K>
 void launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
     if (d.P == 0 || d.nwin == 0 || d.win > (uint32_t)kSortMaxUnit) return;  // win comes from radix_sort_plan
     k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.P, d.offsets, d.pair0, d.win, d.nwin, d.first);
-    k_duplicate<K><<<d.nwin, 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
+    auto kern = d.sat ? k_duplicate<K, true> : k_duplicate<K, false>;
+    kern<<<d.nwin, 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
                                             d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts, d.nwin,
                                             d.sat, d.open_bits, d.unit_len, d.n_total);
 }
@@ -380,7 +383,8 @@ void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_
 template <typename K>
 void launch_ranges(int L, const K* keys, uint2* ranges, uint32_t base, const uint32_t* n_dev, hipStream_t st) {
     if (L == 0) return;
-    k_ranges<K><<<blocks_for(L), 256, 0, st>>>(L, keys, ranges, base, n_dev);
+    const int nb = blocks_for(L);
+    k_ranges<K><<<(n_dev && nb > 2048) ? 2048 : nb, 256, 0, st>>>(L, keys, ranges, base, n_dev);
 }
 template void launch_ranges<uint16_t>(int, const uint16_t*, uint2*, uint32_t, const uint32_t*, hipStream_t);
 template void launch_ranges<uint32_t>(int, const uint32_t*, uint2*, uint32_t, const uint32_t*, hipStream_t);

@@ -159,6 +159,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     const uint32_t unit_items = (uint32_t)rounds * 64 * kWaves;
     const size_t ubase = (size_t)unit * unit_items;
     const uint32_t len = unit_length(unit_len, n_dev, n, unit, unit_items);
+    if (len == 0) return;  // empty unit (sparse producer / past the device-side count): no output
     // wave w owns the contiguous items [wl, wl + 64 * rounds) of the unit (local indices)
     const uint32_t wl = (uint32_t)w * 64 * rounds;
     const size_t wbase = ubase + wl;
