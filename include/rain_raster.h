@@ -274,7 +274,7 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
 int rr_set_tuning(const char* key, int value);
 
 /* Tuning knob (diagnostics / tests): early-stop binning bins L / split_denominator pairs in phase A
- * (1 = one phase) for frames of at least min_pairs pairs; 0 restores a default (4, 2^16).  Results
+ * (1 = one phase) for frames of at least min_pairs pairs; 0 restores a default (3, 2^16).  Results
  * are identical for every choice.  Applies to frames rendered after the call (a backward finds its
  * frame's lists in the image buffer). */
 int rr_set_binning_config(int split_denominator, int min_pairs);

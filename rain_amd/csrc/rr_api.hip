@@ -165,13 +165,14 @@ Img carve_img(void* buf, int W, int H) {
 }
 
 // Early-stop binning split: phase A bins the first L_A pairs (depth order) for every tile, phase B
-// the rest for the tiles phase A left open (rr_kernels.hpp BlendPhase).  L_A = L/4: on the bench
-// frames (1M Gaussians, 1080p) most tiles saturate inside it and phase A + B bin ~25% of the pairs
-// (tools/saturation_stats.py); measured per training step 1.671 ms vs 1.742 ms for one phase, and
-// 1.695 / 1.688 / 1.712 for L/2, L/3, L/6 (tools/host_profile.py --binning-split).  Frames below
-// kEarlyMin pairs are binned in one phase.  rr_set_binning_config changes both (tests force the
-// split onto small frames).
-constexpr uint32_t kEarlyDen = 4, kEarlyMin = 1u << 16;
+// the rest for the tiles phase A left open (rr_kernels.hpp BlendPhase).  L_A = L/3: on the bench
+// frames (1M Gaussians, 1080p) most tiles saturate inside it (tools/saturation_stats.py).  First
+// measured at L/4 (1.671 ms per training step vs 1.742 ms for one phase; 1.695 / 1.688 / 1.712 for
+// L/2, L/3, L/6); after the phase-B fixed costs shrank and the binning kernels sped up, re-measured
+// interleaved (tools/step_ab.py --split 2,3,4, 8 blocks of 60 steps): 1.509 / 1.491 / 1.525 ms.
+// Frames below kEarlyMin pairs are binned in one phase.  rr_set_binning_config changes both (tests
+// force the split onto small frames).
+constexpr uint32_t kEarlyDen = 3, kEarlyMin = 1u << 16;
 uint32_t g_early_den = kEarlyDen, g_early_min = kEarlyMin;
 uint32_t early_split(uint32_t L) {
     if (g_early_den <= 1 || L < g_early_min) return L;

@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--option", default="reuse_binning", help="boolean Trainer attribute to toggle")
     ap.add_argument("--knob", default=None, help="native tuning key toggled 0/1 instead (rr_set_tuning)")
+    ap.add_argument("--split", default=None,
+                    help="comma-separated early-stop split denominators to compare (rr_set_binning_config)")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--points", type=int, default=1_000_000)
@@ -52,10 +54,13 @@ def main():
     for _ in range(10):
         tr.step(it)
         it += 1
-    res = {False: [], True: []}
-    for b in range(2 * a.blocks):
-        val = bool(b % 2)
-        if a.knob:
+    arms = [int(x) for x in a.split.split(",")] if a.split else [False, True]
+    res = {v: [] for v in arms}
+    for b in range(len(arms) * a.blocks):
+        val = arms[b % len(arms)]
+        if a.split:
+            _native.check(_native.raster().rr_set_binning_config(val, 0), "binning config")
+        elif a.knob:
             _native.check(_native.raster().rr_set_tuning(a.knob.encode(), int(val)), "tuning")
         else:
             setattr(tr, a.option, val)
@@ -68,8 +73,8 @@ def main():
             it += 1
         torch.cuda.synchronize()
         res[val].append(1000 * (time.perf_counter() - t0) / a.steps)
-    for v in (False, True):
-        print(f"{a.knob or a.option}={v}: median {statistics.median(res[v]):.4f} ms/step  blocks {[round(x, 4) for x in res[v]]}")
+    for v in arms:
+        print(f"{'split' if a.split else (a.knob or a.option)}={v}: median {statistics.median(res[v]):.4f} ms/step  blocks {[round(x, 4) for x in res[v]]}")
 
 
 if __name__ == "__main__":
