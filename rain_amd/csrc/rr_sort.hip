@@ -44,7 +44,7 @@ __device__ __forceinline__ uint32_t unit_length(const uint32_t* unit_len, const 
     return base >= nn ? 0u : (uint32_t)min((size_t)unit_items, nn - base);
 }
 
-template <typename K>
+template <typename K, int MAXR>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ keys, size_t n, int shift, int dbits,
                                                           int rounds, uint32_t* __restrict__ counts, int units,
                                                           const uint32_t* __restrict__ n_dev) {
@@ -57,15 +57,15 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ 
     const size_t base = (size_t)unit * unit_items;
     const uint32_t len = unit_length(nullptr, n_dev, n, unit, unit_items);
     const uint32_t mask = (uint32_t)ndig - 1u;
-    uint32_t dr[kMaxRounds];
+    uint32_t dr[MAXR];
 #pragma unroll
-    for (int r = 0; r < kMaxRounds; r++) {  // all loads in flight before the first LDS atomic
+    for (int r = 0; r < MAXR; r++) {  // all loads in flight before the first LDS atomic
         const uint32_t li = (uint32_t)r * 64 * kWaves + t;
         dr[r] = (r < rounds && li < len) ? (((uint32_t)keys[base + li] >> shift) & mask) : 0xffffffffu;
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kMaxRounds; r++)
+    for (int r = 0; r < MAXR; r++)
         if (dr[r] != 0xffffffffu) atomicAdd(&hist[dr[r]], 1u);
     __syncthreads();
     for (int d = t; d < ndig; d += 64 * kWaves) counts[(size_t)d * units + unit] = hist[d];
@@ -137,7 +137,10 @@ __global__ __launch_bounds__(256) void k_rs_scan_rows(const uint32_t* __restrict
     if (t == 0) totals[d] = carry;
 }
 
-template <typename K>
+// MAXR: rounds the kernel is compiled for (>= the call's rounds).  Small units get a small
+// instance: the LDS staging is sized by it, so e.g. the 512-item units of a 1M-key sort fit ~4x
+// more workgroups per CU than a 4096-item staging area allows.
+template <typename K, int MAXR>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict__ keys_in,
                                                             const uint32_t* __restrict__ vals_in,
                                                             K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -150,8 +153,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     __shared__ uint32_t wcnt[kWaves][256];  // per-wave digit counts, then per-wave cursors
     __shared__ uint32_t dstart[256];        // block-local start of each digit's run
     __shared__ uint32_t goff[256];          // global slot of block-local position 0 of each digit's run
-    __shared__ uint32_t s_val[kMaxUnitItems];
-    __shared__ K s_key[kMaxUnitItems];
+    __shared__ uint32_t s_val[64 * kWaves * MAXR];
+    __shared__ K s_key[64 * kWaves * MAXR];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int ndig = 1 << dbits;
     const uint32_t mask = (uint32_t)ndig - 1u;
@@ -188,10 +191,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     }
     // the wave's items go to registers once (all loads in flight together); counting, ranking
     // and staging then run from registers
-    K kr[kMaxRounds];
-    uint32_t vr[kMaxRounds];
+    K kr[MAXR];
+    uint32_t vr[MAXR];
 #pragma unroll
-    for (int r = 0; r < kMaxRounds; r++) {
+    for (int r = 0; r < MAXR; r++) {
         const size_t i = wbase + (size_t)r * 64 + lane;
         const bool valid = r < rounds && wl + (uint32_t)r * 64 + lane < len;
         kr[r] = valid ? keys_in[i] : (K)0;
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kMaxRounds; r++) {
+    for (int r = 0; r < MAXR; r++) {
         if (r < rounds && wl + (uint32_t)r * 64 + lane < len) atomicAdd(&wcnt[w][((uint32_t)kr[r] >> shift) & mask], 1u);
     }
     __syncthreads();
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int r = 0; r < kMaxRounds; r++) {
+    for (int r = 0; r < MAXR; r++) {
         if (r >= rounds || wl + (uint32_t)r * 64 >= len) continue;  // wave-uniform; keeps the loop unrollable
         const bool valid = wl + (uint32_t)r * 64 + lane < len;
         const K k = kr[r];
@@ -370,11 +373,13 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
         if (!last && kdst == nullptr) return g_why = "no key storage", hipErrorInvalidValue;
         if (!(p == 0 && first_counts_ready)) {
             if (p == 0 && unit_len) return g_why = "sparse units need producer counts", hipErrorInvalidValue;
-            k_rs_count<K><<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev);
+            auto count = rounds <= 2 ? k_rs_count<K, 2> : rounds <= 4 ? k_rs_count<K, 4> : k_rs_count<K, kMaxRounds>;
+            count<<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev);
         }
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
-        k_rs_scatter<K><<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets,
-                                                       units, s.totals, p == 0 ? unit_len : nullptr, n_dev);
+        auto scatter = rounds <= 2 ? k_rs_scatter<K, 2> : rounds <= 4 ? k_rs_scatter<K, 4> : k_rs_scatter<K, kMaxRounds>;
+        scatter<<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets, units,
+                                               s.totals, p == 0 ? unit_len : nullptr, n_dev);
         ksrc = kdst;
         vsrc = vdst;
         shift += dbits;
