@@ -33,6 +33,11 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
     constexpr bool HALF = NW == 4;
     constexpr int PAIRS = HALF ? 1 : 2 / NW;  // pixel pairs per lane
     constexpr int B = 64 * NW;                // records per round
+#ifndef RR_FWD_GROUP
+#define RR_FWD_GROUP 4
+#endif
+    constexpr int kGroup = RR_FWD_GROUP;      // pairs whose alphas are formed together (8: neutral)
+    static_assert(B % kGroup == 0, "group size");
     const int ntiles = a.gx * a.gy;
     const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
@@ -127,14 +132,14 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
             if (AUX) nn = a.normals[id];
         }
         const int cnt = min(B, n - base);
-        for (int j0 = 0; j0 < cnt; j0 += 4) {
+        for (int j0 = 0; j0 < cnt; j0 += kGroup) {
             if (__all(all_closed())) break;
-            // groups of 4 pairs: the falloff / alpha of the 4 pairs (independent of T) are formed
+            // groups of kGroup pairs: the falloff / alpha of the group (independent of T) are formed
             // first, so their exp / compare chains overlap; only the blend below is sequential.
             // A slot past cnt (stale / uninitialised LDS, j < B still) is computed but never blended.
-            f2 alq[4][PAIRS];
+            f2 alq[kGroup][PAIRS];
 #pragma unroll
-            for (int uu = 0; uu < 4; uu++) {
+            for (int uu = 0; uu < kGroup; uu++) {
                 const int j = j0 + uu;
                 const float4 A = s_a[j];
                 const float4 Bv = s_b[j];
@@ -157,7 +162,7 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd(BlendFwdArgs a) {
                 }
             }
 #pragma unroll
-            for (int uu = 0; uu < 4; uu++) {
+            for (int uu = 0; uu < kGroup; uu++) {
             const int j = j0 + uu;
             if (j >= cnt) break;
             const float4 Bv = s_b[j];
