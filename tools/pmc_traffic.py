@@ -124,7 +124,7 @@ def main():
     fetch = _read(a.fetch_dir, "FETCH_SIZE")
     write = _read(a.write_dir, "WRITE_SIZE")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE over tools/pmc_workload.py "
-                     "(1M Gaussians, SH 3, 1920x1080, fwd+bwd); hbm = 2*FETCH + WRITE (gfx950 correction)",
+                     "(the bench training step: 1M Gaussians, SH 3, 1920x1080, fused Adam); hbm = 2*FETCH + WRITE (gfx950 correction)",
            "unit": "bytes per launch (median over launches)", "kernels": {}}
     for st in sorted(set(fetch) | set(write)):
         f = statistics.median(fetch[st]) * 1024.0 if st in fetch else None
