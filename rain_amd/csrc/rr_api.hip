@@ -109,6 +109,8 @@ struct Geom {
     uint32_t* idx_sorted;
     uint2* offsets;       // inclusive prefix sum of tiles[] in depth order; .y of the last = num_rendered
     float4* normals;      // RR_FLAG_AUX_NORMAL: view-space normal per visible Gaussian
+    uint2* block_sums;    // [ceil(P/256)] per-preprocess-block sums of tiles[] (pairs, rect tiles)
+    unsigned long long* totals;  // [2] their sums (device copy of what the mailbox publishes)
     void* temp;
     size_t temp_bytes;
     size_t total;
@@ -124,6 +126,8 @@ Geom carve_geom(void* buf, int P) {
     g.idx_sorted = c.take<uint32_t>(n);
     g.offsets = c.take<uint2>(n);
     g.normals = c.take<float4>(n);
+    g.block_sums = c.take<uint2>((n + 255) / 256);
+    g.totals = c.take<unsigned long long>(2);
     g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
@@ -295,10 +299,10 @@ int check(const rr_frame* f, hipStream_t st, const char* what) {
 
 // ---------------------------------------------------------------------------------------
 // Readback of the forward's pair counts.  A hipMemcpyAsync into pageable host memory + stream
-// synchronise costs a blit kernel and the runtime's blocking wait (measured 30-140 us of idle
-// GPU per frame between the scan and the binning launches).  Instead a one-lane kernel stores
-// the two counts and a sequence number into a coherent pinned host mailbox (system-scope release
-// store) and the host thread spins on the sequence number.  Every few thousand spins the stream
+// synchronise after the scan costs a blit kernel and the runtime's blocking wait (measured 30-140
+// us of idle GPU per frame before the binning launches).  Instead a one-lane kernel stores the two
+// counts and a sequence number into a coherent pinned host mailbox (system-scope release store)
+// and the host thread spins on the sequence number.  Every few thousand spins the stream
 // is queried: a launch / kernel error is reported, and a stream that went idle without the
 // sequence number becoming visible falls back to the plain copy.
 struct Mailbox {
@@ -309,15 +313,58 @@ struct Mailbox {
 };
 thread_local Mailbox g_mailbox;
 
-__global__ void k_publish_pair_counts(const uint2* __restrict__ src, uint32_t* box, uint32_t seq) {
-    const uint2 v = *src;
-    __hip_atomic_store(box + 0, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(box + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// src: the preprocess's per-block sums of {pairs, rect tiles}; one workgroup adds them in 64 bits
+// (fixed order), saturates to 32 bits (the host rejects anything above 2^31 anyway) and publishes.
+__global__ __launch_bounds__(1024) void k_publish_pair_counts(const uint2* __restrict__ src, int nb, uint32_t* box,
+                                                               uint32_t seq, unsigned long long* copy) {
+    __shared__ unsigned long long s_n[16], s_r[16];
+    unsigned long long n = 0, r = 0;
+    for (int i = threadIdx.x; i < nb; i += 1024) {
+        const uint2 v = src[i];
+        n += v.x;
+        r += v.y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        n += __shfl_xor(n, o);
+        r += __shfl_xor(r, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_n[threadIdx.x >> 6] = n;
+        s_r[threadIdx.x >> 6] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        n = r = 0;
+        for (int w = 0; w < 16; w++) {
+            n += s_n[w];
+            r += s_r[w];
+        }
+        const uint32_t x = n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
+        const uint32_t y = r > 0xffffffffull ? 0xffffffffu : (uint32_t)r;
+        copy[0] = x;  // device copy for the no-mailbox path
+        copy[1] = y;
+        if (box) {
+            __hip_atomic_store(box + 0, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
-hipError_t read_pair_counts(const uint2* src, uint2* out, hipStream_t st) {
+// The publish is enqueued right after the preprocess (whose block sums give the totals), so the
+// host learns the pair count while the depth sort and the scan still run, and has the binning
+// launches queued before the GPU gets to them.
+struct PairCountRead {
+    const unsigned long long* copy = nullptr;  // device {pairs, rect} for the copy path
+    uint32_t seq = 0;  // 0: no mailbox (copy + synchronise at wait time)
+};
+
+hipError_t pair_counts_publish(const uint2* block_sums, int nb, unsigned long long* copy, PairCountRead& r,
+                               hipStream_t st) {
     Mailbox& mb = g_mailbox;
+    r.copy = copy;
+    r.seq = 0;
     if (!mb.host && !mb.failed) {
         void* h = nullptr;
         if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
@@ -330,16 +377,25 @@ hipError_t read_pair_counts(const uint2* src, uint2* out, hipStream_t st) {
             mb.failed = true;
         }
     }
-    if (mb.failed) {
-        hipError_t e = hipMemcpyAsync(out, src, sizeof(uint2), hipMemcpyDeviceToHost, st);
-        return e == hipSuccess ? hipStreamSynchronize(st) : e;
-    }
-    const uint32_t seq = ++mb.seq == 0 ? ++mb.seq : mb.seq;  // 0 is the mailbox's initial value
-    k_publish_pair_counts<<<1, 1, 0, st>>>(src, mb.dev, seq);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (!mb.failed) r.seq = ++mb.seq == 0 ? ++mb.seq : mb.seq;  // 0 is the mailbox's initial value
+    k_publish_pair_counts<<<1, 1024, 0, st>>>(block_sums, nb, mb.failed ? nullptr : mb.dev, r.seq, copy);
+    return hipGetLastError();
+}
+
+hipError_t pair_counts_copy(const unsigned long long* src, uint2* out, hipStream_t st) {
+    unsigned long long v[2] = {0ull, 0ull};
+    hipError_t e = hipMemcpyAsync(v, src, sizeof(v), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    out->x = (uint32_t)v[0];
+    out->y = (uint32_t)v[1];
+    return e;
+}
+
+hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, hipStream_t st) {
+    Mailbox& mb = g_mailbox;
+    if (r.seq == 0) return pair_counts_copy(r.copy, out, st);
     for (uint32_t spin = 1;; spin++) {
-        if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == seq) {
+        if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) {
             out->x = __atomic_load_n(mb.host + 0, __ATOMIC_RELAXED);
             out->y = __atomic_load_n(mb.host + 1, __ATOMIC_RELAXED);
             return hipSuccess;
@@ -347,10 +403,9 @@ hipError_t read_pair_counts(const uint2* src, uint2* out, hipStream_t st) {
         if ((spin & 4095u) == 0) {
             const hipError_t q = hipStreamQuery(st);
             if (q == hipSuccess) {
-                if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == seq) continue;
+                if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) continue;
                 mb.failed = true;  // idle stream, value not visible: never use the mailbox again
-                e = hipMemcpyAsync(out, src, sizeof(uint2), hipMemcpyDeviceToHost, st);
-                return e == hipSuccess ? hipStreamSynchronize(st) : e;
+                return pair_counts_copy(r.copy, out, st);
             }
             if (q != hipErrorNotReady) return q;
         }
@@ -429,12 +484,15 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     a.raw = (f->flags & RR_FLAG_RAW_PARAMS) ? 1 : 0;
     a.shs_rest = g->shs_rest;
     a.normals = (f->flags & RR_FLAG_AUX_NORMAL) ? gm.normals : nullptr;
+    a.block_sums = gm.block_sums;
 
+    PairCountRead rd;
     {
         StageTimer tm(RR_STAGE_PREPROCESS, st);
         launch_preprocess(a, st);
     }
     RR_STAGE_CHECK("preprocess");
+    RR_CHECK(pair_counts_publish(gm.block_sums, (P + 255) / 256, gm.totals, rd, st), "publish pair counts");
     {
         StageTimer tm(RR_STAGE_DEPTH_SORT, st);
         size_t tb = gm.temp_bytes;
@@ -454,7 +512,7 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
     // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
     uint2 tot = make_uint2(0u, 0u);
-    RR_CHECK(read_pair_counts(gm.offsets + (P - 1), &tot, st), "read L");
+    RR_CHECK(pair_counts_wait(rd, &tot, st), "read L");
     if (tot.x > 0x7fffffffu || tot.y > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^31 tile/Gaussian pairs");
     *num_rendered = (int)tot.y;
     *num_pairs = (int)tot.x;
@@ -483,6 +541,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
             d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L = LA;
+            d.zero = reinterpret_cast<uint32_t*>(im.ranges); d.nzero = (int)(im.zero_bytes / sizeof(uint32_t));
             d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
             launch_duplicate<K>(d, st);
         }
@@ -517,6 +576,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         d.first = bn.first + pa.units; d.pair0 = LA; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units; d.L = L;
         d.keys = keys + LA; d.vals = bn.vals + LA; d.dbits = pb.dbits0; d.counts = pb.counts;
         d.sat = im.sat; d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
+        d.zero = nullptr; d.nzero = 0;
         launch_duplicate<K>(d, st);
     }
     RR_STAGE_CHECK("duplicate (phase B)");
@@ -573,7 +633,7 @@ int rr_forward_render_aux(const rr_frame* f, const rr_camera* cam, const rr_gaus
     hipStream_t st = (hipStream_t)stream;
     const int gx = grid_x(W), gy = grid_y(H);
     const bool early = L > 0 && bn.LA < bn.L && !(f->flags & RR_FLAG_FULL_BINNING);
-    {
+    if (L == 0 || bn.LA == 0) {  // otherwise the first duplicate launch clears them (DupArgs::zero)
         StageTimer tm(RR_STAGE_RANGES, st);
         RR_CHECK(hipMemsetAsync(im.ranges, 0, im.zero_bytes, st), "memset ranges");
     }

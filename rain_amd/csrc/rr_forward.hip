@@ -19,7 +19,7 @@ namespace rr {
 // No global atomics here: per-Gaussian counts go to tiles[idx] = {pairs, rect area} and are
 // prefix-summed in depth order (the rect-area sum is the reference's num_rendered).
 template <int DEG>
-__device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
+__device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
     a.radii[idx] = 0;
     a.tiles[idx] = make_uint2(0u, 0u);
     a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
@@ -29,7 +29,7 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     const v3 p_view = xform_point_4x3(p, a.view);
     if (p_view.z <= 0.2f) {
         if (a.prefiltered) __builtin_trap();
-        return;
+        return make_uint2(0u, 0u);
     }
     const float4 p_hom = xform_point_4x4(p, a.proj);
     const float p_w = 1.0f / (p_hom.w + 0.0000001f);
@@ -58,7 +58,7 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     cc += a.low_pass;
 
     const float det = ca * cc - cb * cb;
-    if (det == 0.0f) return;
+    if (det == 0.0f) return make_uint2(0u, 0u);
     const float det_inv = 1.f / det;
     const float cx = cc * det_inv, cy = -cb * det_inv, cz = ca * det_inv;
     const float mid = 0.5f * (ca + cc);
@@ -70,7 +70,7 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     int x0, y0, x1, y1;
     tile_rect(px, py, radius, a.gx, a.gy, x0, y0, x1, y1);
     const int area = (x1 - x0) * (y1 - y0);
-    if (area == 0) return;
+    if (area == 0) return make_uint2(0u, 0u);
 
     float4 rgb;
     if (a.colors_precomp) {
@@ -106,20 +106,40 @@ __device__ __forceinline__ void preprocess_one(const PreArgs& a, int idx) {
     }
     a.tiles[idx] = make_uint2(n, (uint32_t)area);
     a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
+    return make_uint2(n, (uint32_t)area);
 }
 
+// The block's sums of {pairs, rect tiles} go to a.block_sums[blockIdx.x] (plain stores; a single
+// contended 64-bit atomic per block measured +37 us on 1M Gaussians): the frame's pair count is
+// then known right after this kernel (rr_api.hip pair_counts_publish reduces them).
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx < a.P) preprocess_one<DEG>(a, idx);
+    const uint2 c = idx < a.P ? preprocess_one<DEG>(a, idx) : make_uint2(0u, 0u);
+    if (!a.block_sums) return;
+    __shared__ uint2 s_sum[4];
+    uint32_t n = c.x, r = c.y;  // per block <= 256 * T, below 2^32 for T < 2^24
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        n += (uint32_t)__shfl_xor((int)n, o);
+        r += (uint32_t)__shfl_xor((int)r, o);
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) s_sum[w] = make_uint2(n, r);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        a.block_sums[blockIdx.x] = make_uint2(s_sum[0].x + s_sum[1].x + s_sum[2].x + s_sum[3].x,
+                                              s_sum[0].y + s_sum[1].y + s_sum[2].y + s_sum[3].y);
 }
 
 // First Gaussian (depth rank) of every window of `win` consecutive pairs starting at pair0:
 // window k = [pair0 + k*win, pair0 + (k+1)*win) starts inside the pair range [a, b) of exactly
 // one Gaussian.
 __global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __restrict__ offsets, uint32_t pair0,
-                                                       uint32_t win, int nwin, uint32_t* __restrict__ first) {
+                                                       uint32_t win, int nwin, uint32_t* __restrict__ first,
+                                                       uint32_t* __restrict__ zero, int nzero) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int i = s; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0u;
     if (s >= P) return;
     const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
     if (a == b || b <= pair0) return;
@@ -363,8 +383,12 @@ void launch_preprocess(const PreArgs& a, hipStream_t st) {
 
 template <typename K>
 void launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
-    if (d.P == 0 || d.nwin == 0 || d.win > (uint32_t)kSortMaxUnit) return;  // win comes from radix_sort_plan
-    k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.P, d.offsets, d.pair0, d.win, d.nwin, d.first);
+    if (d.P == 0 || d.nwin == 0 || d.win > (uint32_t)kSortMaxUnit) {  // win comes from radix_sort_plan
+        if (d.zero && d.nzero > 0) (void)hipMemsetAsync(d.zero, 0, (size_t)d.nzero * sizeof(uint32_t), st);
+        return;
+    }
+    k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.P, d.offsets, d.pair0, d.win, d.nwin, d.first, d.zero,
+                                                     d.zero ? d.nzero : 0);
     auto kern = d.sat ? k_duplicate<K, true> : k_duplicate<K, false>;
     kern<<<d.nwin, 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
                                             d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts, d.nwin,

@@ -26,6 +26,7 @@ struct PreArgs {
     int raw;                     // RR_FLAG_RAW_PARAMS: apply the GaussianModel getters in-kernel
     const float* shs_rest;       // raw mode: f_rest [P,M-1,3] (shs = f_dc [P,1,3])
     float4* normals;             // RR_FLAG_AUX_NORMAL: view-space unit normal per visible Gaussian, else null
+    uint2* block_sums;           // optional [ceil(P/256)]: per-block sums of tiles[] (pairs, rect tiles)
 };
 
 // Early-stop binning (rr_api.hip): the tile lists are built in two phases.  Phase A bins the
@@ -128,6 +129,11 @@ struct DupArgs {
     const uint32_t* open_bits;
     uint32_t* unit_len;
     uint32_t* n_total;
+    // optional: words cleared by the window-starts kernel before the duplicate runs (the frame's
+    // tile ranges and counters; saves a memset launch on the path right after the pair-count
+    // readback)
+    uint32_t* zero;
+    int nzero;
 };
 template <typename K>
 void launch_duplicate(const DupArgs<K>& d, hipStream_t st);
