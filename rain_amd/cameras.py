@@ -75,7 +75,10 @@ class Camera:
     device: str = "cpu"
 
     def __post_init__(self):
-        self.world_view_transform = torch.tensor(getWorld2View2(self.R, self.T)).transpose(0, 1).to(self.device)
+        # transposed then made contiguous once: the kernels read the column-major W2C, and a strided
+        # view would cost a copy kernel in every render
+        self.world_view_transform = torch.tensor(getWorld2View2(self.R, self.T)).transpose(0, 1).contiguous().to(
+            self.device)
         self.projection_matrix = getProjectionMatrix(self.znear, self.zfar, self.FoVx, self.FoVy).transpose(0, 1).to(
             self.device)
         self.full_proj_transform = (self.world_view_transform.unsqueeze(0).bmm(

@@ -72,6 +72,17 @@ def _window_host():
     return _WINDOW
 
 
+_ONES = {}
+
+
+def _ones(device):
+    """A cached device scalar 1.0 (the default grad_loss; read-only for the kernels)."""
+    t = _ONES.get(device)
+    if t is None:
+        t = _ONES[device] = torch.ones((1,), dtype=torch.float32, device=device)
+    return t
+
+
 def l1_ssim_forward(img, gt, lambda_dssim):
     """Fused forward (include/rain_loss.h).  Returns (loss scalar, parts [3], workspace); the
     workspace carries the per-pixel SSIM derivative maps the backward needs."""
@@ -101,7 +112,7 @@ def l1_ssim_backward(img, gt, lambda_dssim, ws, grad_loss=None):
     C, H, W = img.shape[-3:]
     dimg = torch.empty_like(img)
     if grad_loss is None:
-        grad_loss = torch.ones((1,), dtype=torch.float32, device=img.device)
+        grad_loss = _ones(img.device)
     g = grad_loss.reshape(1).contiguous().float()
     rc = L.rl_l1_ssim_backward(img.data_ptr(), gt.data_ptr(), C, H, W, float(lambda_dssim), _window_host(),
                                ws.data_ptr(), g.data_ptr(), dimg.data_ptr(), N.stream_of(img))
