@@ -159,7 +159,10 @@ template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
-                            const uint32_t* n_dev = nullptr);
+                            const uint32_t* n_dev = nullptr, const uint2* gather_src = nullptr,
+                            uint2* gather_dst = nullptr);
+// gather_src / gather_dst (optional): the last pass also writes gather_dst[i] = gather_src[vals_out[i]]
+// (the depth sort hands the scan its {pairs, rect} in depth order, a contiguous array).
 const char* radix_sort_last_error();  // which check failed in the last radix_sort_pairs call
 // Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
 // can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass

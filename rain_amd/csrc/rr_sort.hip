@@ -148,7 +148,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
                                                             const uint32_t* __restrict__ offsets, int units,
                                                             const uint32_t* __restrict__ totals,
                                                             const uint32_t* __restrict__ unit_len,
-                                                            const uint32_t* __restrict__ n_dev) {
+                                                            const uint32_t* __restrict__ n_dev,
+                                                            const uint2* __restrict__ gather_src,
+                                                            uint2* __restrict__ gather_dst) {
     __shared__ uint32_t dbase[256];         // first output slot of each digit
     __shared__ uint32_t wcnt[kWaves][256];  // per-wave digit counts, then per-wave cursors
     __shared__ uint32_t dstart[256];        // block-local start of each digit's run
@@ -275,7 +277,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
         const uint32_t d = ((uint32_t)k >> shift) & mask;
         const uint32_t pos = goff[d] + (uint32_t)j;
         if (keys_out) keys_out[pos] = k;
-        vals_out[pos] = s_val[j];
+        const uint32_t v = s_val[j];
+        vals_out[pos] = v;
+        if (gather_dst) gather_dst[pos] = gather_src[v];
     }
 }
 
@@ -348,7 +352,8 @@ const char* radix_sort_last_error() { return g_why; }
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
-                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev) {
+                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev,
+                            const uint2* gather_src, uint2* gather_dst) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
     g_why = "";
@@ -379,7 +384,8 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
         auto scatter = rounds <= 2 ? k_rs_scatter<K, 2> : rounds <= 4 ? k_rs_scatter<K, 4> : k_rs_scatter<K, kMaxRounds>;
         scatter<<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets, units,
-                                               s.totals, p == 0 ? unit_len : nullptr, n_dev);
+                                               s.totals, p == 0 ? unit_len : nullptr, n_dev,
+                                               last ? gather_src : nullptr, last ? gather_dst : nullptr);
         ksrc = kdst;
         vsrc = vdst;
         shift += dbits;
@@ -393,10 +399,10 @@ template size_t radix_sort_temp_bytes<uint16_t>(size_t, int);
 template size_t radix_sort_temp_bytes<uint32_t>(size_t, int);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*);
+                                               const uint32_t*, const uint2*, uint2*);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*);
+                                               const uint32_t*, const uint2*, uint2*);
 template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int);
 template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int);
 
