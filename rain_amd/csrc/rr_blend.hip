@@ -295,6 +295,7 @@ int set_tuning(const char* key, int value) {
     else if (k == "fwd_b_waves") g_fwd_b_waves = value ? 4 : 0;
     else if (k == "fwd_waves") g_fwd_waves = value;
     else if (k == "bwd_waves") g_bwd_waves = value;
+    else if (k == "sort_min_units") set_sort_min_units(value);
     else return 1;
     return 0;
 }

@@ -163,7 +163,8 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                             uint2* gather_dst = nullptr);
 // gather_src / gather_dst (optional): the last pass also writes gather_dst[i] = gather_src[vals_out[i]]
 // (the depth sort hands the scan its {pairs, rect} in depth order, a contiguous array).
-const char* radix_sort_last_error();  // which check failed in the last radix_sort_pairs call
+const char* radix_sort_last_error();
+void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)  // which check failed in the last radix_sort_pairs call
 // Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
 // can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass
 // first_counts_ready = true).

@@ -292,10 +292,14 @@ struct SortLayout {
     size_t total;
 };
 
-// rounds per wave: full 16 for large inputs, fewer for small ones so that there are >= ~1024 units
+// rounds per wave: full 16 for large inputs, fewer for small ones so that there are >= ~g_min_units
+// units (rr_set_tuning "sort_min_units"; interleaved A/B on the bench step: 512 beat 1024 by 1.7%,
+// the 1M-key depth sort then runs 1024-item units)
+constexpr int kMinUnitsDefault = 512;
+int g_min_units = kMinUnitsDefault;
 int rounds_for(size_t n) {
     int r = kMaxRounds;
-    while (r > 1 && (n + (size_t)64 * kWaves * r - 1) / ((size_t)64 * kWaves * r) < 1024) r >>= 1;
+    while (r > 1 && (n + (size_t)64 * kWaves * r - 1) / ((size_t)64 * kWaves * r) < (size_t)g_min_units) r >>= 1;
     return r;
 }
 
@@ -345,6 +349,8 @@ RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
     p.counts = s.counts;
     return p;
 }
+
+void set_sort_min_units(int units) { g_min_units = units > 0 ? units : kMinUnitsDefault; }
 
 thread_local const char* g_why = "";
 const char* radix_sort_last_error() { return g_why; }

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--knob", default=None, help="native tuning key toggled 0/1 instead (rr_set_tuning)")
     ap.add_argument("--split", default=None,
                     help="comma-separated early-stop split denominators to compare (rr_set_binning_config)")
+    ap.add_argument("--values", default=None, help="comma-separated integer values of --knob to compare (default 0,1)")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--points", type=int, default=1_000_000)
@@ -54,7 +55,8 @@ def main():
     for _ in range(10):
         tr.step(it)
         it += 1
-    arms = [int(x) for x in a.split.split(",")] if a.split else [False, True]
+    arms = ([int(x) for x in a.split.split(",")] if a.split else
+            [int(x) for x in a.values.split(",")] if a.values else [False, True])
     res = {v: [] for v in arms}
     for b in range(len(arms) * a.blocks):
         val = arms[b % len(arms)]
