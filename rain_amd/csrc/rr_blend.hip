@@ -296,6 +296,7 @@ int set_tuning(const char* key, int value) {
     else if (k == "fwd_waves") g_fwd_waves = value;
     else if (k == "bwd_waves") g_bwd_waves = value;
     else if (k == "sort_min_units") set_sort_min_units(value);
+    else if (k == "sort_max_rounds") set_sort_max_rounds(value);
     else return 1;
     return 0;
 }

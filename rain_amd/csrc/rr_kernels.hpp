@@ -164,7 +164,8 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
 // gather_src / gather_dst (optional): the last pass also writes gather_dst[i] = gather_src[vals_out[i]]
 // (the depth sort hands the scan its {pairs, rect} in depth order, a contiguous array).
 const char* radix_sort_last_error();
-void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)  // which check failed in the last radix_sort_pairs call
+void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
+void set_sort_max_rounds(int r);     // rounds cap per wave (tuning; 0 = default 16)  // which check failed in the last radix_sort_pairs call
 // Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
 // can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass
 // first_counts_ready = true).

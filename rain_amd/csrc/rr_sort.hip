@@ -297,8 +297,9 @@ struct SortLayout {
 // the 1M-key depth sort then runs 1024-item units)
 constexpr int kMinUnitsDefault = 512;
 int g_min_units = kMinUnitsDefault;
+int g_max_rounds = kMaxRounds;  // rr_set_tuning "sort_max_rounds" (power of two <= 16)
 int rounds_for(size_t n) {
-    int r = kMaxRounds;
+    int r = g_max_rounds;
     while (r > 1 && (n + (size_t)64 * kWaves * r - 1) / ((size_t)64 * kWaves * r) < (size_t)g_min_units) r >>= 1;
     return r;
 }
@@ -351,6 +352,7 @@ RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
 }
 
 void set_sort_min_units(int units) { g_min_units = units > 0 ? units : kMinUnitsDefault; }
+void set_sort_max_rounds(int r) { g_max_rounds = (r == 1 || r == 2 || r == 4 || r == 8) ? r : kMaxRounds; }
 
 thread_local const char* g_why = "";
 const char* radix_sort_last_error() { return g_why; }
