@@ -149,7 +149,8 @@ __global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __res
 
 // 2-D inclusive prefix sum of the open-tile flags (phase B's per-Gaussian rectangle test):
 // sat[(y + 1) * (gx + 1) + (x + 1)] = open tiles in [0, x] x [0, y].  One workgroup; rows are
-// scanned by waves (64 tiles per step), then columns by threads, in LDS when the table fits.
+// scanned by waves (64 tiles per step), then columns by threads in row chunks, in LDS when the
+// table fits.
 constexpr int kSatLds = 16384;  // u32 entries of LDS (64 KiB): up to ~128 x 127 tiles
 template <bool LDS>
 __global__ __launch_bounds__(1024) void k_open_sat(int gx, int gy, const uint8_t* __restrict__ open,
@@ -159,13 +160,14 @@ __global__ __launch_bounds__(1024) void k_open_sat(int gx, int gy, const uint8_t
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int sw = gx + 1;
     const int nt = gx * gy;
-    for (int i = t; i < (nt + 31) / 32; i += 1024) {  // the same flags as a bitmask
-        uint32_t m = 0;
-        for (int b = 0; b < 32; b++) {
-            const int tile = 32 * i + b;
-            m |= (tile < nt && open[tile]) ? (1u << b) : 0u;
+    const int nwords = (nt + 31) / 32;
+    for (int base = 64 * w; base < nt; base += 1024) {  // the same flags as a bitmask (one ballot per 64)
+        const int tile = base + lane;
+        const uint64_t m = __ballot(tile < nt && open[tile] != 0);
+        if (lane == 0) {
+            open_bits[base / 32] = (uint32_t)m;
+            if (base / 32 + 1 < nwords) open_bits[base / 32 + 1] = (uint32_t)(m >> 32);
         }
-        open_bits[i] = m;
     }
     for (int x = t; x < sw; x += 1024) tab[x] = 0;
     for (int y = w; y < gy; y += 16) {  // rows: one wave per row
@@ -184,11 +186,30 @@ __global__ __launch_bounds__(1024) void k_open_sat(int gx, int gy, const uint8_t
         }
     }
     __syncthreads();
-    for (int x = t; x < gx; x += 1024) {  // columns
+    // columns: each column split into nch row chunks (one thread each), chunk-local prefix sums,
+    // then every chunk adds the totals of the chunks above it (a 68-row serial chain -> ~2 x 9)
+    __shared__ uint32_t ctot[1024];
+    const int nch = gx >= 1024 ? 1 : min(1024 / gx, gy);
+    const int rpc = (gy + nch - 1) / nch;
+    for (int i = t; i < gx * nch; i += 1024) {
+        const int x = i % gx, c = i / gx;
+        const int y1 = min(gy, (c + 1) * rpc);
         uint32_t run = 0;
-        for (int y = 0; y < gy; y++) {
+        for (int y = c * rpc; y < y1; y++) {
             run += tab[(y + 1) * sw + x + 1];
             tab[(y + 1) * sw + x + 1] = run;
+        }
+        if (nch > 1) ctot[i] = run;
+    }
+    if (nch > 1) {
+        __syncthreads();
+        for (int i = t; i < gx * nch; i += 1024) {
+            const int x = i % gx, c = i / gx;
+            uint32_t add = 0;
+            for (int cc = 0; cc < c; cc++) add += ctot[cc * gx + x];
+            const int y1 = min(gy, (c + 1) * rpc);
+            if (add)
+                for (int y = c * rpc; y < y1; y++) tab[(y + 1) * sw + x + 1] += add;
         }
     }
     if (LDS) {
