@@ -269,8 +269,11 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *                         env RAIN_BWD_TILE_ORDER),
  *   "fwd_tile_order" 0/1  forward blends dispatch tiles longest list first (default 0;
  *                         env RAIN_FWD_TILE_ORDER),
- *   "fwd_waves" / "bwd_waves" as rr_set_blend_config.
- * Unknown keys return RR_ERR_ARG. */
+ *   "fwd_waves" / "bwd_waves" as rr_set_blend_config,
+ *   "fwd_b_waves"    0/1  phase-B forward blend on 4 waves per tile (default 1),
+ *   "sort_min_units" n    radix sorts pick the largest unit with >= n units (default 512; 0 resets),
+ *   "sort_max_rounds" r   cap on 64-item rounds per wave in a sort unit, 1..16 (default 16).
+ * Results are identical for every setting.  Unknown keys return RR_ERR_ARG. */
 int rr_set_tuning(const char* key, int value);
 
 /* Tuning knob (diagnostics / tests): early-stop binning bins L / split_denominator pairs in phase A
