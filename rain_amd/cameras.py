@@ -83,7 +83,7 @@ class Camera:
             self.device)
         self.full_proj_transform = (self.world_view_transform.unsqueeze(0).bmm(
             self.projection_matrix.unsqueeze(0))).squeeze(0)
-        self.camera_center = self.world_view_transform.inverse()[3, :3]
+        self.camera_center = self.world_view_transform.inverse()[3, :3].contiguous()
 
     def to(self, device):
         return Camera(self.R, self.T, self.FoVx, self.FoVy, self.image_width, self.image_height, self.uid,
