@@ -1,7 +1,7 @@
 """Training loss (utils/loss_utils.py:6-53): loss = (1-λ)·L1 + λ·(1-SSIM), 11x11 Gaussian window σ=1.5.
 
-``ssim`` follows the reference exactly (depthwise 11x11 conv2d) and is the test reference.
-``fused_l1_ssim_loss`` is what the train step uses: the whole loss and its gradient in two HIP
+The reference's own ``ssim`` (depthwise 11x11 conv2d) is restated as test infrastructure in
+oracle/loss_ref.py.  ``fused_l1_ssim_loss`` is what the train step uses: the whole loss and its gradient in two HIP
 kernels (rain_amd/csrc/loss.hip) — the window is an outer product of the 1-D Gaussian
 (loss_utils.py:15-19), so it is applied as two 11-tap passes over an LDS tile.  ``ssim_separable``
 is the same factorisation in torch (a CPU-testable statement of what the kernel computes).  All are
@@ -16,46 +16,14 @@ import torch
 import torch.nn.functional as F
 
 
-def l1_loss(network_output, gt):
-    return torch.abs((network_output - gt)).mean()
-
-
-def l2_loss(network_output, gt):
-    return ((network_output - gt) ** 2).mean()
-
-
-def gaussian(window_size, sigma):
-    gauss = torch.Tensor([exp(-(x - window_size // 2) ** 2 / float(2 * sigma ** 2)) for x in range(window_size)])
-    return gauss / gauss.sum()
-
-
-def create_window(window_size, channel):
-    _1D_window = gaussian(window_size, 1.5).unsqueeze(1)
-    _2D_window = _1D_window.mm(_1D_window.t()).float().unsqueeze(0).unsqueeze(0)
-    return _2D_window.expand(channel, 1, window_size, window_size).contiguous()
-
-
-def ssim(img1, img2, window_size=11, size_average=True):
-    channel = img1.size(-3)
-    window = create_window(window_size, channel).to(img1.device).type_as(img1)
-    return _ssim(img1, img2, window, window_size, channel, size_average)
-
-
-def _ssim(img1, img2, window, window_size, channel, size_average=True):
-    mu1 = F.conv2d(img1, window, padding=window_size // 2, groups=channel)
-    mu2 = F.conv2d(img2, window, padding=window_size // 2, groups=channel)
-    mu1_sq = mu1.pow(2)
-    mu2_sq = mu2.pow(2)
-    mu1_mu2 = mu1 * mu2
-    sigma1_sq = F.conv2d(img1 * img1, window, padding=window_size // 2, groups=channel) - mu1_sq
-    sigma2_sq = F.conv2d(img2 * img2, window, padding=window_size // 2, groups=channel) - mu2_sq
-    sigma12 = F.conv2d(img1 * img2, window, padding=window_size // 2, groups=channel) - mu1_mu2
-    C1 = 0.01 ** 2
-    C2 = 0.03 ** 2
-    ssim_map = ((2 * mu1_mu2 + C1) * (2 * sigma12 + C2)) / ((mu1_sq + mu2_sq + C1) * (sigma1_sq + sigma2_sq + C2))
-    if size_average:
-        return ssim_map.mean()
-    return ssim_map.mean(1).mean(1).mean(1)
+def window_1d(window_size: int = 11, sigma: float = 1.5) -> torch.Tensor:
+    """The loss's 1-D Gaussian window (utils/loss_utils.py:15-17): exp(-(x - size//2)² / 2σ²)
+    evaluated in double, stored as fp32 and normalised by its fp32 sum — the same fp32 weights the
+    reference convolves with (pinned by tests/golden/loss.npz)."""
+    c = window_size // 2
+    w = torch.tensor([exp(-((i - c) ** 2) / (2.0 * sigma * sigma)) for i in range(window_size)],
+                     dtype=torch.float32)
+    return w / w.sum()
 
 
 _WINDOW = None
@@ -67,7 +35,7 @@ def _window_host():
     if _WINDOW is None:
         import ctypes
 
-        g = gaussian(11, 1.5)
+        g = window_1d(11, 1.5)
         _WINDOW = (ctypes.c_float * 11)(*[float(v) for v in g])
     return _WINDOW
 
@@ -149,7 +117,7 @@ def fused_l1_ssim_loss(img, gt, lambda_dssim=0.2):
 
 @lru_cache(maxsize=8)
 def _sep_windows(window_size, channels, device, dtype):
-    g = gaussian(window_size, 1.5).to(device=device, dtype=dtype)
+    g = window_1d(window_size, 1.5).to(device=device, dtype=dtype)
     return (g.view(1, 1, 1, window_size).expand(channels, 1, 1, window_size).contiguous(),
             g.view(1, 1, window_size, 1).expand(channels, 1, window_size, 1).contiguous())
 

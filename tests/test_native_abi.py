@@ -108,6 +108,24 @@ def test_import_shim_is_the_product():
     assert shim._C is _C
 
 
+def test_reference_import_path_resolves_to_the_product():
+    """gaussian_renderer/__init__.py:5 imports exactly this dotted path; the reference package's
+    `from ..setup import _C` (diff_gaussian_rasterization/__init__.py:4) resolves too."""
+    import importlib
+
+    m = importlib.import_module("submodules.diff_gaussian_rasterization.diff_gaussian_rasterization")
+    from submodules.diff_gaussian_rasterization.diff_gaussian_rasterization import (
+        GaussianRasterizationSettings as S, GaussianRasterizer as R)
+    from submodules.diff_gaussian_rasterization.setup import _C as setup_C
+
+    from rain_amd.diff_gaussian_rasterization import GaussianRasterizationSettings, rasterize_gaussians
+
+    assert R is GaussianRasterizer and S is GaussianRasterizationSettings
+    assert m.rasterize_gaussians is rasterize_gaussians and m._C is _C and setup_C is _C
+    assert S._fields == ("image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix",
+                         "projmatrix", "sh_degree", "campos", "prefiltered", "debug", "low_pass")
+
+
 def test_simple_knn_shim_and_no_cpu_fallback():
     import simple_knn
     from simple_knn._C import distCUDA2

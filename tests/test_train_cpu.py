@@ -13,7 +13,7 @@ import torch.multiprocessing as mp
 import rain_amd.diff_gaussian_rasterization as dgr
 from rain_amd import cameras, synthetic
 from rain_amd.gaussian_model import GaussianModel, OptimizationParams
-from rain_amd.loss import l1_loss, ssim
+from oracle.loss_ref import l1_loss, ssim
 from rain_amd.renderer import PipelineParams, render
 from rain_amd.train import TrainConfig, Trainer
 from tests import oracle_c
