@@ -70,6 +70,8 @@ def lib():
         L.orc_sh_eval.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
         L.orc_pixel_blend_list.restype = ctypes.c_int
         L.orc_pixel_blend_list.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _u32p, ctypes.c_int]
+        L.orc_cov3d.restype = None
+        L.orc_cov3d.argtypes = [ctypes.c_int, _f32p, ctypes.c_float, _f32p, _f32p]
         L.orc_dist_knn3.restype = None
         L.orc_dist_knn3.argtypes = [ctypes.c_int, _f32p, _f32p, ctypes.POINTER(ctypes.c_uint32), _f32p]
         _lib = L
@@ -248,6 +250,15 @@ def sh_eval(deg, shs, dirs):
     cl = np.zeros((n, 3), np.uint8)
     lib().orc_sh_eval(int(deg), M, n, _p(d), _p(shs), _p(out), _p(cl, _u8p))
     return out, cl.astype(bool)
+
+
+def cov3d(scales, scale_modifier, rotations):
+    """Sigma3D (xx, xy, xz, yy, yz, zz) per Gaussian, computeCov3D (forward.cu:107-141)."""
+    s = _f32(scales)
+    r = _f32(rotations)
+    out = np.zeros((s.shape[0], 6), np.float32)
+    lib().orc_cov3d(s.shape[0], _p(s), float(scale_modifier), _p(r), _p(out))
+    return out
 
 
 def get_higher_msb(n: int) -> int:

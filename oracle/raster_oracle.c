@@ -129,6 +129,11 @@ static void compute_cov3d(const float* scale, float mod, const float* rot, float
     cov3D[3] = Sg[1][1]; cov3D[4] = Sg[1][2]; cov3D[5] = Sg[2][2];
 }
 
+/* Exported for the golden test (tests/test_golden.py): Sigma3D of n Gaussians, 6 floats each. */
+void orc_cov3d(int n, const float* scales, float mod, const float* rots, float* out) {
+    for (int i = 0; i < n; i++) compute_cov3d(scales + 3 * (size_t)i, mod, rots + 4 * (size_t)i, out + 6 * (size_t)i);
+}
+
 /* Auxiliary normal (BASELINE configs[4] "depth+normal aux outputs"; the reference renders no
  * normals, so this follows the build's own definition in include/rain_raster.h RR_FLAG_AUX_NORMAL):
  * the world axis of the smallest scale (column k of Rs), rotated into view space by R_w2c

@@ -46,6 +46,49 @@ class TrainConfig:
     densify: bool = True
 
 
+class Exchange:
+    """The step's collectives over `group`, independent of the backend.
+
+    RCCL (backend "nccl") runs them on the HIP tensors directly.  Other backends (gloo: the
+    multi-process CPU tests, and the 2-rank-on-one-GPU test) do not implement every collective for
+    device tensors, so the tensors are staged through host memory and the gradient reduce-scatter
+    becomes an all-reduce + local slice — the same sums (elementwise, rank order), so the step's
+    arithmetic does not depend on the backend."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.direct = dist.get_backend(group) == "nccl"
+
+    def reduce_scatter_sum(self, out: torch.Tensor, inp: torch.Tensor):
+        """out <- slice `rank` of the elementwise SUM over ranks of inp (inp.numel() = world * out.numel())."""
+        if self.direct:
+            dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group)
+            return
+        h = inp.detach().to("cpu", copy=True)
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+        S = out.numel()
+        out.copy_(h[self.rank * S:(self.rank + 1) * S])
+
+    def all_gather_inplace(self, buf: torch.Tensor, lo: int, S: int):
+        """Every rank contributes buf[lo:lo+S] (lo = rank*S); afterwards buf holds all slices."""
+        if self.direct:
+            dist.all_gather_into_tensor(buf, buf[lo:lo + S], group=self.group)
+            return
+        out = torch.empty(buf.numel(), dtype=buf.dtype)
+        dist.all_gather_into_tensor(out, buf[lo:lo + S].to("cpu", copy=True), group=self.group)
+        buf.copy_(out)
+
+    def all_reduce(self, t: torch.Tensor, op):
+        if self.direct or t.device.type == "cpu":
+            dist.all_reduce(t, op=op, group=self.group)
+            return
+        h = t.to("cpu", copy=True)
+        dist.all_reduce(h, op=op, group=self.group)
+        t.copy_(h)
+
+
 class ViewSampler:
     """Shared permutation of camera indices; rank r takes the r-th of each group of N."""
 
@@ -89,6 +132,7 @@ class Trainer:
         self.loss_fn = loss_fn or (lambda img, gt, lam: fused_l1_ssim_loss(img, gt, lam)[0])
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.exchange = Exchange(group) if self.world > 1 else None
         self.sampler = ViewSampler(len(cameras), self.world, self.cfg.seed)
         dev = gaussians.device
         self.background = torch.tensor([1, 1, 1] if self.cfg.white_background else [0, 0, 0], dtype=torch.float32,
@@ -219,18 +263,18 @@ class Trainer:
             if iteration < opt.iterations:
                 if self._shard is None or self._shard.numel() != S or self._shard.device != flat.device:
                     self._shard = torch.empty(S, dtype=flat.dtype, device=flat.device)
-                dist.reduce_scatter_tensor(self._shard, flat[:n], op=dist.ReduceOp.SUM, group=self.group)
+                self.exchange.reduce_scatter_sum(self._shard, flat[:n])
                 sharded_adam_step(g.optimizer, g.params(), _offs, self._shard, lo, 1.0 / self.world)
-                dist.all_gather_into_tensor(fp, fp[lo:lo + S], group=self.group)
+                self.exchange.all_gather_inplace(fp, lo, S)
                 for p in g.params():
                     p.grad = None
             return False
-        dist.all_gather_into_tensor(fm, fm[lo:lo + S], group=self.group)
-        dist.all_gather_into_tensor(fv, fv[lo:lo + S], group=self.group)
+        self.exchange.all_gather_inplace(fm, lo, S)
+        self.exchange.all_gather_inplace(fv, lo, S)
         if densify_now:
             self.sync_densify_stats()
         elif iteration < opt.iterations:
-            dist.all_reduce(flat[:n], op=dist.ReduceOp.SUM, group=self.group)
+            self.exchange.all_reduce(flat[:n], dist.ReduceOp.SUM)
             flat[:n].mul_(1.0 / self.world)
         return self._densify_and_adam(iteration)
 
@@ -241,9 +285,9 @@ class Trainer:
         (densify), or on copies."""
         g = self.g
         if self.world > 1:
-            dist.all_reduce(g.xyz_gradient_accum, op=dist.ReduceOp.SUM, group=self.group)
-            dist.all_reduce(g.denom, op=dist.ReduceOp.SUM, group=self.group)
-            dist.all_reduce(g.max_radii2D, op=dist.ReduceOp.MAX, group=self.group)
+            self.exchange.all_reduce(g.xyz_gradient_accum, dist.ReduceOp.SUM)
+            self.exchange.all_reduce(g.denom, dist.ReduceOp.SUM)
+            self.exchange.all_reduce(g.max_radii2D, dist.ReduceOp.MAX)
 
     def _step_autograd(self, iteration: int, sync_loss: bool = False) -> StepInfo:
         """The reference-API step: render() through GaussianRasterizer + autograd (train.py:109-147)."""

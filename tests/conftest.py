@@ -27,3 +27,12 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Multi-process GPU tests spawn their ranks before this process initialises the GPU: run them
+    first in the session."""
+    first = [it for it in items if "test_multirank_gpu" in it.nodeid]
+    if first:
+        rest = [it for it in items if "test_multirank_gpu" not in it.nodeid]
+        items[:] = first + rest

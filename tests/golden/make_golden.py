@@ -9,6 +9,13 @@ Pins the pieces of the hot path whose reference implementation runs on CPU:
                    scene/cameras.py:108-111 matrix assembly for synthetic cameras (the kernels' inputs)
   loss.npz         utils/loss_utils.py l1_loss / ssim values and gradients (train.py:113-114)
   lr.npz           utils/general_utils.py get_expon_lr_func (train-step xyz LR schedule)
+  cov3d.npz        utils/general_utils.py build_rotation / build_scaling_rotation / strip_symmetric composed
+                   as scene/gaussian_model.py:16-20 (build_covariance_from_scaling_rotation): Sigma3D, the
+                   compute_cov3D_python path (gaussian_renderer/__init__.py:44-48) and the quantity
+                   computeCov3D (forward.cu:107-141, F4 step 4) builds in-kernel; plus inverse_sigmoid (:7-8)
+                   and the getters' activations (torch.exp, F.normalize, torch.sigmoid) on the same inputs.
+                   Those helpers hard-code device="cuda", so they run with a module-scoped CPU view of
+                   `torch` (CpuTorch below) — the reference's arithmetic, on the CPU.
 
 The fixtures are data (inputs + outputs); no reference source is copied.
 Run:  python tests/golden/make_golden.py
@@ -23,6 +30,18 @@ import torch
 sys.dont_write_bytecode = True
 REF = os.environ.get("RAIN_REFERENCE", "/root/reference")
 HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class CpuTorch:
+    """Stand-in for the `torch` global of ONE reference module: every attribute is torch's own,
+    except that tensor factories ignore `device` (the reference asks for "cuda"; none exists here)."""
+
+    def __getattr__(self, name):
+        return getattr(torch, name)
+
+    @staticmethod
+    def zeros(*shape, device=None, **kw):
+        return torch.zeros(*shape, **kw)
 
 
 def main():
@@ -94,6 +113,27 @@ def main():
         out[f"loss_{i}"] = np.array([float(loss)])
         out[f"grad_{i}"] = x.grad.numpy()
     np.savez_compressed(os.path.join(HERE, "loss.npz"), **out)
+
+    # ---- Sigma3D / activations ----
+    general_utils.torch = CpuTorch()  # module-scoped: only general_utils sees the CPU view
+    out = {}
+    n = 1024
+    raw_scaling = torch.from_numpy(rng.normal(-3.0, 0.8, (n, 3)).astype(np.float32))
+    raw_rotation = torch.from_numpy(rng.standard_normal((n, 4)).astype(np.float32) * 1.7)
+    raw_opacity = torch.from_numpy(rng.normal(0.0, 2.0, (n, 1)).astype(np.float32))
+    scales = torch.exp(raw_scaling)                            # scaling_activation
+    rot_unit = torch.nn.functional.normalize(raw_rotation)     # rotation_activation
+    out["raw_scaling"], out["raw_rotation"], out["raw_opacity"] = (raw_scaling.numpy(), raw_rotation.numpy(),
+                                                                    raw_opacity.numpy())
+    out["scales"], out["rot_unit"] = scales.numpy(), rot_unit.numpy()
+    out["opacity"] = torch.sigmoid(raw_opacity).numpy()
+    out["inverse_sigmoid"] = general_utils.inverse_sigmoid(torch.sigmoid(raw_opacity)).numpy()
+    out["rotation_matrix"] = general_utils.build_rotation(raw_rotation).numpy()
+    for tag, mod in (("m1", 1.0), ("m07", 0.7)):
+        for rtag, rot in (("raw", raw_rotation), ("unit", rot_unit)):
+            L = general_utils.build_scaling_rotation(mod * scales, rot)
+            out[f"cov_{tag}_{rtag}"] = general_utils.strip_symmetric(L @ L.transpose(1, 2)).numpy()
+    np.savez_compressed(os.path.join(HERE, "cov3d.npz"), **out)
 
     # ---- lr schedule ----
     f = general_utils.get_expon_lr_func(lr_init=0.00016 * 4.4, lr_final=0.0000016 * 4.4, lr_delay_mult=0.01,

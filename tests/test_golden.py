@@ -72,3 +72,38 @@ def test_lr_schedule_matches_reference():
     f = gaussian_model.get_expon_lr_func(lr_init=0.00016 * 4.4, lr_final=0.0000016 * 4.4, lr_delay_mult=0.01,
                                          max_steps=30000)
     np.testing.assert_array_equal(np.array([f(int(s)) for s in d["steps"]]), d["lr"])
+
+
+def _cov_close(got, want, rel=4e-6):
+    """Sigma3D entries within `rel` of each Gaussian's largest variance (float32 rounding of a
+    different but equivalent evaluation order: glm's M^T M vs torch's (R S)(R S)^T)."""
+    scale = np.abs(want[:, [0, 3, 5]]).max(axis=1, keepdims=True)
+    err = np.abs(got.astype(np.float64) - want) / scale
+    assert err.max() <= rel, err.max()
+
+
+def test_oracle_cov3d_matches_reference(oracle):
+    """computeCov3D as restated in raster_oracle.c (forward.cu:107-141, fed the getters' unit
+    quaternions as render() does) == the reference's build_scaling_rotation / strip_symmetric
+    composition (gaussian_model.py:16-20) on the same scales, rotations and scale modifiers."""
+    d = _load("cov3d.npz")
+    for tag, mod in (("m1", 1.0), ("m07", 0.7)):
+        _cov_close(oracle.cov3d(d["scales"], mod, d["rot_unit"]), d[f"cov_{tag}_unit"])
+        # the Python path normalises raw quaternions itself: same Sigma as the unit ones
+        _cov_close(d[f"cov_{tag}_raw"].astype(np.float32), d[f"cov_{tag}_unit"])
+
+
+def test_host_getters_and_covariance_match_reference():
+    """rain_amd.gaussian_model's restatements (the compute_cov3D_python path and the getters)."""
+    d = _load("cov3d.npz")
+    s, r = torch.from_numpy(d["scales"]), torch.from_numpy(d["raw_rotation"])
+    np.testing.assert_array_equal(gaussian_model.build_rotation(r).numpy(), d["rotation_matrix"])
+    for tag, mod in (("m1", 1.0), ("m07", 0.7)):
+        L = gaussian_model.build_scaling_rotation(mod * s, r)
+        np.testing.assert_array_equal(gaussian_model.strip_symmetric(L @ L.transpose(1, 2)).numpy(),
+                                      d[f"cov_{tag}_raw"])
+    op = torch.from_numpy(d["raw_opacity"])
+    np.testing.assert_array_equal(torch.sigmoid(op).numpy(), d["opacity"])
+    np.testing.assert_array_equal(gaussian_model.inverse_sigmoid(torch.sigmoid(op)).numpy(), d["inverse_sigmoid"])
+    np.testing.assert_array_equal(torch.nn.functional.normalize(r).numpy(), d["rot_unit"])
+    np.testing.assert_array_equal(torch.exp(torch.from_numpy(d["raw_scaling"])).numpy(), d["scales"])

@@ -205,3 +205,27 @@ def test_cfg2_parity(oracle, gpu, P, W, H):
     got = gpu_run(inp, st, gpu, dL_dpix=dpix)
     _check_forward(ref, got)
     _check_grads(ref, got)
+
+
+@pytest.mark.parametrize("tag,mod", [("m1", 1.0), ("m07", 0.7)])
+def test_hip_cov3d_is_the_reference_sigma(gpu, tag, mod):
+    """F4 step 4 pinned to the reference: the HIP preprocess's Sigma3D built from (scale_modifier *
+    scale, rotation) renders the same frame as the reference's own Sigma3D
+    (tests/golden/cov3d.npz: build_scaling_rotation / strip_symmetric, gaussian_model.py:16-20)
+    passed as cov3D_precomp — same radii, same image and means3D gradient within float rounding."""
+    import os
+
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cov3d.npz"))
+    n = d["scales"].shape[0]
+    inp, st = make_scene(P=n, W=128, H=96, sh_degree=3, scale_modifier=mod)
+    inp["scales"] = torch.from_numpy(d["scales"])
+    inp["rotations"] = torch.from_numpy(d["rot_unit"])
+    dpix = _dpix(st)
+    a = gpu_run(inp, st, gpu, dL_dpix=dpix)
+    pre = {k: v for k, v in inp.items() if k not in ("scales", "rotations")}
+    pre["cov3D_precomp"] = torch.from_numpy(d[f"cov_{tag}_unit"])
+    b = gpu_run(pre, st, gpu, dL_dpix=dpix)
+    assert (a["radii"] != b["radii"]).mean() <= 2e-3
+    assert a["num_rendered"] > 0
+    assert rel_l1(a["color"], b["color"]) <= 1e-5
+    assert rel_l1(a["grads"]["dL_dmeans3D"], b["grads"]["dL_dmeans3D"]) <= 1e-4
