@@ -190,6 +190,10 @@ def main():
     # loss.backward()): render forward + L1/SSIM + backward, no optimizer step, no densification
     bracket_ms = _bracket(trainer, cams, gts, K if K < 50 else 50, world, dev)
 
+    # the same iteration through the reference's own API (what an unchanged train.py:109-147 runs):
+    # render() -> GaussianRasterizer autograd -> getters' autograd -> torch.optim.Adam
+    api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, end_iter + 1, K if K < 30 else 30, world, dev)
+
     # forward-only throughput (preprocess -> blend incl. sorts and the L read-back), no autograd
     Pn = gauss.get_xyz.shape[0]
     with torch.no_grad():
@@ -253,6 +257,16 @@ def main():
             b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2)
             if b is not None:
                 kernels[k]["algorithmic_GBps"] = round(b / (kernels[k]["ms_per_step"] * 1e-3) / 1e9, 1)
+        # north_star states its roofline target on the per-tile blend: both blends' HBM fractions
+        # (event-timed in the profiled window) and VALU-issue fractions (committed SQ pass)
+        headline = (P, W, H) == (1_000_000, 1920, 1080)
+        for k in ("blend_fwd", "blend_bwd"):
+            if k in kernels and "algorithmic_GBps" in kernels[k]:
+                roofline[k] = {"ms_per_step": round(kernels[k]["ms_per_step"], 5),
+                               "achieved_GBps": kernels[k]["algorithmic_GBps"],
+                               "frac": round(kernels[k]["algorithmic_GBps"] / HBM_PEAK_GBS, 4),
+                               "traffic": _pmc_traffic(k) if headline else None,
+                               "valu_issue_frac": _pmc_field(k, "valu_issue_frac") if headline else None}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -282,6 +296,10 @@ def main():
         "views_per_s": round(iters_per_s, 3),  # one view per rank per step: = value
         "bracket_iters_per_s": round(world * 1000.0 / bracket_ms, 3),
         "bracket_ms": round(bracket_ms, 4),
+        "api_iters_per_s": round(world * 1000.0 / api_ms, 3),
+        "api_ms_per_step": round(api_ms, 4),
+        "api_path": "render() -> GaussianRasterizer (autograd) -> GaussianModel getters (autograd) -> HIP L1+SSIM "
+                    "(autograd) -> torch.optim.Adam (foreach); no densify event in the window",
         "gaussians_after": int(Pn),
         "frame_stats": {k: int(v) for k, v in mean_stats.items()},
         "roofline": roofline,
@@ -338,23 +356,102 @@ def _bracket(trainer, cams, gts, n, world, dev):
     return 1000.0 * t / n
 
 
+def _api_leg(gauss, cams, gts, opt, pipe, extent, it0, n, world, dev):
+    """ms per train iteration on the reference-API path (Trainer(fused=False)): the stock
+    torch.optim.Adam the reference builds (gaussian_model.py:153), state carried over from the
+    fused run.  Iterations it0.. (it0 = 1 + a multiple of 100: no densify / reset inside)."""
+    import torch
+    import torch.distributed as dist
+
+    from rain_amd.train import TrainConfig, Trainer
+
+    fused_opt = gauss.optimizer
+    groups = [{"params": g["params"], "lr": g["lr"], "name": g["name"]} for g in fused_opt.param_groups]
+    adam = torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+    for g in fused_opt.param_groups:
+        p = g["params"][0]
+        if p in fused_opt.state and len(fused_opt.state[p]):
+            st = fused_opt.state[p]
+            adam.state[p] = {"step": st["step"].detach().clone().cpu().float().reshape(()),
+                             "exp_avg": st["exp_avg"].detach().clone(), "exp_avg_sq": st["exp_avg_sq"].detach().clone()}
+    gauss.optimizer = adam
+    tr = Trainer(gauss, cams, gts, opt, pipe, TrainConfig(seed=1), scene_extent=extent, fused=False)
+    it = it0
+    for _ in range(3):
+        tr.step(it)
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        tr.step(it)
+        it += 1
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    gauss.optimizer = fused_opt
+    if world > 1:
+        e = torch.tensor([t], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        t = float(e.item())
+    return 1000.0 * t / n
+
+
 def _copy_peak(dev):
-    """Measured device-to-device copy bandwidth (read + write bytes / time), 1 GiB buffers."""
+    """Achievable HBM rate: read + write bytes / time of the library's float4 streaming copy
+    (rt_stream_copy, the MI355X guide's ~6.3 TB/s yardstick), 1 GiB buffers, HIP events on the
+    stream the copy is launched on."""
     import torch
 
+    from rain_amd import _native
+
+    L = _native.train_lib()
     a = torch.empty(1 << 28, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
-    for _ in range(2):
-        b.copy_(a)
+    st = _native.stream_of(a)
+
+    def copy():
+        if L.rt_stream_copy(b.data_ptr(), a.data_ptr(), a.numel() * 4, st) != 0:
+            raise RuntimeError(L.rt_last_error().decode())
+
+    for _ in range(3):
+        copy()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(10):
-        b.copy_(a)
+        copy()
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 10
     del a, b
     return round(2 * (1 << 30) / (ms * 1e-3) / 1e9, 1)
+
+
+def _host_cpus():
+    """(threads the CPU baseline may use, description of the host): every CPU this process is
+    allowed to run on, capped by a cgroup CPU quota when one is set (the GPU box gives each GPU a
+    16-CPU share of a larger machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    use = min(aff, quota) if quota else aff
+    return use, {"host_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                 "cpu_model": model}
 
 
 def _settings(cam, gauss, bg):
@@ -392,7 +489,8 @@ def _cpu_baseline(gauss, cam, bg, D, threads, views=3):
     from oracle import oracle as O
 
     O.build()
-    nthr = threads or min(16, os.cpu_count() or 1)
+    avail, host = _host_cpus()
+    nthr = threads or avail
     with torch.no_grad():
         s = _settings(cam, gauss, bg)
         m = gauss.get_xyz.detach().float().cpu().numpy()
@@ -418,7 +516,7 @@ def _cpu_baseline(gauss, cam, bg, D, threads, views=3):
             "kind": "port",
             "sample": f"{views} x 1 full {s.image_width}x{s.image_height} view, {m.shape[0]} Gaussians, SH {D}: forward "
                       f"{tf / views:.2f}s + backward {tb / views:.2f}s per view (rasterizer only; loss/Adam not included)",
-            "forward_mpix_per_s": round(views * s.image_width * s.image_height / tf / 1e6, 4)}
+            "forward_mpix_per_s": round(views * s.image_width * s.image_height / tf / 1e6, 4), **host}
 
 
 if __name__ == "__main__":

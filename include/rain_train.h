@@ -100,6 +100,12 @@ int rt_densify_apply(const rt_densify_params* p, const float* scaling, const flo
                      const void* workspace, const rt_densify_group* groups, int n_groups, const int64_t counts[4],
                      void* stream);
 
+/* Streaming device-to-device copy of n_bytes (multiple of 16; both pointers 16-B aligned): 16-B
+ * loads/stores per lane, grid sized to fill every CU several times.  Not on the training path: it
+ * is the achievable-HBM yardstick bench.py prices the HBM-bound kernels against (the guide's
+ * float4 copy, ~6.3 TB/s read + write on MI355X). */
+int rt_stream_copy(void* dst, const void* src, size_t n_bytes, void* stream);
+
 const char* rt_last_error(void);
 
 #ifdef __cplusplus

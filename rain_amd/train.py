@@ -289,6 +289,16 @@ class Trainer:
             self.exchange.all_reduce(g.denom, dist.ReduceOp.SUM)
             self.exchange.all_reduce(g.max_radii2D, dist.ReduceOp.MAX)
 
+    def sync_optimizer_state(self):
+        """All-gather the Adam moments: on ordinary sharded iterations each rank advances only its
+        1/N slice of exp_avg / exp_avg_sq, so call this before reading or checkpointing the full
+        optimizer state (GaussianModel.capture, train.py:148-150).  Parameters are always full."""
+        if self.world > 1:
+            _fp, fm, fv, _offs, n = self.g.pack_flat_state(self.world)
+            S = n // self.world
+            self.exchange.all_gather_inplace(fm, self.rank * S, S)
+            self.exchange.all_gather_inplace(fv, self.rank * S, S)
+
     def _step_autograd(self, iteration: int, sync_loss: bool = False) -> StepInfo:
         """The reference-API step: render() through GaussianRasterizer + autograd (train.py:109-147)."""
         g, opt = self.g, self.opt

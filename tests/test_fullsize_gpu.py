@@ -31,6 +31,10 @@ def _scene(P, W, H, dev, seed=0, cam_index=0):
     """Bench-shaped scene: parameters generated on the device (HIP k-NN scales), then the
     activated tensors on the CPU for the oracle and the raw ones for the fused path."""
     raw = synthetic.random_gaussians(P, sh_degree=3, seed=seed, bench=True, device=dev)
+    # anisotropic scales (as training leaves them): the k-NN init is isotropic, where dL/drotation
+    # is analytically zero and both sides are rounding noise (relative L1 meaningless)
+    g = torch.Generator().manual_seed(seed + 100)
+    raw["scaling"] = (raw["scaling"] + 0.3 * torch.randn(raw["scaling"].shape, generator=g).to(dev)).contiguous()
     act = synthetic.activated(raw)
     inp = {"means3D": act["means3D"], "opacities": act["opacities"], "shs": act["shs"], "scales": act["scales"],
            "rotations": act["rotations"]}

@@ -70,6 +70,7 @@ def _worker(rank, world, port, out_path):
     assert tr.fused and tr.world == world
     flags = [tr.step(it).densified for it in ITERS]
     tr.sync_densify_stats()  # merge what accumulated since the last densify
+    tr.sync_optimizer_state()  # iteration 7 advanced only this rank's slice of the moments
     torch.cuda.synchronize()
     torch.save(_snapshot(g, flags), f"{out_path}.{rank}")
     torch.distributed.barrier()
