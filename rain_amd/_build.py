@@ -24,7 +24,7 @@ CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-W
             "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 LIBS = {
-    "librain_raster.so": ["rr_forward.hip", "rr_blend_fwd.hip", "rr_blend.hip", "rr_backward.hip", "rr_sort.hip",
+    "librain_raster.so": ["rr_forward.hip", "rr_blend_fwd.hip", "rr_blend_fwd_s.hip", "rr_blend.hip", "rr_backward.hip", "rr_sort.hip",
                           "rr_api.hip"],
     "librain_loss.so": ["loss.hip"],
     "librain_knn.so": ["knn.hip"],
@@ -39,6 +39,7 @@ LIBS = {
 # larger than clang's default pragma-unroll size limit; packed-fp32 formation is off for the same
 # reason as rr_blend.hip (it pairs unrelated scalars: 940 v_mov, 244 VGPRs in k_ssim_fwd).
 EXTRA = {
+    "rr_blend_fwd_s.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
     "rr_blend.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
     "loss.hip": ["-mllvm", "-pragma-unroll-threshold=200000",
                  "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],

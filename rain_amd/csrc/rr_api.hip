@@ -206,7 +206,7 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     b.LA = early_split(b.L);
     const uint32_t LB = b.L - b.LA;
     const size_t n = (size_t)std::max(L, 1);
-    b.point_list = c.take<uint32_t>(n);
+    b.point_list = c.take<uint32_t>(n + kPointListPad);
     if (b.wide) {
         b.keys = c.take<uint32_t>(n);
         b.keys_sorted = c.take<uint32_t>(n);

@@ -1,0 +1,253 @@
+// rr_blend_fwd_s.hip — per-tile front-to-back alpha blend, forward (forward.cu:251-369), scalar-
+// record / scalar-arithmetic variant.
+//
+// Measured on MI355X (tools/valu_probe.hip, profiles/r02_*): the forward blend is VALU-throughput
+// bound (SQ_ACTIVE_INST_VALU ~0.8 of SIMD cycles), and a packed fp32 op (v_pk_fma_f32, 2 lanes of
+// work) costs ~2x a plain v_fma_f32 — packing buys no throughput and its operand shuffles (v_mov
+// of scalars into register pairs) cost ~14% of the loop.  So this kernel is written for the
+// scalar VALU with as few vector instructions per (pixel, pair) as the reference's arithmetic
+// allows:
+//   * every lane of a wave blends the same pair at the same time, so the pair's id and 48-B Splat
+//     are wave-uniform: they are read with s_load through the constant address space and feed the
+//     VALU ops as scalar operands (no LDS staging, no broadcast VGPRs, no barrier per round);
+//   * a lane owns PIX pixels of one column (rows l/16 + 4k): the x-terms of the falloff are
+//     computed once per lane and pair;
+//   * no per-pixel "open" flag: a saturated pixel keeps -T (T >= 1e-4 > 0 while open), so every
+//     later pair finds T*(1 - alpha) < 1e-4, re-saturates and changes nothing (wgt = 0, T kept by
+//     one select with a -|x| source modifier); the masks of the compares combine on the scalar unit;
+//   * a pixel row k whose 16 x 4 pixels are all closed (or that no lane reaches with alpha >=
+//     1/255) skips the pair's blend with a uniform branch; a wave leaves when all its pixels closed.
+// The arithmetic (blend_power's op order, explicit fmas, T*(1-alpha), wgt = alpha*T) is the packed
+// kernel's, element for element, so the two produce bitwise-identical images and image state.
+#include "rr_common.hpp"
+#include "rr_kernels.hpp"
+
+namespace rr {
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(4))) const v4f cv4f_s;
+typedef __attribute__((address_space(4))) const uint32_t cu32_s;
+typedef __attribute__((address_space(4))) const u2v cu2v_s;
+
+// NW waves per 16x16 tile, PIX = 4/NW pixels per lane: lane l of wave w owns column l%16 and rows
+// l/16 + 4*(w*PIX + k), k < PIX.  G pairs per group (their alphas formed before the blend).
+template <int NW, bool AUX>
+__global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
+#pragma clang fp contract(off)  // blend_power's rounding: every fma below is explicit
+    constexpr int PIX = 4 / NW;
+    constexpr int G = 4;
+    const int ntiles = a.gx * a.gy;
+    const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
+    if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
+    const int tx = tile % a.gx, ty = tile / a.gx;
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int px = tx * TILE_X + (lane & 15);
+    const float pfx = (float)px;
+    const size_t HW = (size_t)a.H * a.W;
+
+    int py[PIX];
+    float pfy[PIX], T[PIX], C0[PIX], C1[PIX], C2[PIX], Dp[PIX], N0[PIX], N1[PIX], N2[PIX];
+    uint32_t last[PIX];
+    bool inside[PIX];
+#pragma unroll
+    for (int k = 0; k < PIX; k++) {
+        py[k] = ty * TILE_Y + (lane >> 4) + 4 * (w * PIX + k);
+        pfy[k] = (float)py[k];
+        inside[k] = px < a.W && py[k] < a.H;
+        T[k] = inside[k] ? 1.f : -1.f;  // T < 0: closed (pixels outside the image start closed)
+        C0[k] = C1[k] = C2[k] = Dp[k] = N0[k] = N1[k] = N2[k] = 0.f;
+        last[k] = 0;
+    }
+    const u2v r0 = ((cu2v_s*)a.ranges)[tile];
+    uint32_t lo = r0.x, hi = r0.y;
+    uint32_t koff = 0;  // contributor index of the list's first pair
+    if (a.phase == kBlendPhaseB) {
+        // resume from the state phase A left for this open tile, then walk the phase-B list
+        koff = hi - lo;
+        const u2v rb = ((cu2v_s*)a.ranges_b)[tile];
+        lo = rb.x;
+        hi = rb.y;
+#pragma unroll
+        for (int k = 0; k < PIX; k++) {
+            if (inside[k]) {
+                const int pix = a.W * py[k] + px;
+                const uint32_t nc = a.n_contrib[pix];
+                T[k] = (nc & kDoneBit) ? -a.final_T[pix] : a.final_T[pix];
+                C0[k] = a.out_color[pix];
+                C1[k] = a.out_color[HW + pix];
+                C2[k] = a.out_color[2 * HW + pix];
+                Dp[k] = a.out_depth[pix];
+                if (AUX) {
+                    N0[k] = a.out_normal[pix];
+                    N1[k] = a.out_normal[HW + pix];
+                    N2[k] = a.out_normal[2 * HW + pix];
+                }
+                last[k] = nc & ~kDoneBit;
+            }
+        }
+    }
+    const int n = (int)(hi - lo);
+    cu32_s* plist = (cu32_s*)a.point_list + lo;  // readable kPointListPad entries past any list end
+    cv4f_s* recs = (cv4f_s*)a.splats;
+    cv4f_s* nrm = (cv4f_s*)a.normals;
+
+    for (int j0 = 0; j0 < n; j0 += G) {
+        bool open[PIX];  // as of the group's start (only used to skip work)
+        uint64_t any_open = 0;
+#pragma unroll
+        for (int k = 0; k < PIX; k++) {
+            open[k] = T[k] > 0.f;
+            any_open |= __builtin_amdgcn_ballot_w64(T[k] > 0.f);
+        }
+        if (!any_open) break;  // every pixel of this wave saturated
+        uint32_t id[G];
+#pragma unroll
+        for (int u = 0; u < G; u++) id[u] = plist[j0 + u];
+#pragma unroll
+        for (int u = 1; u < G; u++) id[u] = (j0 + u < n) ? id[u] : id[0];
+        v4f ra[G], rb[G], rc[G], rn[G];
+#pragma unroll
+        for (int u = 0; u < G; u++) {
+            ra[u] = recs[3 * id[u]];      // x, y, conic.x, conic.y
+            rb[u] = recs[3 * id[u] + 1];  // conic.z, opacity, depth
+            rc[u] = recs[3 * id[u] + 2];  // r, g, b
+            if (AUX) rn[u] = nrm[id[u]];
+        }
+        // alphas of the group (independent of T): forward.cu:329-336 with blend_power's op order
+        float al[G][PIX];
+        bool ok[G][PIX];
+        uint64_t okm[G][PIX];  // ok as a wave mask (ballots of the compares themselves: v_cmp into SGPRs)
+#pragma unroll
+        for (int u = 0; u < G; u++) {
+            const float dx = ra[u].x - pfx;
+            const float cxdx2 = (ra[u].z * dx) * dx;
+            const float wdx = ra[u].w * dx;
+#pragma unroll
+            for (int k = 0; k < PIX; k++) {
+                const float dy = ra[u].y - pfy[k];
+                const float tq = __builtin_fmaf(rb[u].x * dy, dy, cxdx2);
+                const float power = __builtin_fmaf(-0.5f, tq, -(wdx * dy));
+                const float g = __builtin_amdgcn_exp2f(power * kLog2e);
+                const float a99 = fminf(0.99f, rb[u].y * g);
+                // non-short-circuit: both compares become lane masks combined on the scalar unit
+                ok[u][k] = (power <= 0.0f) & (a99 >= 1.0f / 255.0f) & open[k];
+                okm[u][k] = __builtin_amdgcn_ballot_w64(power <= 0.0f) & __builtin_amdgcn_ballot_w64(a99 >= 1.0f / 255.0f) &
+                            __builtin_amdgcn_ballot_w64(open[k]);
+                al[u][k] = a99;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < G; u++) {
+            if (j0 + u >= n) break;
+            const uint32_t k1 = koff + (uint32_t)(j0 + u + 1);
+#pragma unroll
+            for (int k = 0; k < PIX; k++) {
+                if (!okm[u][k]) continue;  // this pixel row: nothing to blend
+                const float alpha = ok[u][k] ? al[u][k] : 0.f;
+                const float testT = T[k] * (1.f - alpha);
+                // forward.cu:337-341: saturation closes the pixel without blending this Gaussian
+                // (a closed pixel, T < 0, always lands here)
+                const bool sat = testT < 0.0001f;
+                const bool blend = ok[u][k] & !sat;
+                const float wgt = sat ? 0.f : alpha * T[k];
+                C0[k] = __builtin_fmaf(rc[u].x, wgt, C0[k]);
+                C1[k] = __builtin_fmaf(rc[u].y, wgt, C1[k]);
+                C2[k] = __builtin_fmaf(rc[u].z, wgt, C2[k]);
+                Dp[k] = __builtin_fmaf(rb[u].z, wgt, Dp[k]);
+                if (AUX) {
+                    N0[k] = __builtin_fmaf(rn[u].x, wgt, N0[k]);
+                    N1[k] = __builtin_fmaf(rn[u].y, wgt, N1[k]);
+                    N2[k] = __builtin_fmaf(rn[u].z, wgt, N2[k]);
+                }
+                T[k] = sat ? -fabsf(T[k]) : testT;
+                last[k] = blend ? k1 : last[k];
+            }
+        }
+    }
+
+    if (a.phase == kBlendPhaseA) {
+        // still open somewhere in the tile: leave the raw state (no background) for phase B
+        bool any_open = false;
+#pragma unroll
+        for (int k = 0; k < PIX; k++) any_open |= T[k] > 0.f;
+        const bool tile_open = NW == 1 ? __builtin_amdgcn_ballot_w64(any_open) != 0
+                                       : __syncthreads_or(any_open) != 0;
+        if (threadIdx.x == 0) a.open[tile] = tile_open ? 1 : 0;
+        if (tile_open) {
+#pragma unroll
+            for (int k = 0; k < PIX; k++) {
+                if (px < a.W && py[k] < a.H) {
+                    const int pix = a.W * py[k] + px;
+                    a.final_T[pix] = fabsf(T[k]);
+                    a.n_contrib[pix] = last[k] | (T[k] > 0.f ? 0u : kDoneBit);
+                    a.out_color[pix] = C0[k];
+                    a.out_color[HW + pix] = C1[k];
+                    a.out_color[2 * HW + pix] = C2[k];
+                    a.out_depth[pix] = Dp[k];
+                    if (AUX) {
+                        a.out_normal[pix] = N0[k];
+                        a.out_normal[HW + pix] = N1[k];
+                        a.out_normal[2 * HW + pix] = N2[k];
+                    }
+                }
+            }
+            return;
+        }
+    }
+    const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < PIX; k++) {
+        if (px < a.W && py[k] < a.H) {
+            m = max(m, last[k]);
+            const int pix = a.W * py[k] + px;
+            const float Tk = fabsf(T[k]);
+            a.final_T[pix] = Tk;
+            a.n_contrib[pix] = last[k];
+            a.out_color[pix] = C0[k] + Tk * bg0;
+            a.out_color[HW + pix] = C1[k] + Tk * bg1;
+            a.out_color[2 * HW + pix] = C2[k] + Tk * bg2;
+            a.out_depth[pix] = Dp[k];
+            if (AUX) {
+                a.out_normal[pix] = N0[k];
+                a.out_normal[HW + pix] = N1[k];
+                a.out_normal[2 * HW + pix] = N2[k];
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if (NW == 1) {
+        if (lane == 0) a.tile_max[tile] = m;
+    } else {
+        __shared__ uint32_t s_m[NW];
+        if (lane == 0) s_m[w] = m;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t mm = s_m[0];
+#pragma unroll
+            for (int i = 1; i < NW; i++) mm = max(mm, s_m[i]);
+            a.tile_max[tile] = mm;
+        }
+    }
+}
+
+void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st) {
+    const int T = a.gx * a.gy;
+    if (T == 0) return;
+    const bool aux = a.out_normal != nullptr;
+    if (waves == 1) {
+        if (aux) k_blend_fwd_s<1, true><<<T, 64, 0, st>>>(a);
+        else k_blend_fwd_s<1, false><<<T, 64, 0, st>>>(a);
+    } else if (waves == 4) {
+        if (aux) k_blend_fwd_s<4, true><<<T, 256, 0, st>>>(a);
+        else k_blend_fwd_s<4, false><<<T, 256, 0, st>>>(a);
+    } else {
+        if (aux) k_blend_fwd_s<2, true><<<T, 128, 0, st>>>(a);
+        else k_blend_fwd_s<2, false><<<T, 128, 0, st>>>(a);
+    }
+}
+
+}  // namespace rr

@@ -148,6 +148,9 @@ void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);
 // Largest sort unit (items per workgroup) of rr_sort.hip; the duplicate kernel's LDS windows are
 // sort units, so it sizes its staging arrays with this too.
 constexpr int kSortMaxUnit = 4096;
+// point_list is followed by at least this many readable u32 (the scalar-record forward blend loads
+// the ids of a whole group, up to 8, before masking the ones past its list's end)
+constexpr int kPointListPad = 16;
 
 // rr_sort.hip: stable LSD radix sort of (K key, u32 value) pairs on bits [begin_bit, end_bit).
 // vals_in == nullptr means values = input index.  keys_out may be nullptr only for a single pass.
@@ -186,6 +189,11 @@ int blend_fwd_waves();    // 1 or 2 (forward blend, rr_blend_fwd.hip)
 int blend_fwd_b_waves();  // phase B of early-stop binning: 4 (one pixel per lane) or as phase A
 bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_set_tuning "bwd_tile_order")
 bool fwd_tile_order();  // forward blends dispatch tiles longest list first (rr_set_tuning "fwd_tile_order")
+// forward blend implementation (rr_set_tuning "fwd_impl"): 0 packed fp32 + LDS-staged records,
+// 1 packed fp32 + scalar-loaded records, 2 scalar fp32 + scalar-loaded records (rr_blend_fwd_s.hip)
+int blend_fwd_impl();
+int blend_fwd_s_waves(bool phase_b);  // waves per tile of impl 2 ("fwd_s_waves" / "fwd_s_b_waves")
+void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
 }  // namespace rr

@@ -4,7 +4,8 @@ frame of the same model and camera.
 
 Bar: the oracle and the GPU agree to ~1e-6 per pixel, so an 8-bit encoding can differ only where a
 value sits within that of a rounding boundary: at most 1 level, on at most 0.1 % of the samples.
-The inferno image is compared the same way (its colormap lookup quantises depth to 256 bins)."""
+The inferno image may differ where depth crosses one of the colormap's 256 bins: by one LUT
+step (a few levels per channel), on the same small share of samples."""
 import os
 
 import numpy as np
@@ -29,11 +30,11 @@ def _u8(x):
     return np.clip(x * 255.0 + 0.5, 0, 255).astype(np.uint8).transpose(1, 2, 0)
 
 
-def _close_u8(a, b, what):
+def _close_u8(a, b, what, max_level=1):
     a, b = np.asarray(a).astype(np.int32), np.asarray(b).astype(np.int32)
     assert a.shape == b.shape, (what, a.shape, b.shape)
     d = np.abs(a - b)
-    assert d.max() <= 1, f"{what}: max level difference {d.max()}"
+    assert d.max() <= max_level, f"{what}: max level difference {d.max()}"
     assert (d > 0).mean() <= 1e-3, f"{what}: {(d > 0).mean():.2e} of samples differ"
 
 
@@ -62,5 +63,6 @@ def test_render_set_pngs_match_oracle_frames(oracle, gpu, tmp_path):
         dep = depth.reshape(1, H, W).astype(np.float32)
         dn = (dep - dep.min()) / (dep.max() - dep.min() + np.float32(1e-6))
         _close_u8(np.asarray(Image.open(base + "_depth.png")), _u8(dn), "normalised depth")
-        _close_u8(np.asarray(Image.open(base + "_depth_inferno.png")), depth_inferno(dep[0]), "inferno depth")
+        _close_u8(np.asarray(Image.open(base + "_depth_inferno.png")), depth_inferno(dep[0]), "inferno depth",
+                  max_level=5)  # largest step between adjacent inferno LUT entries
         _close_u8(np.asarray(Image.open(base + "_normal.png")), _u8(nmap.reshape(3, H, W) * 0.5 + 0.5), "normal map")

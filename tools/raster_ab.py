@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--low-pass", type=float, default=0.3)
+    ap.add_argument("--knob", default=None, help="compare values of a native tuning key (rr_set_tuning) instead")
+    ap.add_argument("--values", default="0,1", help="with --knob: comma-separated values")
     args = ap.parse_args()
 
     import torch
@@ -39,13 +41,18 @@ def main():
     L = _native.raster()
     from rain_amd.diff_gaussian_rasterization import _C
 
-    cfgs = [tuple(int(x) for x in (c.split(":") + ["1"])[:3]) for c in args.configs.split(",")]
+    if args.knob:
+        cfgs = [(0, 0, 1, int(v)) for v in args.values.split(",")]
+    else:
+        cfgs = [tuple(int(x) for x in (c.split(":") + ["1"])[:3]) for c in args.configs.split(",")]
     times = {c: {} for c in cfgs}
     outs = {}
     for r in range(args.rounds):
         for c in cfgs:
             L.rr_set_blend_config(c[0], c[1])
             _C.TILE_CULLING = bool(c[2])
+            if args.knob:
+                _native.check(L.rr_set_tuning(args.knob.encode(), c[3]), "tuning")
             L.rr_profile_enable(1)
             _native.Profiler.collect()
             for vi, cam in enumerate(cams):
@@ -72,7 +79,7 @@ def main():
         o = outs[c]
         same_img = bool(torch.equal(o[0], base[0]))
         rel = lambda a, b: float((a - b).abs().sum() / b.abs().sum().clamp_min(1e-30))  # noqa: E731
-        res[f"{c[0]}:{c[1]}:{c[2]}"] = {"stages_ms": {k: round(statistics.median(v), 4) for k, v in times[c].items()},
+        res[f"{args.knob}={c[3]}" if args.knob else f"{c[0]}:{c[1]}:{c[2]}"] = {"stages_ms": {k: round(statistics.median(v), 4) for k, v in times[c].items()},
                                  "image_bitwise_equal": same_img, "dmeans3D_relL1": rel(o[1], base[1]),
                                  "dsh_relL1": rel(o[2], base[2])}
     print(json.dumps(res, indent=1))
