@@ -14,7 +14,8 @@ import torch  # noqa: F401  (must be loaded before the HIP library; see module d
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_PKG, "lib")
-RASTER_LIB = os.path.join(LIB_DIR, "librain_raster.so")
+# RAIN_RASTER_LIB: an alternative build of the same library (tools/build_variant.py A/B builds)
+RASTER_LIB = os.environ.get("RAIN_RASTER_LIB") or os.path.join(LIB_DIR, "librain_raster.so")
 KNN_LIB = os.path.join(LIB_DIR, "librain_knn.so")
 KNN_SYMBOLS = ["sk_workspace_bytes", "sk_dist_cuda2", "sk_last_error"]
 

@@ -36,7 +36,10 @@ template <int NW, bool AUX>
 __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
 #pragma clang fp contract(off)  // blend_power's rounding: every fma below is explicit
     constexpr int PIX = 4 / NW;
-    constexpr int G = 4;
+#ifndef RR_FWD_S_GROUP
+#define RR_FWD_S_GROUP 4
+#endif
+    constexpr int G = RR_FWD_S_GROUP;
     const int ntiles = a.gx * a.gy;
     const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
