@@ -25,6 +25,10 @@
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
+#ifndef RR_BWD_FOLD
+#define RR_BWD_FOLD 1
+#endif
+
 namespace rr {
 
 // OCC: minimum waves per SIMD requested from the register allocator (4 caps k_blend_bwd<1> at
@@ -108,9 +112,20 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             const float4 Bv = s_b[j];
             float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
             bool any = false;
+#if RR_BWD_FOLD
+            // The conic-side terms are linear in u = G * dL/dalpha, and a lane's PPL pixels share
+            // its column (dx): per pixel only S_u, S_u.dy, S_u.dy^2 are accumulated, and the six
+            // components follow once per lane and pair (g0 = o dx S_u, g1 = o S_udy, g2 = dx g0,
+            // g3 = dx g1, g4 = o S_udy2, g5 = S_u with o the opacity): 5 VALU per pixel instead of 11.
+            const float dx = A.x - pfx;
+            float su = 0.f, sudy = 0.f, sudy2 = 0.f;
+#endif
 #pragma unroll
             for (int q = 0; q < PPL; q++) {
-                const float dx = A.x - pfx, dy = A.y - (float)(py0 + 4 * q);
+#if !RR_BWD_FOLD
+                const float dx = A.x - pfx;
+#endif
+                const float dy = A.y - (float)(py0 + 4 * q);
                 const float power = blend_power(A, Bv, dx, dy);  // identical to the forward's value
                 const float G = blend_G(power);
                 const float alpha = fminf(0.99f, Bv.y * G);
@@ -126,11 +141,22 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     g6 += dchannel_dcolor * dp0[q];
                     g7 += dchannel_dcolor * dp1[q];
                     g8 += dchannel_dcolor * dp2[q];
+#if RR_BWD_FOLD
+                    R[q] = __builtin_fmaf(la[q], lcdp[q] - R[q], R[q]);  // la lcdp + (1 - la) R
+#else
                     R[q] = la[q] * lcdp[q] + (1.f - la[q]) * R[q];
+#endif
                     lcdp[q] = cdp;
                     la[q] = alpha;
                     // dL/dalpha = T_i (c - accum_rec) . dL/dpix - T_final (bg . dL/dpix) / (1 - alpha)
                     const float dL_dalpha = (cdp - R[q]) * T[q] + tfbg[q] * inv;
+#if RR_BWD_FOLD
+                    const float u = G * dL_dalpha;
+                    const float udy = u * dy;
+                    su += u;
+                    sudy += udy;
+                    sudy2 = __builtin_fmaf(udy, dy, sudy2);
+#else
                     const float dL_dG = Bv.y * dL_dalpha;
                     // dG/d(delta) = -G (conic . delta): the conic is the same for every pixel of
                     // the pair, so only Sx = sum dL_dG G dx and Sy = sum dL_dG G dy are summed per
@@ -143,8 +169,20 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     g3 += tx * dy;
                     g4 += ty * dy;
                     g5 += G * dL_dalpha;
+#endif
                 }
             }
+#if RR_BWD_FOLD
+            if (any) {
+                const float osu = Bv.y * su;
+                g0 = osu * dx;
+                g1 = Bv.y * sudy;
+                g2 = g0 * dx;
+                g3 = g1 * dx;
+                g4 = Bv.y * sudy2;
+                g5 = su;
+            }
+#endif
             float* sg = &s_g[w][j * NGRAD];
             float t0 = 0.f, t1 = 0.f, t2 = 0.f;
             if (__ballot(any) != 0ull) wave_sum9(g0, g1, g2, g3, g4, g5, g6, g7, g8, t0, t1, t2);

@@ -23,6 +23,7 @@ def main():
                     help="comma-separated early-stop split denominators to compare (rr_set_binning_config)")
     ap.add_argument("--values", default=None, help="comma-separated integer values of --knob to compare (default 0,1)")
     ap.add_argument("--blocks", type=int, default=6)
+    ap.add_argument("--stages", action="store_true", help="also report per-stage kernel time per arm")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--points", type=int, default=1_000_000)
     a = ap.parse_args()
@@ -58,6 +59,7 @@ def main():
     arms = ([int(x) for x in a.split.split(",")] if a.split else
             [int(x) for x in a.values.split(",")] if a.values else [False, True])
     res = {v: [] for v in arms}
+    stages = {v: {} for v in arms}
     for b in range(len(arms) * a.blocks):
         val = arms[b % len(arms)]
         if a.split:
@@ -75,8 +77,19 @@ def main():
             it += 1
         torch.cuda.synchronize()
         res[val].append(1000 * (time.perf_counter() - t0) / a.steps)
+        if a.stages:  # an extra profiled block: per-stage kernel time (HIP events) of this arm
+            _native.Profiler.collect()
+            with _native.Profiler():
+                for _ in range(10):
+                    tr.step(it)
+                    it += 1
+            for k, (ms, n) in _native.Profiler.collect().items():
+                if n:
+                    stages[val].setdefault(k, []).append(ms / 10)
     for v in arms:
         print(f"{'split' if a.split else (a.knob or a.option)}={v}: median {statistics.median(res[v]):.4f} ms/step  blocks {[round(x, 4) for x in res[v]]}")
+        if a.stages:
+            print("   stages ms/step:", {k: round(statistics.median(x), 4) for k, x in stages[v].items()})
 
 
 if __name__ == "__main__":
