@@ -36,6 +36,9 @@ template <int NW, bool AUX>
 __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
 #pragma clang fp contract(off)  // blend_power's rounding: every fma below is explicit
     constexpr int PIX = 4 / NW;
+#ifndef RR_FWD_ROW_SKIP
+#define RR_FWD_ROW_SKIP 1
+#endif
 #ifndef RR_FWD_S_GROUP
 #define RR_FWD_S_GROUP 4
 #endif
@@ -98,11 +101,12 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
 
     for (int j0 = 0; j0 < n; j0 += G) {
         bool open[PIX];  // as of the group's start (only used to skip work)
-        uint64_t any_open = 0;
+        uint64_t any_open = 0, any_row[PIX];
 #pragma unroll
         for (int k = 0; k < PIX; k++) {
             open[k] = T[k] > 0.f;
-            any_open |= __builtin_amdgcn_ballot_w64(T[k] > 0.f);
+            any_row[k] = __builtin_amdgcn_ballot_w64(T[k] > 0.f);
+            any_open |= any_row[k];
         }
         if (!any_open) break;  // every pixel of this wave saturated
         uint32_t id[G];
@@ -122,16 +126,33 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
         float al[G][PIX];
         bool ok[G][PIX];
         uint64_t okm[G][PIX];  // ok as a wave mask (ballots of the compares themselves: v_cmp into SGPRs)
+        float cxdx2[G], wdx[G];
 #pragma unroll
         for (int u = 0; u < G; u++) {
             const float dx = ra[u].x - pfx;
-            const float cxdx2 = (ra[u].z * dx) * dx;
-            const float wdx = ra[u].w * dx;
+            cxdx2[u] = (ra[u].z * dx) * dx;
+            wdx[u] = ra[u].w * dx;
+        }
 #pragma unroll
-            for (int k = 0; k < PIX; k++) {
+        for (int k = 0; k < PIX; k++) {
+#if RR_FWD_ROW_SKIP
+            // a pixel row whose 64 pixels all saturated before this group evaluates no falloff
+            // (one uniform branch per group and row, the group's pairs stay interleaved inside)
+            if (!(any_row[k])) {
+#pragma unroll
+                for (int u = 0; u < G; u++) {
+                    okm[u][k] = 0;
+                    ok[u][k] = false;
+                    al[u][k] = 0.f;
+                }
+                continue;
+            }
+#endif
+#pragma unroll
+            for (int u = 0; u < G; u++) {
                 const float dy = ra[u].y - pfy[k];
-                const float tq = __builtin_fmaf(rb[u].x * dy, dy, cxdx2);
-                const float power = __builtin_fmaf(-0.5f, tq, -(wdx * dy));
+                const float tq = __builtin_fmaf(rb[u].x * dy, dy, cxdx2[u]);
+                const float power = __builtin_fmaf(-0.5f, tq, -(wdx[u] * dy));
                 const float g = __builtin_amdgcn_exp2f(power * kLog2e);
                 const float a99 = fminf(0.99f, rb[u].y * g);
                 // non-short-circuit: both compares become lane masks combined on the scalar unit
