@@ -61,19 +61,20 @@ MODELED = ("preprocess", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd"
 
 def algorithmic_bytes(stage, st, P, W, H, K):
     """SURVEY §8(d) algorithmic bytes per frame (one training step renders one frame).  Binning
-    stages are priced on the pairs this implementation actually sorts into tile lists (num_binned:
-    after exact tile culling and early-stop binning), not on the reference's larger num_rendered, so
-    they are not credited for pairs they never write.  The tile sort is priced at its minimum: read
-    + write each key and u32 value once."""
+    stages are priced on the (bin, Gaussian) pairs this implementation actually sorts (num_binned:
+    bins of 2 x 2 tiles, after exact culling and early-stop binning), not on the reference's larger
+    num_rendered, so they are not credited for pairs they never write.  The bin sort ("tile_sort")
+    is priced at its minimum: read + write each key and u32 value once; the expand ("ranges") at
+    reading the sorted pairs once (its per-tile list writes are not counted)."""
     Lb, V, Le, T, N = st["num_binned"], st["num_visible"], st["l_eff"], st["tiles"], W * H
     M = K
-    kw = 2 if T <= 65536 else 4
+    kw = 2 if (W + 31) // 32 * ((H + 31) // 32) <= 65536 else 4
     return {
         "preprocess": 20 * P + V * (99 + 12 * K),
         "scan": 8 * P,
         "duplicate": 4 * P + 16 * V + (kw + 4) * Lb,
         "tile_sort": 2 * (kw + 4) * Lb,
-        "ranges": kw * Lb + 8 * T,
+        "ranges": (kw + 4) * Lb + 8 * T,
         "blend_fwd": 8 * T + 44 * Le + 24 * N,
         "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
         "gauss_bwd": gauss_bwd_bytes(P, V, K, M),

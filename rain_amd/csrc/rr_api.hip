@@ -179,17 +179,20 @@ uint32_t early_split(uint32_t L) {
 }
 
 struct Bin {
-    uint32_t* point_list;  // FIRST, so the backward finds it without knowing the pair count
-    void* keys;
+    // FIRST, so the backward finds it without knowing the pair count: the per-tile lists k_expand
+    // writes, 4 slots per (bin, Gaussian) pair (phase A's at [0, 4 LA), phase B's at [4 LA, 4 L))
+    uint32_t* point_list;
+    void* keys;            // bin ids of the (bin, Gaussian) pairs, then sorted
     void* keys_sorted;
-    uint32_t* vals;
+    uint32_t* vals;        // Gaussian | tile mask << BIN_SHIFT, then sorted
+    uint32_t* vals_sorted;
     uint32_t* first;     // first Gaussian of every duplicate window (= sort unit), phase A then B
     uint32_t* unit_len;  // phase B: pairs kept per window
     void* temp;          // tile-sort scratch, shared by the two phases
     size_t temp_bytes;
-    bool wide;  // 32-bit tile keys (T > 65536)
+    bool wide;  // 32-bit bin keys (more than 65536 bins)
     int bits;
-    uint32_t L, LA;  // pairs, and pairs binned for every tile in phase A (LA == L: one phase)
+    uint32_t L, LA;  // (bin, Gaussian) pairs, and those binned for every bin in phase A (LA == L: one phase)
     size_t total;
 };
 template <typename K>
@@ -199,14 +202,14 @@ RadixPlan tile_plan(void* temp, uint32_t n, int bits) {
 Bin carve_bin(void* buf, int L, int W, int H) {
     Carver c(buf);
     Bin b;
-    const int T = grid_x(W) * grid_y(H);
-    b.wide = T > 65536;
-    b.bits = std::max(1, (int)higher_msb((uint32_t)T));  // >= 1: the duplicate windows are sort units
+    const int NB = bins_x(grid_x(W)) * bins_y(grid_y(H));
+    b.wide = NB > 65536;
+    b.bits = std::max(1, (int)higher_msb((uint32_t)NB));  // >= 1: the duplicate windows are sort units
     b.L = (uint32_t)std::max(L, 0);
     b.LA = early_split(b.L);
     const uint32_t LB = b.L - b.LA;
     const size_t n = (size_t)std::max(L, 1);
-    b.point_list = c.take<uint32_t>(n + kPointListPad);
+    b.point_list = c.take<uint32_t>(4 * n + kPointListPad);
     if (b.wide) {
         b.keys = c.take<uint32_t>(n);
         b.keys_sorted = c.take<uint32_t>(n);
@@ -215,6 +218,7 @@ Bin carve_bin(void* buf, int L, int W, int H) {
         b.keys_sorted = c.take<uint16_t>(n);
     }
     b.vals = c.take<uint32_t>(n);
+    b.vals_sorted = c.take<uint32_t>(n);
     const int ua = b.wide ? tile_plan<uint32_t>(nullptr, b.LA, b.bits).units : tile_plan<uint16_t>(nullptr, b.LA, b.bits).units;
     const int ub = b.wide ? tile_plan<uint32_t>(nullptr, LB, b.bits).units : tile_plan<uint16_t>(nullptr, LB, b.bits).units;
     b.first = c.take<uint32_t>((size_t)std::max(ua + ub, 1));
@@ -411,6 +415,7 @@ hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, hipStream_t st) 
 int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, bool forward) {
     if (!f || !cam || !g) return fail(RR_ERR_ARG, "null frame/camera/gaussians");
     if (f->P < 0 || f->width <= 0 || f->height <= 0) return fail(RR_ERR_ARG, "bad P/width/height");
+    if (f->P > (int)BIN_ID_MASK) return fail(RR_ERR_ARG, "P >= 2^28 (pair values carry a 4-bit tile mask)");
     if (f->P == 0) return RR_OK;
     if (!g->means3D || (forward && !g->opacities)) return fail(RR_ERR_ARG, "means3D and opacities are required");
     if (!cam->background || !cam->viewmatrix || !cam->projmatrix || !cam->campos)
@@ -508,7 +513,7 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
     uint2 tot = make_uint2(0u, 0u);
     RR_CHECK(pair_counts_wait(rd, &tot, st), "read L");
-    if (tot.x > 0x7fffffffu || tot.y > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^31 tile/Gaussian pairs");
+    if (tot.x > 0x1fffffffu || tot.y > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^29 bin/Gaussian pairs");
     *num_rendered = (int)tot.y;
     *num_pairs = (int)tot.x;
     return RR_OK;
@@ -543,16 +548,16 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         RR_STAGE_CHECK("duplicate");
         {
             StageTimer tm(RR_STAGE_TILE_SORT, st);
-            RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.point_list, LA, 0,
+            RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.vals_sorted, LA, 0,
                                          bn.bits, st, true),
-                     std::string("tile sort (") + radix_sort_last_error() + ")");
+                     std::string("bin sort (") + radix_sort_last_error() + ")");
         }
-        RR_STAGE_CHECK("tile sort");
+        RR_STAGE_CHECK("bin sort");
         {
             StageTimer tm(RR_STAGE_RANGES, st);
-            launch_ranges<K>((int)LA, keys_sorted, im.ranges, 0u, nullptr, st);
+            launch_expand<K>(LA, nullptr, keys_sorted, bn.vals_sorted, gx, gy, 0u, bn.point_list, im.ranges, st);
         }
-        RR_STAGE_CHECK("ranges");
+        RR_STAGE_CHECK("expand");
     }
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
@@ -578,15 +583,16 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_TILE_SORT, st);
         RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys + LA, keys_sorted + LA, bn.vals + LA,
-                                     bn.point_list + LA, LB, 0, bn.bits, st, true, bn.unit_len, im.counters),
-                 std::string("tile sort, phase B (") + radix_sort_last_error() + ")");
+                                     bn.vals_sorted + LA, LB, 0, bn.bits, st, true, bn.unit_len, im.counters),
+                 std::string("bin sort, phase B (") + radix_sort_last_error() + ")");
     }
-    RR_STAGE_CHECK("tile sort (phase B)");
+    RR_STAGE_CHECK("bin sort (phase B)");
     {
         StageTimer tm(RR_STAGE_RANGES, st);
-        launch_ranges<K>((int)LB, keys_sorted + LA, im.ranges_b, LA, im.counters, st);
+        launch_expand<K>(LB, im.counters, keys_sorted + LA, bn.vals_sorted + LA, gx, gy, 4u * LA, bn.point_list,
+                         im.ranges_b, st);
     }
-    RR_STAGE_CHECK("ranges (phase B)");
+    RR_STAGE_CHECK("expand (phase B)");
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = kBlendPhaseB;

@@ -272,6 +272,7 @@ int g_bwd_order = -1;  // -1: RAIN_BWD_TILE_ORDER or the default (on)
 int g_fwd_b_waves = -1;  // -1: RAIN_BLEND_FWD_B_WAVES or the default
 int g_fwd_order = -1;  // -1: RAIN_FWD_TILE_ORDER or the default (off)
 int g_fwd_impl = -1;  // -1: RAIN_FWD_IMPL or the default
+int g_fwd_impl_b = 2;
 int g_fwd_s_waves = 2, g_fwd_s_b_waves = 4;
 int env_waves(const char* name, int dflt) {
     const char* s = std::getenv(name);
@@ -323,12 +324,12 @@ bool fwd_tile_order() {
     return g_fwd_order != 0;
 }
 
-int blend_fwd_impl() {
+int blend_fwd_impl(bool phase_b) {
     if (g_fwd_impl < 0) {
         const char* s = std::getenv("RAIN_FWD_IMPL");
         g_fwd_impl = s ? std::atoi(s) : 2;
     }
-    return g_fwd_impl;
+    return phase_b ? g_fwd_impl_b : g_fwd_impl;
 }
 
 int blend_fwd_s_waves(bool phase_b) { return phase_b ? g_fwd_s_b_waves : g_fwd_s_waves; }
@@ -345,6 +346,7 @@ int set_tuning(const char* key, int value) {
     else if (k == "fwd_b_waves") g_fwd_b_waves = value ? 4 : 0;
     else if (k == "fwd_waves") g_fwd_waves = value;
     else if (k == "fwd_impl") g_fwd_impl = (value >= 0 && value <= 2) ? value : 2;
+    else if (k == "fwd_impl_b") g_fwd_impl_b = (value >= 0 && value <= 2) ? value : 2;
     else if (k == "fwd_s_waves") g_fwd_s_waves = (value == 1 || value == 4) ? value : 2;
     else if (k == "fwd_s_b_waves") g_fwd_s_b_waves = (value == 1 || value == 2) ? value : 4;
     else if (k == "bwd_waves") g_bwd_waves = value;

@@ -345,7 +345,7 @@ void launch_blend_fwd_t(const BlendFwdArgs& a, hipStream_t st) {
 
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
     if (a.gx * a.gy == 0) return;
-    const int impl = blend_fwd_impl();
+    const int impl = blend_fwd_impl(a.phase == kBlendPhaseB);
     if (impl == 2) launch_blend_fwd_s(a, blend_fwd_s_waves(a.phase == kBlendPhaseB), st);
     else if (impl == 1) launch_blend_fwd_t<true>(a, st);
     else launch_blend_fwd_t<false>(a, st);

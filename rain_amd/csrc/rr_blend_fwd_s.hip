@@ -36,9 +36,6 @@ template <int NW, bool AUX>
 __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
 #pragma clang fp contract(off)  // blend_power's rounding: every fma below is explicit
     constexpr int PIX = 4 / NW;
-#ifndef RR_FWD_ROW_SKIP
-#define RR_FWD_ROW_SKIP 1
-#endif
 #ifndef RR_FWD_S_GROUP
 #define RR_FWD_S_GROUP 4
 #endif
@@ -101,12 +98,11 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
 
     for (int j0 = 0; j0 < n; j0 += G) {
         bool open[PIX];  // as of the group's start (only used to skip work)
-        uint64_t any_open = 0, any_row[PIX];
+        uint64_t any_open = 0;
 #pragma unroll
         for (int k = 0; k < PIX; k++) {
             open[k] = T[k] > 0.f;
-            any_row[k] = __builtin_amdgcn_ballot_w64(T[k] > 0.f);
-            any_open |= any_row[k];
+            any_open |= __builtin_amdgcn_ballot_w64(T[k] > 0.f);
         }
         if (!any_open) break;  // every pixel of this wave saturated
         uint32_t id[G];
@@ -135,19 +131,6 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < PIX; k++) {
-#if RR_FWD_ROW_SKIP
-            // a pixel row whose 64 pixels all saturated before this group evaluates no falloff
-            // (one uniform branch per group and row, the group's pairs stay interleaved inside)
-            if (!(any_row[k])) {
-#pragma unroll
-                for (int u = 0; u < G; u++) {
-                    okm[u][k] = 0;
-                    ok[u][k] = false;
-                    al[u][k] = 0.f;
-                }
-                continue;
-            }
-#endif
 #pragma unroll
             for (int u = 0; u < G; u++) {
                 const float dy = ra[u].y - pfy[k];

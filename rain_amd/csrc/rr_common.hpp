@@ -130,6 +130,52 @@ __device__ __forceinline__ void cull_row_span(float mx, float my, float ca, floa
     *hi = (int)floorf(fminf(fmaxf(vh, (float)x0 - 1.f), (float)x1 - 1.f)) + 1;
 }
 
+// ---- bins: 2 x 2 blend tiles (32 x 32 px) ------------------------------------------------------
+// The binning sorts (bin, Gaussian) pairs instead of (tile, Gaussian) pairs: a Gaussian that
+// covers a 3 x 3 block of tiles covers ~2 x 2 bins, so about half as many pairs are emitted,
+// sorted and stored, on fewer key bits.  A pair carries the 4-bit mask of the bin's tiles the
+// Gaussian reaches (bit 2 r + c: tile row r, column c of the bin) in the top bits of its value;
+// after the sort, k_expand splits every bin's list into its four per-tile lists (stable), so the
+// blend kernels still walk exact per-tile lists in (depth, index) order.
+constexpr int BIN_SHIFT = 28;                     // value = gaussian | mask << BIN_SHIFT (P < 2^28)
+constexpr uint32_t BIN_ID_MASK = (1u << BIN_SHIFT) - 1u;
+__host__ __device__ __forceinline__ int bins_x(int gx) { return (gx + 1) >> 1; }
+__host__ __device__ __forceinline__ int bins_y(int gy) { return (gy + 1) >> 1; }
+
+// The two tile rows 2Y, 2Y+1 of bin row Y: the tile-column span [l, h) each row's pixels are
+// reached in (exact culling, cull_row_span) or the bounding rect's columns; rows outside [y0, y1)
+// are empty.
+__device__ __forceinline__ void bin_row_spans(float mx, float my, float ca, float cb, float cc, float qmax, int cull,
+                                              int Y, int x0, int x1, int y0, int y1, int& l0, int& h0, int& l1,
+                                              int& h1) {
+    l0 = h0 = l1 = h1 = x0;
+    const int ya = 2 * Y, yb = 2 * Y + 1;
+    if (ya >= y0 && ya < y1) {
+        l0 = x0;
+        h0 = x1;
+        if (cull) cull_row_span(mx, my, ca, cb, cc, qmax, ya, x0, x1, &l0, &h0);
+    }
+    if (yb >= y0 && yb < y1) {
+        l1 = x0;
+        h1 = x1;
+        if (cull) cull_row_span(mx, my, ca, cb, cc, qmax, yb, x0, x1, &l1, &h1);
+    }
+}
+// Mask of bin column X given its two rows' spans (bit 2 r + c = tile (2Y + r, 2X + c) reached).
+__device__ __forceinline__ uint32_t bin_mask(int X, int l0, int h0, int l1, int h1) {
+    const int c0 = 2 * X, c1 = 2 * X + 1;
+    return (uint32_t)(c0 >= l0 && c0 < h0) | ((uint32_t)(c1 >= l0 && c1 < h0) << 1) |
+           ((uint32_t)(c0 >= l1 && c0 < h1) << 2) | ((uint32_t)(c1 >= l1 && c1 < h1) << 3);
+}
+// Bin columns [Xa, Xb) that can hold a non-zero mask in a bin row.
+__device__ __forceinline__ void bin_cols(int l0, int h0, int l1, int h1, int& Xa, int& Xb) {
+    const bool e0 = h0 <= l0, e1 = h1 <= l1;
+    const int lo = e0 ? l1 : (e1 ? l0 : min(l0, l1));
+    const int hi = e0 ? h1 : (e1 ? h0 : max(h0, h1));
+    Xa = lo >> 1;
+    Xb = (e0 && e1) ? Xa : (hi + 1) >> 1;
+}
+
 // Column-major 4x4 transforms (auxiliary.h:47-86).  Matrices live in device memory and are
 // indexed with wave-uniform offsets, so the compiler keeps them in SGPRs (s_load).
 __device__ __forceinline__ v3 xform_point_4x3(v3 p, const float* m) {

@@ -1,8 +1,10 @@
 // rr_forward.hip — forward kernels of the MI355X rasterizer.
 //
 //   k_preprocess<DEG>  one thread per Gaussian (forward.cu:144-246 semantics)
-//   k_duplicate<K>     (tile, Gaussian) pairs in depth order, key = tile id only (LDS windows)
-//   k_ranges<K>        per-tile [start, end) in the tile-sorted list (rasterizer_impl.cu:105-127)
+//   k_duplicate<K>     (bin, Gaussian) pairs in depth order, key = bin id only, value = Gaussian |
+//                      tile mask << BIN_SHIFT (LDS windows; bins: rr_common.hpp)
+//   k_expand<K>        per bin of the bin-sorted list: its four per-tile lists (stable) and their
+//                      [start, end) (rasterizer_impl.cu:105-127's ranges)
 //   k_blend_fwd        per-tile front-to-back alpha blend (forward.cu:251-369)
 //   k_mark_visible     frustum test (rasterizer_impl.cu:43-55)
 //
@@ -94,15 +96,15 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
     a.splats[idx] = s;
     if (a.normals) a.normals[idx] = gaussian_normal(sc, q, a.view, p_view);
     a.radii[idx] = radius;
-    uint32_t n = (uint32_t)area;
-    if (a.cull) {
-        const float qmax = cull_qmax(opacity);
-        n = 0;
-        for (int y = y0; y < y1; y++) {
-            int lo, hi;
-            cull_row_span(px, py, cx, cy, cz, qmax, y, x0, x1, &lo, &hi);
-            n += hi > lo ? (uint32_t)(hi - lo) : 0u;
-        }
+    // (bin, Gaussian) pairs: bins (2 x 2 tiles, rr_common.hpp) holding a tile the Gaussian reaches
+    // (exact culling) or a tile of its bounding rect
+    const float qmax = a.cull ? cull_qmax(opacity) : 0.f;
+    uint32_t n = 0;
+    for (int Y = y0 >> 1; Y < (y1 + 1) >> 1; Y++) {
+        int l0, h0, l1, h1, Xa, Xb;
+        bin_row_spans(px, py, cx, cy, cz, qmax, a.cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
+        bin_cols(l0, h0, l1, h1, Xa, Xb);
+        for (int X = Xa; X < Xb; X++) n += bin_mask(X, l0, h0, l1, h1) != 0u ? 1u : 0u;
     }
     a.tiles[idx] = make_uint2(n, (uint32_t)area);
     a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
@@ -240,13 +242,13 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                                                    const uint32_t* __restrict__ sat,
                                                    const uint32_t* __restrict__ open_bits,
                                                    uint32_t* __restrict__ unit_len, uint32_t* __restrict__ n_total) {
-    // open-tile bitmask in LDS for 16-bit tile ids (T <= 65536); wider grids read open[] directly
+    // open-tile bitmask in LDS for grids of <= 65536 tiles; larger grids read open_bits directly
     // (FILTER: phase B; the unfiltered kernel does without the mask's 8 KiB of LDS)
-    constexpr bool kMaskLds = sizeof(K) == 2 && FILTER;
+    const bool kMaskLds = FILTER && gx * gy <= 65536;
     __shared__ K s_key[kSortMaxUnit];
     __shared__ uint32_t s_val[kSortMaxUnit];
     __shared__ uint32_t hist[256];
-    __shared__ uint32_t s_open[kMaskLds ? 2048 : 1];
+    __shared__ uint32_t s_open[FILTER ? 2048 : 1];
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
@@ -264,6 +266,17 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
         const uint32_t word = kMaskLds ? s_open[tile >> 5] : open_bits[tile >> 5];
         return ((word >> (tile & 31)) & 1u) != 0;
     };
+    // the bin's tiles still open (phase B), as a bin mask
+    auto open4 = [&](int X, int Y) -> uint32_t {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int tx = 2 * X + (b & 1), ty = 2 * Y + (b >> 1);
+            if (tx < gx && ty < gy && is_open((uint32_t)(ty * gx + tx))) m |= 1u << b;
+        }
+        return m;
+    };
+    const int bgx = bins_x(gx);
     const int sw = gx + 1;
     const int s0 = (int)first[blockIdx.x];
     for (int base = s0;; base += 256) {
@@ -281,24 +294,30 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                     !filter || (sat[y1 * sw + x1] + sat[y0 * sw + x0] - sat[y0 * sw + x1] - sat[y1 * sw + x0]) > 0;
                 if (any_open) {
                     const float qmax = cull ? cull_qmax(splats[g].b.y) : 0.f;
-                    const float cz = cull ? splats[g].b.x : 0.f;
+                    const float cz = splats[g].b.x;
                     uint32_t pos = a;
-                    for (int y = y0; y < y1 && pos < hi; y++) {
-                        int l = x0, h = x1;
-                        if (cull) cull_row_span(A.x, A.y, A.z, A.w, cz, qmax, y, x0, x1, &l, &h);
-                        const uint32_t c = h > l ? (uint32_t)(h - l) : 0u;
-                        if (pos + c <= lo) {  // row entirely before the window
+                    for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && pos < hi; Y++) {
+                        int l0, h0, l1, h1, Xa, Xb;
+                        bin_row_spans(A.x, A.y, A.z, A.w, cz, qmax, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
+                        bin_cols(l0, h0, l1, h1, Xa, Xb);
+                        uint32_t c = 0;
+                        for (int X = Xa; X < Xb; X++) c += bin_mask(X, l0, h0, l1, h1) != 0u ? 1u : 0u;
+                        if (pos + c <= lo) {  // bin row entirely before the window
                             pos += c;
                             continue;
                         }
-                        for (int x = l; x < h && pos < hi; x++, pos++)
+                        for (int X = Xa; X < Xb && pos < hi; X++) {
+                            uint32_t m = bin_mask(X, l0, h0, l1, h1);
+                            if (!m) continue;
                             if (pos >= lo) {
-                                const uint32_t tile = (uint32_t)(y * gx + x);
-                                if (!filter || is_open(tile)) {
-                                    s_key[pos - w0] = (K)tile;
-                                    s_val[pos - w0] = g;
+                                if (filter) m &= open4(X, Y);
+                                if (m) {
+                                    s_key[pos - w0] = (K)(Y * bgx + X);
+                                    s_val[pos - w0] = g | (m << BIN_SHIFT);
                                 }
                             }
+                            pos++;
+                        }
                     }
                 }
             }
@@ -356,25 +375,74 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + blockIdx.x] = hist[d];
 }
 
+// One workgroup per bin.  The bin's run [lo, hi) of the bin-sorted list (two binary searches over
+// the sorted keys) holds its pairs in (depth, index) order with their tile masks; each of the bin's
+// (up to) four tiles gets the stable sub-list of the pairs whose mask has its bit, written at
+// out_base + 4 lo + b (hi - lo) (capacity 4x the bin pairs, so no global scan), and its range
+// (rasterizer_impl.cu:105-127 identifyTileRanges).  Every tile of the grid gets a range, so the
+// ranges need no clearing.  n_dev: device-side count of a filtered (phase B) list.
 template <typename K>
-__global__ __launch_bounds__(256) void k_ranges(int L, const K* __restrict__ keys, uint2* __restrict__ ranges,
-                                                uint32_t base, const uint32_t* __restrict__ n_dev) {
-    // L: host bound; n_dev (optional): the device-side count of a filtered list (grid-stride, so a
-    // short filtered list does not pay for a grid sized by its bound).  Ranges are absolute
-    // point_list indices (base + position).
-    const int n = n_dev ? (int)*n_dev : L;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t cur = keys[i];
-        if (i == 0) {
-            ranges[cur].x = base;
-        } else {
-            const uint32_t prev = keys[i - 1];
-            if (cur != prev) {
-                ranges[prev].y = base + i;
-                ranges[cur].x = base + i;
-            }
+__global__ __launch_bounds__(256) void k_expand(uint32_t n_host, const uint32_t* __restrict__ n_dev,
+                                                const K* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                int gx, int gy, uint32_t out_base, uint32_t* __restrict__ point_list,
+                                                uint2* __restrict__ ranges) {
+    __shared__ uint32_t wsum[4][4];
+    const int bgx = bins_x(gx);
+    const int bin = blockIdx.x;
+    const int X = bin % bgx, Y = bin / bgx;
+    const uint32_t n = n_dev ? *n_dev : n_host;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // 256-ary search: each round probes 256 evenly spaced keys at once (one load latency per round,
+    // 3 rounds for 16M pairs, instead of a 24-deep chain of dependent loads)
+    auto lower_bound = [&](uint32_t v) {
+        uint32_t l = 0, h = n;  // answer in [l, h]
+        while (h - l > 1) {
+            const uint32_t step = (h - l + 255) / 256;
+            const uint32_t idx = l + (uint32_t)t * step;
+            const int c = __syncthreads_count(idx < h && (uint32_t)keys[idx] < v);  // probes below v
+            // probes 0..c-1 are below v: the answer lies in (l + (c-1) step, l + c step]
+            const uint32_t nl = c == 0 ? l : l + (uint32_t)(c - 1) * step + 1u;
+            const uint32_t nh = min(h, l + (uint32_t)c * step);
+            l = nl;
+            h = nh;
         }
-        if (i == n - 1) ranges[cur].y = base + n;
+        if (l < h) l += (uint32_t)__syncthreads_count((uint32_t)keys[l] < v) != 0 ? 1u : 0u;
+        return l;
+    };
+    const uint32_t lo = lower_bound((uint32_t)bin), hi = lower_bound((uint32_t)bin + 1u);
+    const uint32_t len = hi - lo;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t dst0 = out_base + 4u * lo;
+    uint32_t carry[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t r0 = 0; r0 < len; r0 += 256) {
+        const uint32_t j = r0 + (uint32_t)t;
+        const uint32_t v = j < len ? vals[lo + j] : 0u;
+        const uint32_t m = j < len ? v >> BIN_SHIFT : 0u;
+        uint32_t rank[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint64_t bal = __ballot((m >> b) & 1u);
+            rank[b] = (uint32_t)__popcll(bal & lt);
+            if (lane == 0) wsum[w][b] = (uint32_t)__popcll(bal);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            uint32_t pre = carry[b], tot = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                pre += i < w ? wsum[i][b] : 0u;
+                tot += wsum[i][b];
+            }
+            if ((m >> b) & 1u) point_list[dst0 + (uint32_t)b * len + pre + rank[b]] = v & BIN_ID_MASK;
+            carry[b] += tot;
+        }
+        __syncthreads();
+    }
+    if (t < 4) {
+        const int tx = 2 * X + (t & 1), ty = 2 * Y + (t >> 1);
+        const uint32_t s = dst0 + (uint32_t)t * len;
+        if (tx < gx && ty < gy) ranges[ty * gx + tx] = make_uint2(s, s + carry[t]);
     }
 }
 
@@ -426,13 +494,15 @@ void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_
 }
 
 template <typename K>
-void launch_ranges(int L, const K* keys, uint2* ranges, uint32_t base, const uint32_t* n_dev, hipStream_t st) {
-    if (L == 0) return;
-    const int nb = blocks_for(L);
-    k_ranges<K><<<(n_dev && nb > 2048) ? 2048 : nb, 256, 0, st>>>(L, keys, ranges, base, n_dev);
+void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,
+                   uint32_t out_base, uint32_t* point_list, uint2* ranges, hipStream_t st) {
+    const int nb = bins_x(gx) * bins_y(gy);
+    if (nb > 0) k_expand<K><<<nb, 256, 0, st>>>(L, n_dev, keys, vals, gx, gy, out_base, point_list, ranges);
 }
-template void launch_ranges<uint16_t>(int, const uint16_t*, uint2*, uint32_t, const uint32_t*, hipStream_t);
-template void launch_ranges<uint32_t>(int, const uint32_t*, uint2*, uint32_t, const uint32_t*, hipStream_t);
+template void launch_expand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, int, int, uint32_t,
+                                      uint32_t*, uint2*, hipStream_t);
+template void launch_expand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, int, int, uint32_t,
+                                      uint32_t*, uint2*, hipStream_t);
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;

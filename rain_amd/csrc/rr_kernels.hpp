@@ -139,7 +139,8 @@ template <typename K>
 void launch_duplicate(const DupArgs<K>& d, hipStream_t st);
 void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_t* open_bits, hipStream_t st);
 template <typename K>
-void launch_ranges(int L, const K* keys, uint2* ranges, uint32_t base, const uint32_t* n_dev, hipStream_t st);
+void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,
+                   uint32_t out_base, uint32_t* point_list, uint2* ranges, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
@@ -191,7 +192,7 @@ bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_se
 bool fwd_tile_order();  // forward blends dispatch tiles longest list first (rr_set_tuning "fwd_tile_order")
 // forward blend implementation (rr_set_tuning "fwd_impl"): 0 packed fp32 + LDS-staged records,
 // 1 packed fp32 + scalar-loaded records, 2 scalar fp32 + scalar-loaded records (rr_blend_fwd_s.hip)
-int blend_fwd_impl();
+int blend_fwd_impl(bool phase_b);  // phase B of early-stop binning: "fwd_impl_b"
 int blend_fwd_s_waves(bool phase_b);  // waves per tile of impl 2 ("fwd_s_waves" / "fwd_s_b_waves")
 void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);

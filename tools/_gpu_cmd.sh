@@ -1,7 +1,5 @@
 mkdir -p gpurun_out
-timeout -k 10 120 python tools/phaseb_stats.py > gpurun_out/phaseb_stats.json 2>&1 || exit 1
-timeout -k 10 120 python tools/fwd_check.py --impls 0,2 --points 100000 --width 800 --height 800 > gpurun_out/fwd_check.txt 2>&1 || exit 1
-timeout -k 10 200 python tools/raster_ab.py --knob fwd_impl --values 0,2 --rounds 5 > gpurun_out/skip1.json 2>&1 || exit 1
-for v in noskip skipg8; do
-RAIN_RASTER_LIB=$PWD/gpurun_variants/$v.so timeout -k 10 200 python tools/raster_ab.py --knob fwd_impl --values 2 --rounds 5 > gpurun_out/$v.json 2>&1 || exit 1
-done
+timeout -k 10 600 python -u -m pytest tests/test_parity_gpu.py tests/test_early_stop_gpu.py tests/test_fused_gpu.py tests/test_aux_normal_gpu.py tests/test_fullsize_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/bins_tests.log 2>&1
+rc=$?; [ $rc -eq 0 -o $rc -eq 1 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 60 --no-cpu-baseline > gpurun_out/bench_bins.json 2> gpurun_out/bench_bins.err || exit 1
+RAIN_RASTER_LIB=$PWD/gpurun_variants/head.so timeout -k 10 300 python bench.py --steps 60 --no-cpu-baseline > gpurun_out/bench_head.json 2> gpurun_out/bench_head.err
