@@ -101,8 +101,8 @@ __device__ __forceinline__ void put(float* grad, size_t e, float g) {
 // Adam over n elements whose (param, moment) addresses are given: all loads first, then the
 // math, then the stores (the compiler cannot batch them itself: the arrays may alias).
 template <int N>
-__device__ __forceinline__ void adam_batch(const GaussBwdArgs& a, float* const (&pp)[N], float* const (&mp)[N],
-                                           float* const (&vp)[N], const float (&g)[N], const rr_adam_group* const (&gr)[N]) {
+__device__ __forceinline__ void adam_batch(float* const (&pp)[N], float* const (&mp)[N], float* const (&vp)[N],
+                                           const float (&g)[N], const AdamC (&c)[N]) {
     float p[N], m[N], v[N];
 #pragma unroll
     for (int i = 0; i < N; i++) {
@@ -112,8 +112,7 @@ __device__ __forceinline__ void adam_batch(const GaussBwdArgs& a, float* const (
     }
 #pragma unroll
     for (int i = 0; i < N; i++)
-        adam_elem(p[i], g[i], m[i], v[i], gr[i]->lr, gr[i]->bias_correction1, gr[i]->bias_correction2_sqrt,
-                  a.adam.beta1, a.adam.beta2, a.adam.eps);
+        adam_elem(p[i], g[i], m[i], v[i], c[i]);
 #pragma unroll
     for (int i = 0; i < N; i++) {
         *pp[i] = p[i];
@@ -124,20 +123,30 @@ __device__ __forceinline__ void adam_batch(const GaussBwdArgs& a, float* const (
 
 __device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const SmallGrads& sg) {
     const rr_adam& ad = a.adam;
+    auto consts = [&](const rr_adam_group& G) {
+        return adam_consts(G.lr, G.bias_correction1, G.bias_correction2_sqrt, ad.beta1, ad.beta2, ad.eps);
+    };
+    const AdamC c_xyz = consts(ad.xyz), c_sc = consts(ad.scaling), c_op = consts(ad.opacity),
+                c_rot = consts(ad.rotation);
     const rr_adam_group* gr[11];
+    AdamC cc[11];  // values (indices are compile-time after unrolling: stays in registers)
     size_t e[11];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         gr[i] = &ad.xyz;
+        cc[i] = c_xyz;
         e[i] = 3 * (size_t)idx + i;
         gr[4 + i] = &ad.scaling;
+        cc[4 + i] = c_sc;
         e[4 + i] = 3 * (size_t)idx + i;
     }
     gr[3] = &ad.opacity;
+    cc[3] = c_op;
     e[3] = idx;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         gr[7 + i] = &ad.rotation;
+        cc[7 + i] = c_rot;
         e[7 + i] = 4 * (size_t)idx + i;
     }
     float* pp[11];
@@ -149,7 +158,7 @@ __device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const
         mp[i] = gr[i]->exp_avg + e[i];
         vp[i] = gr[i]->exp_avg_sq + e[i];
     }
-    adam_batch<11>(a, pp, mp, vp, sg.v, gr);
+    adam_batch<11>(pp, mp, vp, sg.v, cc);
 }
 
 // One Gaussian.  `row` is this thread's LDS row holding its SH coefficients (staged by the
@@ -451,13 +460,19 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
         auto stage_out = [&](float* dst, const rr_adam_group* grp, int w, int koff) {
             const int total = nvalid * w;
             const float inv = 1.0f / (float)w;
-            constexpr int kB = 8;  // Adam elements per batch of loads
+            const AdamC c = grp ? adam_consts(grp->lr, grp->bias_correction1, grp->bias_correction2_sqrt, a.adam.beta1,
+                                              a.adam.beta2, a.adam.eps)
+                                : AdamC{};
+#ifndef RR_GB_ADAM_BATCH
+#define RR_GB_ADAM_BATCH 8
+#endif
+            constexpr int kB = RR_GB_ADAM_BATCH;  // Adam elements per batch of loads
             for (int e0 = t; e0 < total; e0 += kB * kGB) {
                 float g[kB];
                 float* pp[kB];
                 float* mp[kB];
                 float* vp[kB];
-                const rr_adam_group* gr[kB];
+                AdamC cq[kB];
                 int n = 0;
 #pragma unroll
                 for (int q = 0; q < kB; q++) {
@@ -473,17 +488,16 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
                         pp[q] = grp->param + ge;
                         mp[q] = grp->exp_avg + ge;
                         vp[q] = grp->exp_avg_sq + ge;
-                        gr[q] = grp;
+                        cq[q] = c;
                     }
                 }
                 if (grp) {
                     if (n == kB) {
-                        adam_batch<kB>(a, pp, mp, vp, g, gr);
+                        adam_batch<kB>(pp, mp, vp, g, cq);
                     } else {  // tail: one at a time, never touching an element twice
                         for (int q = 0; q < n; q++) {
                             float p = *pp[q], m = *mp[q], v = *vp[q];
-                            adam_elem(p, g[q], m, v, grp->lr, grp->bias_correction1, grp->bias_correction2_sqrt,
-                                      a.adam.beta1, a.adam.beta2, a.adam.eps);
+                            adam_elem(p, g[q], m, v, c);
                             *pp[q] = p;
                             *mp[q] = m;
                             *vp[q] = v;

@@ -55,16 +55,19 @@ __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
     const AdamGroupDev& G = a.grp[gi];
     const int64_t e0 = (int64_t)(b - G.block0) * kPerBlock + (int64_t)threadIdx.x * kPerThread;
     if (e0 >= G.n) return;
+    const AdamC c = adam_consts(G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
     if (G.vec && e0 + kPerThread <= G.n) {
         float4 p = *reinterpret_cast<const float4*>(G.p + e0);
         float4 g = *reinterpret_cast<const float4*>(G.g + e0);
-        g.x *= a.grad_scale; g.y *= a.grad_scale; g.z *= a.grad_scale; g.w *= a.grad_scale;
+        // rounded product (no fma contraction into the update): bitwise torch's grad.mul_(scale) + step
+        g.x = mul_rounded(g.x, a.grad_scale); g.y = mul_rounded(g.y, a.grad_scale);
+        g.z = mul_rounded(g.z, a.grad_scale); g.w = mul_rounded(g.w, a.grad_scale);
         float4 m = *reinterpret_cast<const float4*>(G.m + e0);
         float4 v = *reinterpret_cast<const float4*>(G.v + e0);
-        adam_elem(p.x, g.x, m.x, v.x, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
-        adam_elem(p.y, g.y, m.y, v.y, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
-        adam_elem(p.z, g.z, m.z, v.z, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
-        adam_elem(p.w, g.w, m.w, v.w, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
+        adam_elem(p.x, g.x, m.x, v.x, c);
+        adam_elem(p.y, g.y, m.y, v.y, c);
+        adam_elem(p.z, g.z, m.z, v.z, c);
+        adam_elem(p.w, g.w, m.w, v.w, c);
         *reinterpret_cast<float4*>(G.p + e0) = p;
         *reinterpret_cast<float4*>(G.m + e0) = m;
         *reinterpret_cast<float4*>(G.v + e0) = v;
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
         for (int k = 0; k < kPerThread && e0 + k < G.n; k++) {
             const int64_t e = e0 + k;
             float p = G.p[e], m = G.m[e], v = G.v[e];
-            adam_elem(p, G.g[e] * a.grad_scale, m, v, G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
+            adam_elem(p, mul_rounded(G.g[e], a.grad_scale), m, v, c);
             G.p[e] = p;
             G.m[e] = m;
             G.v[e] = v;

@@ -89,7 +89,11 @@ def test_raw_mode_matches_reference_api(gpu, sh_degree, active, low_pass):
     assert torch.equal(mr, mr_ref)
 
 
-def test_fused_adam_matches_torch_adam(gpu):
+@pytest.mark.parametrize("impl", ["foreach", "fused"])
+def test_fused_adam_matches_torch_adam(gpu, impl):
+    """FusedAdam == torch.optim.Adam: the default (foreach) implementation the reference's
+    training_setup gets on GPU tensors (gaussian_model.py:153), restated op for op in fp32 by
+    adam_math.hpp; and torch's fused kernel (double-precision moment update) within rounding."""
     torch.manual_seed(0)
     shapes = [(1000, 3), (1000, 1, 3), (1000, 15, 3), (1000, 1), (1000, 3), (1000, 4), (7,), (5, 5)]
     lrs = [1.6e-4, 2.5e-3, 1.25e-4, 0.05, 5e-3, 1e-3, 0.1, 0.01]
@@ -100,7 +104,8 @@ def test_fused_adam_matches_torch_adam(gpu):
     from rain_amd.optim import FusedAdam
 
     oa = FusedAdam([{"params": [p], "lr": lr} for p, lr in zip(pa, lrs)], lr=0.0, eps=1e-15)
-    ob = torch.optim.Adam([{"params": [p], "lr": lr} for p, lr in zip(pb, lrs)], lr=0.0, eps=1e-15, fused=True)
+    kw = {"fused": True} if impl == "fused" else {"foreach": True}
+    ob = torch.optim.Adam([{"params": [p], "lr": lr} for p, lr in zip(pb, lrs)], lr=0.0, eps=1e-15, **kw)
     for it in range(20):
         for x, y in zip(pa, pb):
             gr = torch.randn_like(x) * (0.0 if it == 3 else 1.0)
@@ -111,13 +116,16 @@ def test_fused_adam_matches_torch_adam(gpu):
             pb[2].grad = None
         oa.step()
         ob.step()
+    # torch's fused kernel updates the moments in double: an fp32 lerp differs by <= 1 ulp per step,
+    # which near zero is far beyond a relative bar (absolute bar instead)
+    rtol, atol_m, atol_v = (1e-6, 1e-9, 1e-12) if impl == "foreach" else (4e-6, 1e-6, 1e-9)
     for x, y in zip(pa, pb):
         assert (x - y).abs().max() <= 1e-6 * max(1.0, y.abs().max().item()), (x - y).abs().max()
     for x, y in zip(pa, pb):
         sa, sb = oa.state[x], ob.state[y]
         assert float(sa["step"]) == float(sb["step"])
-        assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-6, atol=1e-9)
-        assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-6, atol=1e-12)
+        assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=rtol, atol=atol_m)
+        assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=rtol, atol=atol_v)
 
 
 def test_fused_trainer_matches_autograd_trainer(gpu):
