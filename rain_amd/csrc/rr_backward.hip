@@ -104,20 +104,33 @@ template <int N>
 __device__ __forceinline__ void adam_batch(float* const (&pp)[N], float* const (&mp)[N], float* const (&vp)[N],
                                            const float (&g)[N], const AdamC (&c)[N]) {
     float p[N], m[N], v[N];
+#ifndef RR_GB_NT
+#define RR_GB_NT 0
+#endif
 #pragma unroll
     for (int i = 0; i < N; i++) {
         p[i] = *pp[i];
-        m[i] = *mp[i];
-        v[i] = *vp[i];
+        if (RR_GB_NT) {  // moments are read and written once per step: no reuse to keep in the caches
+            m[i] = __builtin_nontemporal_load(mp[i]);
+            v[i] = __builtin_nontemporal_load(vp[i]);
+        } else {
+            m[i] = *mp[i];
+            v[i] = *vp[i];
+        }
     }
 #pragma unroll
-    for (int i = 0; i < N; i++)
-        adam_elem(p[i], g[i], m[i], v[i], c[i]);
+    for (int i = 0; i < N; i++) adam_elem(p[i], g[i], m[i], v[i], c[i]);
 #pragma unroll
     for (int i = 0; i < N; i++) {
-        *pp[i] = p[i];
-        *mp[i] = m[i];
-        *vp[i] = v[i];
+        if (RR_GB_NT) {
+            __builtin_nontemporal_store(p[i], pp[i]);
+            __builtin_nontemporal_store(m[i], mp[i]);
+            __builtin_nontemporal_store(v[i], vp[i]);
+        } else {
+            *pp[i] = p[i];
+            *mp[i] = m[i];
+            *vp[i] = v[i];
+        }
     }
 }
 
@@ -408,7 +421,10 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 // M = 16) are staged into LDS one Gaussian row per wave instruction (coalesced 192-B reads instead
 // of 64 lanes each walking its own 192-B record), and dL/dsh leaves the same way.  Row stride
 // kShStride is odd, so the per-thread row accesses are LDS-bank-conflict free.
-constexpr int kGB = 128;
+#ifndef RR_GB_THREADS
+#define RR_GB_THREADS 128
+#endif
+constexpr int kGB = RR_GB_THREADS;
 constexpr int kShStride = 49;
 
 template <int DEG>
@@ -422,22 +438,46 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     if (stage && a.shs) {
         // flat, coalesced loads of the block's coefficient region(s), all in flight at once, then
         // scattered into the padded LDS rows; j = e / w via a float reciprocal (exact: e < 2^13)
+        // float4 per lane when the region is 16-B aligned (1 KiB per wave instruction instead of 256 B)
         auto stage_in = [&](const float* src, int w, int koff) {
             const int total = nvalid * w;
             const float inv = 1.0f / (float)w;
+            const float* base = src + (size_t)i0 * w;
+            auto put_lds = [&](int e, float x) {
+                const int j = (int)(((float)e + 0.5f) * inv);
+                s_sh[j * kShStride + koff + (e - j * w)] = x;
+            };
+            if (((uintptr_t)base & 15u) == 0) {
+                const int nv = total >> 2;
+                float4 buf[12];
+#pragma unroll
+                for (int q = 0; q < 12; q++) {
+                    const int i = t + q * kGB;
+                    buf[q] = i < nv ? reinterpret_cast<const float4*>(base)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int q = 0; q < 12; q++) {
+                    const int i = t + q * kGB;
+                    if (i < nv) {
+                        put_lds(4 * i, buf[q].x);
+                        put_lds(4 * i + 1, buf[q].y);
+                        put_lds(4 * i + 2, buf[q].z);
+                        put_lds(4 * i + 3, buf[q].w);
+                    }
+                }
+                for (int e = 4 * nv + t; e < total; e += kGB) put_lds(e, base[e]);
+                return;
+            }
             float buf[48];
 #pragma unroll
             for (int q = 0; q < 48; q++) {
                 const int e = t + q * kGB;
-                buf[q] = e < total ? src[(size_t)i0 * w + e] : 0.f;
+                buf[q] = e < total ? base[e] : 0.f;
             }
 #pragma unroll
             for (int q = 0; q < 48; q++) {
                 const int e = t + q * kGB;
-                if (e < total) {
-                    const int j = (int)(((float)e + 0.5f) * inv);
-                    s_sh[j * kShStride + koff + (e - j * w)] = buf[q];
-                }
+                if (e < total) put_lds(e, buf[q]);
             }
         };
         if (!a.raw) {
@@ -450,7 +490,11 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     __syncthreads();
     if (t < nvalid) {
         SmallGrads sg;
+#ifdef RR_GB_SKIP_COMPUTE  // timing probe only: memory phases without the per-Gaussian arithmetic
+        for (int i = 0; i < 11; i++) sg.v[i] = a.gacc[(size_t)(i0 + t) * GACC_STRIDE + i];
+#else
         gauss_bwd_one<DEG>(a, i0 + t, stage ? s_sh + t * kShStride : nullptr, sg);
+#endif
         if (a.use_adam) adam_small(a, i0 + t, sg);
     }
     __syncthreads();
@@ -467,6 +511,60 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
 #define RR_GB_ADAM_BATCH 8
 #endif
             constexpr int kB = RR_GB_ADAM_BATCH;  // Adam elements per batch of loads
+            auto grad_at = [&](int e) {
+                const int j = (int)(((float)e + 0.5f) * inv);
+                return s_sh[j * kShStride + koff + (e - j * w)];
+            };
+            const size_t gb = (size_t)i0 * w;
+            const uintptr_t al = (grp ? ((uintptr_t)(grp->param + gb) | (uintptr_t)(grp->exp_avg + gb) |
+                                         (uintptr_t)(grp->exp_avg_sq + gb))
+                                      : 0u) |
+                                 (dst ? (uintptr_t)(dst + gb) : 0u);
+            if ((al & 15u) == 0) {
+                // float4 per lane: kB / 4 vectors per batch, (param, m, v) loads all in flight
+                constexpr int kV = kB / 4 > 0 ? kB / 4 : 1;
+                const int nv = total >> 2;
+                for (int v0 = t; v0 < nv; v0 += kV * kGB) {
+                    float4 g4[kV], p4[kV], m4[kV], s4[kV];
+#pragma unroll
+                    for (int q = 0; q < kV; q++) {
+                        const int i = min(v0 + q * kGB, nv - 1);  // clamped duplicates are not stored
+                        g4[q] = make_float4(grad_at(4 * i), grad_at(4 * i + 1), grad_at(4 * i + 2), grad_at(4 * i + 3));
+                        if (grp) {
+                            p4[q] = reinterpret_cast<const float4*>(grp->param + gb)[i];
+                            m4[q] = reinterpret_cast<const float4*>(grp->exp_avg + gb)[i];
+                            s4[q] = reinterpret_cast<const float4*>(grp->exp_avg_sq + gb)[i];
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < kV; q++) {
+                        const int i = v0 + q * kGB;
+                        if (i >= nv) break;
+                        if (dst) reinterpret_cast<float4*>(dst + gb)[i] = g4[q];
+                        if (grp) {
+                            adam_elem(p4[q].x, g4[q].x, m4[q].x, s4[q].x, c);
+                            adam_elem(p4[q].y, g4[q].y, m4[q].y, s4[q].y, c);
+                            adam_elem(p4[q].z, g4[q].z, m4[q].z, s4[q].z, c);
+                            adam_elem(p4[q].w, g4[q].w, m4[q].w, s4[q].w, c);
+                            reinterpret_cast<float4*>(grp->param + gb)[i] = p4[q];
+                            reinterpret_cast<float4*>(grp->exp_avg + gb)[i] = m4[q];
+                            reinterpret_cast<float4*>(grp->exp_avg_sq + gb)[i] = s4[q];
+                        }
+                    }
+                }
+                for (int e = 4 * nv + t; e < total; e += kGB) {  // tail (< 4 elements)
+                    const float g = grad_at(e);
+                    put(dst, gb + e, g);
+                    if (grp) {
+                        float p = grp->param[gb + e], m = grp->exp_avg[gb + e], v = grp->exp_avg_sq[gb + e];
+                        adam_elem(p, g, m, v, c);
+                        grp->param[gb + e] = p;
+                        grp->exp_avg[gb + e] = m;
+                        grp->exp_avg_sq[gb + e] = v;
+                    }
+                }
+                return;
+            }
             for (int e0 = t; e0 < total; e0 += kB * kGB) {
                 float g[kB];
                 float* pp[kB];

@@ -39,6 +39,9 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
 #ifndef RR_FWD_S_GROUP
 #define RR_FWD_S_GROUP 4
 #endif
+#ifndef RR_FWD_S_PIPE
+#define RR_FWD_S_PIPE 0
+#endif
     constexpr int G = RR_FWD_S_GROUP;
     const int ntiles = a.gx * a.gy;
     const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
@@ -96,28 +99,12 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
     cv4f_s* recs = (cv4f_s*)a.splats;
     cv4f_s* nrm = (cv4f_s*)a.normals;
 
-    for (int j0 = 0; j0 < n; j0 += G) {
+    // One group of G pairs: their alphas first (independent of T), then the sequential blend.
+    // ra/rb/rc/rn: the pairs' records as wave-uniform values (SGPR operands).
+    auto blend_group = [&](int j0, const v4f (&ra)[G], const v4f (&rb)[G], const v4f (&rc)[G], const v4f (&rn)[G]) {
         bool open[PIX];  // as of the group's start (only used to skip work)
-        uint64_t any_open = 0;
 #pragma unroll
-        for (int k = 0; k < PIX; k++) {
-            open[k] = T[k] > 0.f;
-            any_open |= __builtin_amdgcn_ballot_w64(T[k] > 0.f);
-        }
-        if (!any_open) break;  // every pixel of this wave saturated
-        uint32_t id[G];
-#pragma unroll
-        for (int u = 0; u < G; u++) id[u] = plist[j0 + u];
-#pragma unroll
-        for (int u = 1; u < G; u++) id[u] = (j0 + u < n) ? id[u] : id[0];
-        v4f ra[G], rb[G], rc[G], rn[G];
-#pragma unroll
-        for (int u = 0; u < G; u++) {
-            ra[u] = recs[3 * id[u]];      // x, y, conic.x, conic.y
-            rb[u] = recs[3 * id[u] + 1];  // conic.z, opacity, depth
-            rc[u] = recs[3 * id[u] + 2];  // r, g, b
-            if (AUX) rn[u] = nrm[id[u]];
-        }
+        for (int k = 0; k < PIX; k++) open[k] = T[k] > 0.f;
         // alphas of the group (independent of T): forward.cu:329-336 with blend_power's op order
         float al[G][PIX];
         bool ok[G][PIX];
@@ -172,7 +159,74 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
                 last[k] = blend ? k1 : last[k];
             }
         }
+    };
+    auto wave_open = [&]() {
+        uint64_t any_open = 0;
+#pragma unroll
+        for (int k = 0; k < PIX; k++) any_open |= __builtin_amdgcn_ballot_w64(T[k] > 0.f);
+        return any_open != 0;
+    };
+    // The G ids of group j0 (entries past the list end, readable thanks to kPointListPad, are
+    // replaced by a valid id of the list: their records are loaded but never blended).
+    auto group_ids = [&](int j0, uint32_t (&id)[G], uint32_t fallback) {
+#pragma unroll
+        for (int u = 0; u < G; u++) id[u] = plist[j0 + u];
+#pragma unroll
+        for (int u = 0; u < G; u++) id[u] = (j0 + u < n) ? id[u] : fallback;
+    };
+    auto group_recs = [&](const uint32_t (&id)[G], v4f (&ra)[G], v4f (&rb)[G], v4f (&rc)[G], v4f (&rn)[G]) {
+#pragma unroll
+        for (int u = 0; u < G; u++) {
+            cv4f_s* r = recs + 3 * (size_t)id[u];  // one base, immediate offsets 0 / 16 / 32
+            ra[u] = r[0];  // x, y, conic.x, conic.y
+            rb[u] = r[1];  // conic.z, opacity, depth
+            rc[u] = r[2];  // r, g, b
+            if (AUX) rn[u] = nrm[id[u]];
+        }
+    };
+#if RR_FWD_S_PIPE
+    // Software pipeline over groups: while group j blends, the records of group j+1 and the ids of
+    // group j+2 are in flight.  Scalar loads return out of order (the only wait is lgkmcnt(0)), so
+    // the wait sits at the top of the group and sched barriers keep the compiler from hoisting the
+    // next group's loads above it (which would make the wait cover them too).
+    if (n > 0) {
+        uint32_t idc[G], idn[G];
+        group_ids(0, idc, 0u);
+        const uint32_t id0 = plist[0];
+        v4f ra[G], rb[G], rc[G], rn[G];
+        group_recs(idc, ra, rb, rc, rn);
+        group_ids(G, idn, id0);
+        for (int j0 = 0; j0 < n; j0 += G) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this group's records, next ids
+            __builtin_amdgcn_sched_barrier(0);
+            if (!wave_open()) break;  // every pixel of this wave saturated
+            v4f na[G], nb[G], nc[G], nn[G];
+            uint32_t inn[G];
+            group_recs(idn, na, nb, nc, nn);
+            group_ids(j0 + 2 * G, inn, id0);
+            __builtin_amdgcn_sched_barrier(0);
+            blend_group(j0, ra, rb, rc, rn);
+#pragma unroll
+            for (int u = 0; u < G; u++) {
+                ra[u] = na[u];
+                rb[u] = nb[u];
+                rc[u] = nc[u];
+                rn[u] = nn[u];
+                idn[u] = inn[u];
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // no scalar load outstanding past the loop
     }
+#else
+    for (int j0 = 0; j0 < n; j0 += G) {
+        if (!wave_open()) break;  // every pixel of this wave saturated
+        uint32_t id[G];
+        group_ids(j0, id, plist[j0]);
+        v4f ra[G], rb[G], rc[G], rn[G];
+        group_recs(id, ra, rb, rc, rn);
+        blend_group(j0, ra, rb, rc, rn);
+    }
+#endif
 
     if (a.phase == kBlendPhaseA) {
         // still open somewhere in the tile: leave the raw state (no background) for phase B
