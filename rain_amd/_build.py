@@ -39,7 +39,9 @@ LIBS = {
 # larger than clang's default pragma-unroll size limit; packed-fp32 formation is off for the same
 # reason as rr_blend.hip (it pairs unrelated scalars: 940 v_mov, 244 VGPRs in k_ssim_fwd).
 EXTRA = {
-    "rr_blend_fwd_s.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
+    # rr_blend_fwd_s.hip: machine sinking would move the software-pipelined next-group record loads
+    # below the blend (next to their use in the loop latch), serialising them again
+    "rr_blend_fwd_s.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-mllvm", "-disable-machine-sink"],
     "rr_blend.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
     "loss.hip": ["-mllvm", "-pragma-unroll-threshold=200000",
                  "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
