@@ -275,6 +275,10 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *   "sort_max_rounds" r   cap on 64-item rounds per wave in a sort unit, 1..16 (default 16).
  * Results are identical for every setting.  Unknown keys return RR_ERR_ARG. */
 int rr_set_tuning(const char* key, int value);
+/* Diagnostics: device buffer of >= 8 * 8 * tiles u32 receiving one timing record per forward-blend
+ * wave (start / end s_memrealtime, tile, pairs walked, list length, phase) — only builds compiled
+ * with -DRR_FWD_TRACE=1 write it (tools/fwd_trace.py); NULL turns it off. */
+int rr_debug_set_fwd_trace(void* dev_buf);
 
 /* Tuning knob (diagnostics / tests): early-stop binning bins L / split_denominator pairs in phase A
  * (1 = one phase) for frames of at least min_pairs pairs; 0 restores a default (3, 2^16).  Results

@@ -24,7 +24,7 @@ CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-W
             "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 LIBS = {
-    "librain_raster.so": ["rr_forward.hip", "rr_blend_fwd.hip", "rr_blend_fwd_s.hip", "rr_blend.hip", "rr_backward.hip", "rr_sort.hip",
+    "librain_raster.so": ["rr_forward.hip", "rr_blend_fwd_s.hip", "rr_blend.hip", "rr_backward.hip", "rr_sort.hip",
                           "rr_api.hip"],
     "librain_loss.so": ["loss.hip"],
     "librain_knn.so": ["knn.hip"],

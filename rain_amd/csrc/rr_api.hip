@@ -814,6 +814,11 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves) {
     return RR_OK;
 }
 
+int rr_debug_set_fwd_trace(void* dev_buf) {
+    set_fwd_trace(dev_buf);
+    return RR_OK;
+}
+
 int rr_set_tuning(const char* key, int value) {
     if (set_tuning(key, value) != 0) return fail(RR_ERR_ARG, std::string("unknown tuning key: ") + (key ? key : "(null)"));
     return RR_OK;

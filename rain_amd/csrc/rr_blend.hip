@@ -1,5 +1,5 @@
 // rr_blend.hip — per-tile alpha blending backward (backward.cu:389-547); the forward blend lives in
-// rr_blend_fwd.hip (packed fp32 math, compiled with packed ops enabled).
+// rr_blend_fwd_s.hip.
 //
 // CDNA4 mapping.  A 16x16 tile is processed by NW wave64s (NW = 1, 2 or 4, chosen per kernel at
 // run time, see rr_set_blend_config), each lane owning PPL = 4/NW pixels of one column: thread t
@@ -24,10 +24,6 @@
 
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
-
-#ifndef RR_BWD_FOLD
-#define RR_BWD_FOLD 1
-#endif
 
 namespace rr {
 
@@ -112,24 +108,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             const float4 Bv = s_b[j];
             float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
             bool any = false;
-#if RR_BWD_FOLD
-            // The conic-side terms are linear in u = G * dL/dalpha, and a lane's PPL pixels share
-            // its column (dx): per pixel only S_u, S_u.dy, S_u.dy^2 are accumulated, and the six
-            // components follow once per lane and pair (g0 = o dx S_u, g1 = o S_udy, g2 = dx g0,
-            // g3 = dx g1, g4 = o S_udy2, g5 = S_u with o the opacity): 5 VALU per pixel instead of 11.
+            // The conic-side terms are linear in v = e * dL/dalpha with e = opacity G (the unclamped
+            // alpha), and a lane's PPL pixels share its column (dx): per pixel only S_v, S_v.dy,
+            // S_v.dy^2 are accumulated, and the six components follow once per lane and pair
+            // (g0 = S_v dx, g1 = S_vdy, g2 = dx g0, g3 = dx g1, g4 = S_vdy2, g5 = S_v / opacity):
+            // 5 VALU per pixel instead of 11.
             const float dx = A.x - pfx;
-            float su = 0.f, sudy = 0.f, sudy2 = 0.f;
-#endif
+            const P2X px2 = blend_p2_x(A.z, A.w, dx);  // identical to the forward's values
+            float sv = 0.f, svdy = 0.f, svdy2 = 0.f;
 #pragma unroll
             for (int q = 0; q < PPL; q++) {
-#if !RR_BWD_FOLD
-                const float dx = A.x - pfx;
-#endif
                 const float dy = A.y - (float)(py0 + 4 * q);
-                const float power = blend_power(A, Bv, dx, dy);  // identical to the forward's value
-                const float G = blend_G(power);
-                const float alpha = fminf(0.99f, Bv.y * G);
-                const bool act = contributor < last[q] && power <= 0.0f && alpha >= 1.0f / 255.0f;
+                const float p2 = blend_p2(px2, Bv.x, dy);
+                const float e = __builtin_amdgcn_exp2f(p2 + Bv.y);
+                const float alpha = fminf(0.99f, e);
+                const bool act = contributor < last[q] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
                 if (act) {
                     any = true;
                     const float one_m = 1.f - alpha;
@@ -141,48 +134,26 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     g6 += dchannel_dcolor * dp0[q];
                     g7 += dchannel_dcolor * dp1[q];
                     g8 += dchannel_dcolor * dp2[q];
-#if RR_BWD_FOLD
                     R[q] = __builtin_fmaf(la[q], lcdp[q] - R[q], R[q]);  // la lcdp + (1 - la) R
-#else
-                    R[q] = la[q] * lcdp[q] + (1.f - la[q]) * R[q];
-#endif
                     lcdp[q] = cdp;
                     la[q] = alpha;
                     // dL/dalpha = T_i (c - accum_rec) . dL/dpix - T_final (bg . dL/dpix) / (1 - alpha)
                     const float dL_dalpha = (cdp - R[q]) * T[q] + tfbg[q] * inv;
-#if RR_BWD_FOLD
-                    const float u = G * dL_dalpha;
-                    const float udy = u * dy;
-                    su += u;
-                    sudy += udy;
-                    sudy2 = __builtin_fmaf(udy, dy, sudy2);
-#else
-                    const float dL_dG = Bv.y * dL_dalpha;
-                    // dG/d(delta) = -G (conic . delta): the conic is the same for every pixel of
-                    // the pair, so only Sx = sum dL_dG G dx and Sy = sum dL_dG G dy are summed per
-                    // pixel, and the flush forms -(conic . S) once per (tile, Gaussian); it also
-                    // applies the constant factors (0.5 W, 0.5 H, -0.5)
-                    const float tx = dL_dG * (G * dx), ty = dL_dG * (G * dy);
-                    g0 += tx;
-                    g1 += ty;
-                    g2 += tx * dx;
-                    g3 += tx * dy;
-                    g4 += ty * dy;
-                    g5 += G * dL_dalpha;
-#endif
+                    const float v = e * dL_dalpha;
+                    const float vdy = v * dy;
+                    sv += v;
+                    svdy += vdy;
+                    svdy2 = __builtin_fmaf(vdy, dy, svdy2);
                 }
             }
-#if RR_BWD_FOLD
             if (any) {
-                const float osu = Bv.y * su;
-                g0 = osu * dx;
-                g1 = Bv.y * sudy;
+                g0 = sv * dx;
+                g1 = svdy;
                 g2 = g0 * dx;
                 g3 = g1 * dx;
-                g4 = Bv.y * sudy2;
-                g5 = su;
+                g4 = svdy2;
+                g5 = sv * s_c[j].w;  // 1 / opacity
             }
-#endif
             float* sg = &s_g[w][j * NGRAD];
             float t0 = 0.f, t1 = 0.f, t2 = 0.f;
             if (__ballot(any) != 0ull) wave_sum9(g0, g1, g2, g3, g4, g5, g6, g7, g8, t0, t1, t2);
@@ -206,8 +177,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                         sx += s_g[i][pair * NGRAD];
                         sy += s_g[i][pair * NGRAD + 1];
                     }
-                    const float cw = s_a[pair].w;
-                    v = comp == 0 ? -(s_a[pair].z * sx + cw * sy) * ddelx_dx : -(s_b[pair].x * sy + cw * sx) * ddely_dy;
+                    float ccx, ccy, ccz;
+                    splat_conic(s_a[pair], s_b[pair], ccx, ccy, ccz);
+                    v = comp == 0 ? -(ccx * sx + ccy * sy) * ddelx_dx : -(ccz * sy + ccy * sx) * ddely_dy;
                 } else {
                     v *= comp <= 4 ? -0.5f : 1.f;
                 }
@@ -266,13 +238,9 @@ __global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __re
 }
 
 namespace {
-int g_fwd_waves = 0;
 int g_bwd_waves = 0;
 int g_bwd_order = -1;  // -1: RAIN_BWD_TILE_ORDER or the default (on)
-int g_fwd_b_waves = -1;  // -1: RAIN_BLEND_FWD_B_WAVES or the default
 int g_fwd_order = -1;  // -1: RAIN_FWD_TILE_ORDER or the default (off)
-int g_fwd_impl = -1;  // -1: RAIN_FWD_IMPL or the default
-int g_fwd_impl_b = 2;
 int g_fwd_s_waves = 2, g_fwd_s_b_waves = 4;
 int env_waves(const char* name, int dflt) {
     const char* s = std::getenv(name);
@@ -282,20 +250,13 @@ int env_waves(const char* name, int dflt) {
 }
 }  // namespace
 
-// Defaults: measured on MI355X (profiles/, DESIGN.md §Blend kernels).  The forward blend
-// (rr_blend_fwd.hip) runs 1 or 2 waves per tile (4 or 2 pixels per lane, packed in pairs).
-constexpr int kFwdWavesDefault = 2;
+// Defaults: measured on MI355X (profiles/).  The forward blend (rr_blend_fwd_s.hip)
+// runs 2 waves per tile in phase A (2 pixels per lane), 4 in phase B (1 pixel per lane).
 constexpr int kBwdWavesDefault = 1;
-constexpr int kFwdBWavesDefault = 4;
 
 void set_blend_config(int fwd_waves, int bwd_waves) {
-    g_fwd_waves = fwd_waves;
+    g_fwd_s_waves = (fwd_waves == 1 || fwd_waves == 4) ? fwd_waves : 2;
     g_bwd_waves = bwd_waves;
-}
-
-int blend_fwd_waves() {
-    const int nw = g_fwd_waves ? g_fwd_waves : env_waves("RAIN_BLEND_FWD_WAVES", kFwdWavesDefault);
-    return nw == 1 ? 1 : 2;
 }
 
 bool bwd_tile_order() {
@@ -306,30 +267,15 @@ bool bwd_tile_order() {
     return g_bwd_order != 0;
 }
 
-int blend_fwd_b_waves() {
-    if (g_fwd_b_waves < 0) {
-        const char* s = std::getenv("RAIN_BLEND_FWD_B_WAVES");
-        g_fwd_b_waves = s ? std::atoi(s) : kFwdBWavesDefault;
-    }
-    return g_fwd_b_waves == 4 ? 4 : 0;
-}
-
 bool fwd_tile_order() {
     if (g_fwd_order < 0) {
         // default off: list length is not what a forward tile costs (saturation is); measured
-        // 1.585 vs 1.581 ms per training step with / without
+        // 1.585 vs 1.581 ms per training step with / without, and in a wave-timing trace of phase A
+        // (tools/fwd_trace.py) the duration of a tile is uncorrelated with its list length (-0.07)
         const char* s = std::getenv("RAIN_FWD_TILE_ORDER");
         g_fwd_order = s ? (std::atoi(s) != 0) : 0;
     }
     return g_fwd_order != 0;
-}
-
-int blend_fwd_impl(bool phase_b) {
-    if (g_fwd_impl < 0) {
-        const char* s = std::getenv("RAIN_FWD_IMPL");
-        g_fwd_impl = s ? std::atoi(s) : 2;
-    }
-    return phase_b ? g_fwd_impl_b : g_fwd_impl;
 }
 
 int blend_fwd_s_waves(bool phase_b) { return phase_b ? g_fwd_s_b_waves : g_fwd_s_waves; }
@@ -343,11 +289,8 @@ int set_tuning(const char* key, int value) {
     const std::string k(key);
     if (k == "bwd_tile_order") g_bwd_order = value != 0;
     else if (k == "fwd_tile_order") g_fwd_order = value != 0;
-    else if (k == "fwd_b_waves") g_fwd_b_waves = value ? 4 : 0;
-    else if (k == "fwd_waves") g_fwd_waves = value;
-    else if (k == "fwd_impl") g_fwd_impl = (value >= 0 && value <= 2) ? value : 2;
-    else if (k == "fwd_impl_b") g_fwd_impl_b = (value >= 0 && value <= 2) ? value : 2;
-    else if (k == "fwd_s_waves") g_fwd_s_waves = (value == 1 || value == 4) ? value : 2;
+    else if (k == "fwd_b_waves") g_fwd_s_b_waves = value ? 4 : g_fwd_s_waves;
+    else if (k == "fwd_waves" || k == "fwd_s_waves") g_fwd_s_waves = (value == 1 || value == 4) ? value : 2;
     else if (k == "fwd_s_b_waves") g_fwd_s_b_waves = (value == 1 || value == 2) ? value : 4;
     else if (k == "bwd_waves") g_bwd_waves = value;
     else if (k == "sort_min_units") set_sort_min_units(value);

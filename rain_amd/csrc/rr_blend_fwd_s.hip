@@ -1,15 +1,16 @@
 // rr_blend_fwd_s.hip — per-tile front-to-back alpha blend, forward (forward.cu:251-369), scalar-
 // record / scalar-arithmetic variant.
 //
-// Measured on MI355X (tools/valu_probe.hip, profiles/r02_*): the forward blend is VALU-throughput
-// bound (SQ_ACTIVE_INST_VALU ~0.8 of SIMD cycles), and a packed fp32 op (v_pk_fma_f32, 2 lanes of
-// work) costs ~2x a plain v_fma_f32 — packing buys no throughput and its operand shuffles (v_mov
-// of scalars into register pairs) cost ~14% of the loop.  So this kernel is written for the
-// scalar VALU with as few vector instructions per (pixel, pair) as the reference's arithmetic
-// allows:
+// Written for the scalar VALU with as few vector instructions per (pixel, pair) as possible (a
+// packed v_pk_fma_f32 costs ~2x a plain v_fma_f32 on gfx950 and needs operand shuffles, so packing
+// buys nothing here):
 //   * every lane of a wave blends the same pair at the same time, so the pair's id and 48-B Splat
 //     are wave-uniform: they are read with s_load through the constant address space and feed the
-//     VALU ops as scalar operands (no LDS staging, no broadcast VGPRs, no barrier per round);
+//     VALU ops as scalar operands (no LDS staging, no broadcast VGPRs, no barrier per round); a
+//     group's records and the next group's ids leave in one batch (RR_FWD_S_BATCH), one
+//     scalar-memory round trip per group;
+//   * alpha in log2 units from the pre-scaled conic (rr_common.hpp blend_p2): per pixel 3 fma-class
+//     ops, an add of log2(opacity) and one exp2;
 //   * a lane owns PIX pixels of one column (rows l/16 + 4k): the x-terms of the falloff are
 //     computed once per lane and pair;
 //   * no per-pixel "open" flag: a saturated pixel keeps -T (T >= 1e-4 > 0 while open), so every
@@ -17,8 +18,8 @@
 //     one select with a -|x| source modifier); the masks of the compares combine on the scalar unit;
 //   * a pixel row k whose 16 x 4 pixels are all closed (or that no lane reaches with alpha >=
 //     1/255) skips the pair's blend with a uniform branch; a wave leaves when all its pixels closed.
-// The arithmetic (blend_power's op order, explicit fmas, T*(1-alpha), wgt = alpha*T) is the packed
-// kernel's, element for element, so the two produce bitwise-identical images and image state.
+// Measured (tools/fwd_trace.py, per-wave s_memrealtime records): phase A runs ~6 waves per SIMD
+// for ~2/3 of its span, then drains; a wave walks ~100 pairs (its 8 rows saturate) in ~40 us.
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
@@ -34,13 +35,19 @@ typedef __attribute__((address_space(4))) const u2v cu2v_s;
 // l/16 + 4*(w*PIX + k), k < PIX.  G pairs per group (their alphas formed before the blend).
 template <int NW, bool AUX>
 __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
-#pragma clang fp contract(off)  // blend_power's rounding: every fma below is explicit
+#pragma clang fp contract(off)  // blend_p2's rounding: every fma below is explicit
     constexpr int PIX = 4 / NW;
 #ifndef RR_FWD_S_GROUP
-#define RR_FWD_S_GROUP 4
+#define RR_FWD_S_GROUP 3
 #endif
 #ifndef RR_FWD_S_PIPE
 #define RR_FWD_S_PIPE 0
+#endif
+#ifndef RR_FWD_S_BATCH
+#define RR_FWD_S_BATCH 1  // measured: 0.208 vs 0.222 ms/step (G = 3 vs the unbatched G = 4)
+#endif
+#ifndef RR_FWD_TRACE
+#define RR_FWD_TRACE 0
 #endif
     constexpr int G = RR_FWD_S_GROUP;
     const int ntiles = a.gx * a.gy;
@@ -95,6 +102,10 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
         }
     }
     const int n = (int)(hi - lo);
+#if RR_FWD_TRACE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    int walked = 0;
+#endif
     cu32_s* plist = (cu32_s*)a.point_list + lo;  // readable kPointListPad entries past any list end
     cv4f_s* recs = (cv4f_s*)a.splats;
     cv4f_s* nrm = (cv4f_s*)a.normals;
@@ -105,29 +116,22 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
         bool open[PIX];  // as of the group's start (only used to skip work)
 #pragma unroll
         for (int k = 0; k < PIX; k++) open[k] = T[k] > 0.f;
-        // alphas of the group (independent of T): forward.cu:329-336 with blend_power's op order
+        // alphas of the group (independent of T): forward.cu:329-336 as blend_p2 (rr_common.hpp)
         float al[G][PIX];
         bool ok[G][PIX];
         uint64_t okm[G][PIX];  // ok as a wave mask (ballots of the compares themselves: v_cmp into SGPRs)
-        float cxdx2[G], wdx[G];
+        P2X px2[G];
 #pragma unroll
-        for (int u = 0; u < G; u++) {
-            const float dx = ra[u].x - pfx;
-            cxdx2[u] = (ra[u].z * dx) * dx;
-            wdx[u] = ra[u].w * dx;
-        }
+        for (int u = 0; u < G; u++) px2[u] = blend_p2_x(ra[u].z, ra[u].w, ra[u].x - pfx);
 #pragma unroll
         for (int k = 0; k < PIX; k++) {
 #pragma unroll
             for (int u = 0; u < G; u++) {
-                const float dy = ra[u].y - pfy[k];
-                const float tq = __builtin_fmaf(rb[u].x * dy, dy, cxdx2[u]);
-                const float power = __builtin_fmaf(-0.5f, tq, -(wdx[u] * dy));
-                const float g = __builtin_amdgcn_exp2f(power * kLog2e);
-                const float a99 = fminf(0.99f, rb[u].y * g);
+                const float p2 = blend_p2(px2[u], rb[u].x, ra[u].y - pfy[k]);
+                const float a99 = fminf(0.99f, __builtin_amdgcn_exp2f(p2 + rb[u].y));
                 // non-short-circuit: both compares become lane masks combined on the scalar unit
-                ok[u][k] = (power <= 0.0f) & (a99 >= 1.0f / 255.0f) & open[k];
-                okm[u][k] = __builtin_amdgcn_ballot_w64(power <= 0.0f) & __builtin_amdgcn_ballot_w64(a99 >= 1.0f / 255.0f) &
+                ok[u][k] = (p2 <= 0.0f) & (a99 >= 1.0f / 255.0f) & open[k];
+                okm[u][k] = __builtin_amdgcn_ballot_w64(p2 <= 0.0f) & __builtin_amdgcn_ballot_w64(a99 >= 1.0f / 255.0f) &
                             __builtin_amdgcn_ballot_w64(open[k]);
                 al[u][k] = a99;
             }
@@ -217,14 +221,55 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // no scalar load outstanding past the loop
     }
+#elif RR_FWD_S_BATCH
+    // Per group one scalar-memory round trip: the group's records and the next group's ids are
+    // issued together (a sched barrier keeps the compiler from interleaving them with the blend,
+    // which would put an lgkmcnt(0) wait - covering every load in flight - before each record).
+    if (n > 0) {
+        const uint32_t id0 = plist[0];
+        uint32_t idc[G];
+        group_ids(0, idc, id0);
+        for (int j0 = 0; j0 < n; j0 += G) {
+            if (!wave_open()) break;  // every pixel of this wave saturated
+#if RR_FWD_TRACE
+            walked = j0 + G;
+#endif
+            v4f ra[G], rb[G], rc[G], rn[G];
+            uint32_t idn[G];
+            group_recs(idc, ra, rb, rc, rn);
+            group_ids(j0 + G, idn, id0);
+            __builtin_amdgcn_sched_barrier(0);
+            blend_group(j0, ra, rb, rc, rn);
+#pragma unroll
+            for (int u = 0; u < G; u++) idc[u] = idn[u];
+        }
+    }
 #else
     for (int j0 = 0; j0 < n; j0 += G) {
         if (!wave_open()) break;  // every pixel of this wave saturated
+#if RR_FWD_TRACE
+        walked = j0 + G;
+#endif
         uint32_t id[G];
         group_ids(j0, id, plist[j0]);
         v4f ra[G], rb[G], rc[G], rn[G];
         group_recs(id, ra, rb, rc, rn);
         blend_group(j0, ra, rb, rc, rn);
+    }
+#endif
+#if RR_FWD_TRACE
+    if (a.trace && lane == 0) {  // timing record of this wave (tools/fwd_trace.py)
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const int ntl = a.gx * a.gy;
+        uint32_t* r = a.trace + 8 * ((size_t)(a.phase == kBlendPhaseB ? 4 * ntl : 0) + (size_t)blockIdx.x * NW + w);
+        r[0] = (uint32_t)t_start;
+        r[1] = (uint32_t)(t_start >> 32);
+        r[2] = (uint32_t)t_end;
+        r[3] = (uint32_t)(t_end >> 32);
+        r[4] = (uint32_t)tile;
+        r[5] = (uint32_t)min(walked, n);
+        r[6] = (uint32_t)n;
+        r[7] = (uint32_t)a.phase | ((uint32_t)w << 8) | ((uint32_t)NW << 16);
     }
 #endif
 
@@ -295,7 +340,14 @@ __global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
     }
 }
 
-void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st) {
+namespace {
+uint32_t* g_fwd_trace = nullptr;
+}
+void set_fwd_trace(void* dev_buf) { g_fwd_trace = static_cast<uint32_t*>(dev_buf); }
+
+void launch_blend_fwd_s(const BlendFwdArgs& a_in, int waves, hipStream_t st) {
+    BlendFwdArgs a = a_in;
+    a.trace = g_fwd_trace;
     const int T = a.gx * a.gy;
     if (T == 0) return;
     const bool aux = a.out_normal != nullptr;
@@ -309,6 +361,11 @@ void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st) {
         if (aux) k_blend_fwd_s<2, true><<<T, 128, 0, st>>>(a);
         else k_blend_fwd_s<2, false><<<T, 128, 0, st>>>(a);
     }
+}
+
+void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
+    if (a.gx * a.gy == 0) return;
+    launch_blend_fwd_s(a, blend_fwd_s_waves(a.phase == kBlendPhaseB), st);
 }
 
 }  // namespace rr

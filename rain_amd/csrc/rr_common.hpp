@@ -5,9 +5,12 @@
 //     Gaussian, so a (tile, Gaussian) pair costs one 4-B id load plus three 16-B loads of one
 //     record, instead of the reference's id + xy + conic_opacity + per-use rgb/depth gathers
 //     (forward.cu:310-349).
-//       a = {x_pix, y_pix, conic.x, conic.y}
-//       b = {conic.z, opacity, depth(view z), 0}
-//       c = {r, g, b, 0}        (SH colour, or colors_precomp copied in)
+//       a = {x_pix, y_pix, qa, qb}
+//       b = {qc, log2(opacity), depth(view z), opacity}
+//       c = {r, g, b, 1/opacity}   (SH colour, or colors_precomp copied in)
+//     with the conic pre-scaled into the exponent's log2 units (blend_p2): qa = -log2(e)/2 conic.x,
+//     qb = -log2(e) conic.y, qc = -log2(e)/2 conic.z, so a pixel's alpha costs 3 fma-class ops and
+//     one exp2 of (p2 + log2 opacity) instead of the reference's 6 ops, a scaling and a multiply.
 //   * Backward accumulators: 16 floats (one 64-B line) per Gaussian, components
 //     0..1 dL/dmean2D(ndc), 2..4 dL/dconic (x,y,w), 5 dL/dopacity, 6..8 dL/dcolor.
 #pragma once
@@ -339,18 +342,34 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
     return x < r ? x * (q + 1) + s : r * (q + 1) + (x - r) * q + s;
 }
 
-// Falloff exponent of a (pair, pixel) (forward.cu:329-331 / backward.cu:481-486) with a fixed op
-// sequence — explicit fmas, no contraction — shared by the forward (packed, rr_blend_fwd.hip) and
-// backward (scalar) blends, so both take bitwise-identical alpha decisions.  dx, dy = mean - pixel.
-__device__ __forceinline__ float blend_power(float4 A, float4 Bv, float dx, float dy) {
-#pragma clang fp contract(off)
-    const float cxdx2 = (A.z * dx) * dx;
-    const float t = __builtin_fmaf(Bv.x * dy, dy, cxdx2);
-    const float u = (A.w * dx) * dy;
-    return __builtin_fmaf(-0.5f, t, -u);
-}
+// Falloff of a (pair, pixel) (forward.cu:329-336 / backward.cu:481-491) in log2 units:
+//   power = -0.5 (cx dx^2 + cz dy^2) - cy dx dy,   p2 = log2(e) power = qa dx^2 + qb dx dy + qc dy^2,
+//   alpha = min(0.99, opacity exp(power)) = min(0.99, exp2(p2 + log2 opacity)),
+// evaluated with one fixed op sequence (blend_p2_x per pair and lane, then blend_p2 per pixel;
+// explicit fmas, no contraction) by both blend kernels, so forward and backward take
+// bitwise-identical alpha decisions.  p2 <= 0 <=> power <= 0.  dx, dy = mean - pixel.
 constexpr float kLog2e = 1.44269504088896340736f;
-__device__ __forceinline__ float blend_G(float power) { return __builtin_amdgcn_exp2f(power * kLog2e); }
+constexpr float kQHalf = -0.5f * kLog2e;          // qa = kQHalf cx, qc = kQHalf cz
+constexpr float kQFull = -kLog2e;                 // qb = kQFull cy
+constexpr float kQHalfInv = -1.38629436111989061883f;  // -2 ln 2: cx = kQHalfInv qa (back-conversion, <= 2 ulp)
+constexpr float kQFullInv = -0.69314718055994530942f;  // -ln 2
+struct P2X {  // the x terms of p2, once per (pair, lane)
+    float ax, bx;
+};
+__device__ __forceinline__ P2X blend_p2_x(float qa, float qb, float dx) {
+#pragma clang fp contract(off)
+    return P2X{(qa * dx) * dx, qb * dx};
+}
+__device__ __forceinline__ float blend_p2(P2X x, float qc, float dy) {
+    return __builtin_fmaf(__builtin_fmaf(qc, dy, x.bx), dy, x.ax);
+}
+// The raw conic (cx, cy, cz) and opacity of a record, for the tile culling and the backward's
+// conic-gradient flush.
+__device__ __forceinline__ void splat_conic(float4 a, float4 b, float& cx, float& cy, float& cz) {
+    cx = a.z * kQHalfInv;
+    cy = a.w * kQFullInv;
+    cz = b.x * kQHalfInv;
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 

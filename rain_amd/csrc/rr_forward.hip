@@ -90,9 +90,9 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
     }
     const float opacity = a.raw ? act_opacity(a.opacities[idx]) : a.opacities[idx];
     Splat s;
-    s.a = make_float4(px, py, cx, cy);
-    s.b = make_float4(cz, opacity, p_view.z, 0.f);
-    s.c = rgb;
+    s.a = make_float4(px, py, kQHalf * cx, kQFull * cy);
+    s.b = make_float4(kQHalf * cz, __builtin_amdgcn_logf(opacity), p_view.z, opacity);
+    s.c = make_float4(rgb.x, rgb.y, rgb.z, opacity > 0.f ? 1.0f / opacity : 0.f);
     a.splats[idx] = s;
     if (a.normals) a.normals[idx] = gaussian_normal(sc, q, a.view, p_view);
     a.radii[idx] = radius;
@@ -288,17 +288,19 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                 const uint32_t g = idx_sorted[s];
                 const int r = radii[g];
                 const float4 A = splats[g].a;
+                const float4 Bv = splats[g].b;
+                float ccx, ccy, ccz;
+                splat_conic(A, Bv, ccx, ccy, ccz);
                 int x0, y0, x1, y1;
                 tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
                 const bool any_open =
                     !filter || (sat[y1 * sw + x1] + sat[y0 * sw + x0] - sat[y0 * sw + x1] - sat[y1 * sw + x0]) > 0;
                 if (any_open) {
-                    const float qmax = cull ? cull_qmax(splats[g].b.y) : 0.f;
-                    const float cz = splats[g].b.x;
+                    const float qmax = cull ? cull_qmax(Bv.w) : 0.f;
                     uint32_t pos = a;
                     for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && pos < hi; Y++) {
                         int l0, h0, l1, h1, Xa, Xb;
-                        bin_row_spans(A.x, A.y, A.z, A.w, cz, qmax, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
+                        bin_row_spans(A.x, A.y, ccx, ccy, ccz, qmax, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
                         bin_cols(l0, h0, l1, h1, Xa, Xb);
                         uint32_t c = 0;
                         for (int X = Xa; X < Xb; X++) c += bin_mask(X, l0, h0, l1, h1) != 0u ? 1u : 0u;

@@ -55,6 +55,7 @@ struct BlendFwdArgs {
     const float4* normals;  // aux normal output (RR_FLAG_AUX_NORMAL): per-Gaussian normals and
     float* out_normal;      // the blended normal map [3,H,W]; both null otherwise
     const uint32_t* order;  // [T] tile of each workgroup, longest list first; null: XCD order
+    uint32_t* trace;        // RR_FWD_TRACE builds only: per-wave timing records (rr_debug_set_fwd_trace)
 };
 
 struct BlendBwdArgs {
@@ -186,14 +187,10 @@ void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
 namespace rr {
 // Tuning knob: waves per tile (1, 2, 4) of the blend kernels; 0 = default / env override.
 void set_blend_config(int fwd_waves, int bwd_waves);
-int blend_fwd_waves();    // 1 or 2 (forward blend, rr_blend_fwd.hip)
-int blend_fwd_b_waves();  // phase B of early-stop binning: 4 (one pixel per lane) or as phase A
 bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_set_tuning "bwd_tile_order")
 bool fwd_tile_order();  // forward blends dispatch tiles longest list first (rr_set_tuning "fwd_tile_order")
-// forward blend implementation (rr_set_tuning "fwd_impl"): 0 packed fp32 + LDS-staged records,
-// 1 packed fp32 + scalar-loaded records, 2 scalar fp32 + scalar-loaded records (rr_blend_fwd_s.hip)
-int blend_fwd_impl(bool phase_b);  // phase B of early-stop binning: "fwd_impl_b"
-int blend_fwd_s_waves(bool phase_b);  // waves per tile of impl 2 ("fwd_s_waves" / "fwd_s_b_waves")
+int blend_fwd_s_waves(bool phase_b);  // waves per tile of the forward blend ("fwd_s_waves" / "fwd_b_waves")
+void set_fwd_trace(void* dev_buf);
 void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
