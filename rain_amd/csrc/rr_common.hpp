@@ -88,47 +88,64 @@ __device__ __forceinline__ float cull_qmax(float opacity) {
 // x-projection is one interval [xl, xr] and the row's touched tiles are the contiguous columns
 // whose pixel-centre span [16 tx, 16 tx + 15] meets it.  xr over the band is the concave
 // x_right(y) = (-cb y + sqrt(ca qmax - D y^2)) / ca maximised at y clamped to the ellipse's
-// rightmost point y* = -cb xmax / cc (mirror for xl).  Returns the column range [*lo, *hi)
-// clipped to the bounding rect [x0, x1); empty rows give lo >= hi.  Slack of 1e-3 px + 1e-5
-// relative keeps it conservative against rounding (the q margin of cull_qmax covers the blend).
-__device__ __forceinline__ void cull_row_span(float mx, float my, float ca, float cb, float cc, float qmax, int ty,
-                                              int x0, int x1, int* lo, int* hi) {
+// rightmost point y* = -cb xmax / cc (mirror for xl).  Slack of 1e-3 px + 1e-5 relative keeps
+// it conservative against rounding — including that of the hardware square root and reciprocal
+// (<= 1-2 ulp) used here — and the q margin of cull_qmax covers the blend's.
+// The per-Gaussian part (cull_setup) is computed once; cull_row_span is the per-row part.  The
+// preprocess (counting) and the duplicate (emitting) evaluate both on the same inputs with the
+// same op sequence (no contraction), so they agree on every Gaussian's pair count bit for bit.
+struct CullEll {
+    float mx, my, ca, cb, qmax, D, yext, xmax, ystar, inv_ca, slack_y, slack_x;
+    int mode;  // 0 ellipse, 1 not a proper ellipse (keep the rect row), 2 opacity < 1/255 everywhere (empty)
+};
+__device__ __forceinline__ CullEll cull_setup(float mx, float my, float ca, float cb, float cc, float qmax) {
 #pragma clang fp contract(off)
-    const float D = ca * cc - cb * cb;
-    if (!(ca > 0.f && cc > 0.f && D > 0.f)) {  // not a proper ellipse: keep the whole rect row
+    CullEll e;
+    e.mx = mx;
+    e.my = my;
+    e.ca = ca;
+    e.cb = cb;
+    e.qmax = qmax;
+    e.D = ca * cc - cb * cb;
+    e.mode = !(ca > 0.f && cc > 0.f && e.D > 0.f) ? 1 : !(qmax > 0.f) ? 2 : 0;
+    const float qd = qmax * __builtin_amdgcn_rcpf(e.D);
+    e.yext = __builtin_amdgcn_sqrtf(ca * qd);
+    e.xmax = __builtin_amdgcn_sqrtf(cc * qd);
+    e.ystar = -cb * e.xmax * __builtin_amdgcn_rcpf(cc);  // rightmost point; leftmost is at -ystar
+    e.inv_ca = __builtin_amdgcn_rcpf(ca);
+    e.slack_y = 1e-3f + 1e-5f * e.yext;
+    e.slack_x = 1e-3f + 1e-5f * e.xmax;
+    return e;
+}
+// Column range [*lo, *hi) of tile row ty, clipped to the bounding rect [x0, x1); empty rows give
+// lo >= hi.
+__device__ __forceinline__ void cull_row_span(const CullEll& e, int ty, int x0, int x1, int* lo, int* hi) {
+#pragma clang fp contract(off)
+    if (e.mode == 1) {
         *lo = x0;
         *hi = x1;
         return;
     }
-    if (!(qmax > 0.f)) {  // opacity below 1/255 everywhere: the blend skips every pixel
+    const float by0 = (float)(ty * TILE_Y) - e.my, by1 = by0 + (float)(TILE_Y - 1);
+    const float ya = fmaxf(by0, -e.yext), yb = fminf(by1, e.yext);
+    if (e.mode == 2 || ya > yb + e.slack_y) {
         *lo = x1;
         *hi = x1;
         return;
     }
-    const float yext = sqrtf(ca * qmax / D);
-    const float by0 = (float)(ty * TILE_Y) - my, by1 = by0 + (float)(TILE_Y - 1);
-    const float slack_y = 1e-3f + 1e-5f * yext;
-    const float ya = fmaxf(by0, -yext), yb = fminf(by1, yext);
-    if (ya > yb + slack_y) {
-        *lo = x1;
-        *hi = x1;
-        return;
-    }
-    const float xmax = sqrtf(cc * qmax / D);
-    const float ystar = -cb * xmax / cc;               // rightmost point; leftmost is at -ystar
-    const float yr = fminf(fmaxf(ystar, ya), yb);
-    const float yl = fminf(fmaxf(-ystar, ya), yb);
-    const float xr = (-cb * yr + sqrtf(fmaxf(ca * qmax - D * yr * yr, 0.f))) / ca;
-    const float xl = (-cb * yl - sqrtf(fmaxf(ca * qmax - D * yl * yl, 0.f))) / ca;
+    const float yr = fminf(fmaxf(e.ystar, ya), yb);
+    const float yl = fminf(fmaxf(-e.ystar, ya), yb);
+    const float cq = e.ca * e.qmax;
+    const float xr = (-e.cb * yr + __builtin_amdgcn_sqrtf(fmaxf(cq - e.D * yr * yr, 0.f))) * e.inv_ca;
+    const float xl = (-e.cb * yl - __builtin_amdgcn_sqrtf(fmaxf(cq - e.D * yl * yl, 0.f))) * e.inv_ca;
     if (!(xr >= xl) || !(xr - xl < 3.0e38f)) {  // non-finite arithmetic: stay conservative
         *lo = x0;
         *hi = x1;
         return;
     }
-    const float slack_x = 1e-3f + 1e-5f * xmax;
     // tile tx is touched iff 16 tx - mx <= xr and 16 tx + 15 - mx >= xl
-    const float vl = (xl - slack_x + mx - (float)(TILE_X - 1)) / (float)TILE_X;
-    const float vh = (xr + slack_x + mx) / (float)TILE_X;
+    const float vl = (xl - e.slack_x + e.mx - (float)(TILE_X - 1)) * (1.0f / TILE_X);
+    const float vh = (xr + e.slack_x + e.mx) * (1.0f / TILE_X);
     *lo = (int)ceilf(fminf(fmaxf(vl, (float)x0), (float)x1));
     *hi = (int)floorf(fminf(fmaxf(vh, (float)x0 - 1.f), (float)x1 - 1.f)) + 1;
 }
@@ -148,20 +165,19 @@ __host__ __device__ __forceinline__ int bins_y(int gy) { return (gy + 1) >> 1; }
 // The two tile rows 2Y, 2Y+1 of bin row Y: the tile-column span [l, h) each row's pixels are
 // reached in (exact culling, cull_row_span) or the bounding rect's columns; rows outside [y0, y1)
 // are empty.
-__device__ __forceinline__ void bin_row_spans(float mx, float my, float ca, float cb, float cc, float qmax, int cull,
-                                              int Y, int x0, int x1, int y0, int y1, int& l0, int& h0, int& l1,
-                                              int& h1) {
+__device__ __forceinline__ void bin_row_spans(const CullEll& e, int cull, int Y, int x0, int x1, int y0, int y1,
+                                              int& l0, int& h0, int& l1, int& h1) {
     l0 = h0 = l1 = h1 = x0;
     const int ya = 2 * Y, yb = 2 * Y + 1;
     if (ya >= y0 && ya < y1) {
         l0 = x0;
         h0 = x1;
-        if (cull) cull_row_span(mx, my, ca, cb, cc, qmax, ya, x0, x1, &l0, &h0);
+        if (cull) cull_row_span(e, ya, x0, x1, &l0, &h0);
     }
     if (yb >= y0 && yb < y1) {
         l1 = x0;
         h1 = x1;
-        if (cull) cull_row_span(mx, my, ca, cb, cc, qmax, yb, x0, x1, &l1, &h1);
+        if (cull) cull_row_span(e, yb, x0, x1, &l1, &h1);
     }
 }
 // Mask of bin column X given its two rows' spans (bit 2 r + c = tile (2Y + r, 2X + c) reached).

@@ -98,11 +98,15 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
     a.radii[idx] = radius;
     // (bin, Gaussian) pairs: bins (2 x 2 tiles, rr_common.hpp) holding a tile the Gaussian reaches
     // (exact culling) or a tile of its bounding rect
-    const float qmax = a.cull ? cull_qmax(opacity) : 0.f;
+    // culling on the conic as the duplicate reads it back from the record (splat_conic), so both
+    // kernels count the same pairs
+    float ccx, ccy, ccz;
+    splat_conic(s.a, s.b, ccx, ccy, ccz);
+    const CullEll ell = cull_setup(px, py, ccx, ccy, ccz, a.cull ? cull_qmax(opacity) : 0.f);
     uint32_t n = 0;
     for (int Y = y0 >> 1; Y < (y1 + 1) >> 1; Y++) {
         int l0, h0, l1, h1, Xa, Xb;
-        bin_row_spans(px, py, cx, cy, cz, qmax, a.cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
+        bin_row_spans(ell, a.cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
         bin_cols(l0, h0, l1, h1, Xa, Xb);
         for (int X = Xa; X < Xb; X++) n += bin_mask(X, l0, h0, l1, h1) != 0u ? 1u : 0u;
     }
@@ -296,11 +300,11 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                 const bool any_open =
                     !filter || (sat[y1 * sw + x1] + sat[y0 * sw + x0] - sat[y0 * sw + x1] - sat[y1 * sw + x0]) > 0;
                 if (any_open) {
-                    const float qmax = cull ? cull_qmax(Bv.w) : 0.f;
+                    const CullEll ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
                     uint32_t pos = a;
                     for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && pos < hi; Y++) {
                         int l0, h0, l1, h1, Xa, Xb;
-                        bin_row_spans(A.x, A.y, ccx, ccy, ccz, qmax, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
+                        bin_row_spans(ell, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
                         bin_cols(l0, h0, l1, h1, Xa, Xb);
                         uint32_t c = 0;
                         for (int X = Xa; X < Xb; X++) c += bin_mask(X, l0, h0, l1, h1) != 0u ? 1u : 0u;
