@@ -335,6 +335,23 @@ __device__ __forceinline__ v3 sh_eval(v3 dir, const float* dc, const float* rest
     return mk(r.x + 0.5f, r.y + 0.5f, r.z + 0.5f);
 }
 
+// N consecutive floats at a dword-aligned address, as 16-B loads (the target runs in unaligned
+// access mode, so a 16-B global load needs only dword alignment) plus a scalar tail.
+template <int N>
+__device__ __forceinline__ void load_floats_u(const float* p, float (&out)[N > 0 ? N : 1]) {
+    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+#pragma unroll
+    for (int i = 0; i + 4 <= N; i += 4) {
+        const f4u v = *reinterpret_cast<const f4u*>(p + i);
+        out[i] = v.x;
+        out[i + 1] = v.y;
+        out[i + 2] = v.z;
+        out[i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = N & ~3; i < N; i++) out[i] = p[i];
+}
+
 // Prefetch of one Splat record into three float4 registers.  Plain float4 variables: keeping
 // the prefetched record in a struct made hipcc place it in scratch (private memory).
 __device__ __forceinline__ void load_splat(const Splat* __restrict__ s, uint32_t i, float4& a, float4& b, float4& c) {
