@@ -195,6 +195,17 @@ __device__ __forceinline__ void bin_cols(int l0, int h0, int l1, int h1, int& Xa
     Xb = (e0 && e1) ? Xa : (hi + 1) >> 1;
 }
 
+// Number of bin columns X with bin_mask(X, ...) != 0, in closed form: the bins a non-empty span
+// [l, h) touches are [l / 2, (h - 1) / 2], and a bin counts once if both rows touch it.  (A loop
+// over the columns makes a wave wait for its widest Gaussian's row length times every row.)
+__device__ __forceinline__ uint32_t bin_count(int l0, int h0, int l1, int h1) {
+    const bool e0 = h0 <= l0, e1 = h1 <= l1;
+    const int a0 = l0 >> 1, b0 = (h0 - 1) >> 1, a1 = l1 >> 1, b1 = (h1 - 1) >> 1;
+    const int n0 = e0 ? 0 : b0 - a0 + 1, n1 = e1 ? 0 : b1 - a1 + 1;
+    const int ov = (e0 || e1) ? 0 : max(0, min(b0, b1) - max(a0, a1) + 1);
+    return (uint32_t)(n0 + n1 - ov);
+}
+
 // Column-major 4x4 transforms (auxiliary.h:47-86).  Matrices live in device memory and are
 // indexed with wave-uniform offsets, so the compiler keeps them in SGPRs (s_load).
 __device__ __forceinline__ v3 xform_point_4x3(v3 p, const float* m) {

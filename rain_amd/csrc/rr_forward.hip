@@ -110,10 +110,9 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
     const CullEll ell = cull_setup(px, py, ccx, ccy, ccz, a.cull ? cull_qmax(opacity) : 0.f);
     uint32_t n = 0;
     for (int Y = y0 >> 1; Y < (y1 + 1) >> 1; Y++) {
-        int l0, h0, l1, h1, Xa, Xb;
+        int l0, h0, l1, h1;
         bin_row_spans(ell, a.cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
-        bin_cols(l0, h0, l1, h1, Xa, Xb);
-        for (int X = Xa; X < Xb; X++) n += bin_mask(X, l0, h0, l1, h1) != 0u ? 1u : 0u;
+        n += bin_count(l0, h0, l1, h1);
     }
     a.tiles[idx] = make_uint2(n, (uint32_t)area);
     a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
@@ -311,8 +310,7 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                         int l0, h0, l1, h1, Xa, Xb;
                         bin_row_spans(ell, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
                         bin_cols(l0, h0, l1, h1, Xa, Xb);
-                        uint32_t c = 0;
-                        for (int X = Xa; X < Xb; X++) c += bin_mask(X, l0, h0, l1, h1) != 0u ? 1u : 0u;
+                        const uint32_t c = bin_count(l0, h0, l1, h1);
                         if (pos + c <= lo) {  // bin row entirely before the window
                             pos += c;
                             continue;
