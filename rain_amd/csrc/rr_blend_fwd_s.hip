@@ -34,7 +34,10 @@ typedef __attribute__((address_space(4))) const u2v cu2v_s;
 // NW waves per 16x16 tile, PIX = 4/NW pixels per lane: lane l of wave w owns column l%16 and rows
 // l/16 + 4*(w*PIX + k), k < PIX.  G pairs per group (their alphas formed before the blend).
 template <int NW, bool AUX>
-__global__ __launch_bounds__(64 * NW) void k_blend_fwd_s(BlendFwdArgs a) {
+#ifndef RR_FWD_S_OCC
+#define RR_FWD_S_OCC 1
+#endif
+__global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdArgs a) {
 #pragma clang fp contract(off)  // blend_p2's rounding: every fma below is explicit
     constexpr int PIX = 4 / NW;
 #ifndef RR_FWD_S_GROUP

@@ -46,7 +46,7 @@ def main():
     pl, rg, nc = it["point_list"], it["ranges"], it["n_contrib"]
     xy, co = it["xy"], it["conic_opacity"]
     gx, gy = (W + 15) // 16, (H + 15) // 16
-    base_half = base_tile = masked = masked_half = pairs_walk = 0
+    base_half = base_tile = masked = masked_half = pairs_walk = live_only = band_only = 0
     touched_hist = np.zeros(5, np.int64)
     ys = np.arange(16, dtype=np.float32)
     xs = np.arange(16, dtype=np.float32)
@@ -78,6 +78,8 @@ def main():
         j = np.arange(len(ids))[:, None]
         live = j < bmax[None, :]
         masked += int((band & live).sum()) * 64
+        live_only += int(live.sum()) * 64
+        band_only += int(band.sum()) * 64
         touched_hist += np.bincount(band.sum(axis=1), minlength=5)
         hmax = np.array([ncp[:8].max(), ncp[8:].max()])
         hl = j < hmax[None, :]
@@ -85,7 +87,8 @@ def main():
         masked_half += int((hband & hl).sum()) * 128
     print(f"view {a.view}: num_rendered {nr}, pairs walked (sum tile_max) {pairs_walk}")
     print(f"pixel-pair evaluations: whole-tile walk {base_tile/1e6:.1f}M, half-tile waves {base_half/1e6:.1f}M, "
-          f"half-tile waves + half masks {masked_half/1e6:.1f}M, 4-row band masks {masked/1e6:.1f}M")
+          f"half-tile waves + half masks {masked_half/1e6:.1f}M, 4-row band masks {masked/1e6:.1f}M "
+          f"(band max n_contrib alone {live_only/1e6:.1f}M, band reach alone {band_only/1e6:.1f}M)")
     print("bands touched per walked pair (0..4):", (touched_hist / touched_hist.sum()).round(3).tolist())
 
 
