@@ -106,7 +106,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             const int contributor = nmax - 1 - (base + j);
             const float4 A = s_a[j];
             const float4 Bv = s_b[j];
-            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
+            float g0, g1, g2, g3, g4, g5, g6 = 0.f, g7 = 0.f, g8 = 0.f;
             bool any = false;
             // The conic-side terms are linear in v = e * dL/dalpha with e = opacity G (the unclamped
             // alpha), and a lane's PPL pixels share its column (dx): per pixel only S_v, S_v.dy,
@@ -146,14 +146,14 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     svdy2 = __builtin_fmaf(vdy, dy, svdy2);
                 }
             }
-            if (any) {
-                g0 = sv * dx;
-                g1 = svdy;
-                g2 = g0 * dx;
-                g3 = g1 * dx;
-                g4 = svdy2;
-                g5 = sv * s_c[j].w;  // 1 / opacity
-            }
+            // unconditionally: with no active pixel the sums are 0 and so are these (a branch here
+            // costs a zero-initialising move per component and pair)
+            g0 = sv * dx;
+            g1 = svdy;
+            g2 = g0 * dx;
+            g3 = g1 * dx;
+            g4 = svdy2;
+            g5 = sv * s_c[j].w;  // 1 / opacity
             float* sg = &s_g[w][j * NGRAD];
             float t0 = 0.f, t1 = 0.f, t2 = 0.f;
             if (__ballot(any) != 0ull) wave_sum9(g0, g1, g2, g3, g4, g5, g6, g7, g8, t0, t1, t2);
