@@ -80,7 +80,7 @@ class RRDebugViews(ctypes.Structure):
 RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
                   "rr_forward_geometry", "rr_forward_render", "rr_forward_render_aux", "rr_forward", "rr_backward", "rr_mark_visible", "rr_last_error",
                   "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
-                  "rr_set_binning_config", "rr_set_tuning", "rr_profile_enable",
+                  "rr_set_binning_config", "rr_set_tuning", "rr_debug_set_fwd_trace", "rr_profile_enable",
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name"]
 
 _raster = None
@@ -134,6 +134,8 @@ def raster():
         L.rr_profile_enable.argtypes = [ci]
         L.rr_set_tuning.restype = ci
         L.rr_set_tuning.argtypes = [ctypes.c_char_p, ci]
+        L.rr_debug_set_fwd_trace.restype = ci
+        L.rr_debug_set_fwd_trace.argtypes = [ctypes.c_void_p]
         L.rr_set_binning_config.restype = ci
         L.rr_set_binning_config.argtypes = [ci, ci]
         L.rr_profile_select.restype = ci
