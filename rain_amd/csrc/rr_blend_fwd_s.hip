@@ -4,11 +4,12 @@
 // Written for the scalar VALU with as few vector instructions per (pixel, pair) as possible (a
 // packed v_pk_fma_f32 costs ~2x a plain v_fma_f32 on gfx950 and needs operand shuffles, so packing
 // buys nothing here):
-//   * every lane of a wave blends the same pair at the same time, so the pair's id and 48-B Splat
-//     are wave-uniform: they are read with s_load through the constant address space and feed the
-//     VALU ops as scalar operands (no LDS staging, no broadcast VGPRs, no barrier per round); a
-//     group's records and the next group's ids leave in one batch (RR_FWD_S_BATCH), one
-//     scalar-memory round trip per group;
+//   * every lane of a wave blends the same pair at the same time, so the pair's 48-B Splat is
+//     wave-uniform.  Default (RR_FWD_S_LDS): the workgroup stages a round of 64 NW records in LDS
+//     (one per thread, gathered by id) while the previous round blends, and the waves read them
+//     as LDS broadcasts — one exposed gather latency per tile: the records come from a 48 B x P
+//     array that no L2 holds, ~1-2 us away, and the scalar-load variants (s_load per group,
+//     RR_FWD_S_BATCH / RR_FWD_S_PIPE) wait that long every group of 2-4 pairs;
 //   * alpha in log2 units from the pre-scaled conic (rr_common.hpp blend_p2): per pixel 3 fma-class
 //     ops, an add of log2(opacity) and one exp2;
 //   * a lane owns PIX pixels of one column (rows l/16 + 4k): the x-terms of the falloff are
@@ -45,6 +46,9 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
 #endif
 #ifndef RR_FWD_S_PIPE
 #define RR_FWD_S_PIPE 0
+#endif
+#ifndef RR_FWD_S_LDS
+#define RR_FWD_S_LDS 1  // measured: 0.176 vs 0.203 ms/step (scalar loads batched per group)
 #endif
 #ifndef RR_FWD_S_BATCH
 #define RR_FWD_S_BATCH 1  // measured: 0.208 vs 0.222 ms/step (G = 3 vs the unbatched G = 4)
@@ -115,7 +119,8 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
 
     // One group of G pairs: their alphas first (independent of T), then the sequential blend.
     // ra/rb/rc/rn: the pairs' records as wave-uniform values (SGPR operands).
-    auto blend_group = [&](int j0, const v4f (&ra)[G], const v4f (&rb)[G], const v4f (&rc)[G], const v4f (&rn)[G]) {
+    auto blend_group = [&](int j0, int jlim, const v4f (&ra)[G], const v4f (&rb)[G], const v4f (&rc)[G],
+                           const v4f (&rn)[G]) {
         bool open[PIX];  // as of the group's start (only used to skip work)
 #pragma unroll
         for (int k = 0; k < PIX; k++) open[k] = T[k] > 0.f;
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
         }
 #pragma unroll
         for (int u = 0; u < G; u++) {
-            if (j0 + u >= n) break;
+            if (j0 + u >= jlim) break;
             const uint32_t k1 = koff + (uint32_t)(j0 + u + 1);
 #pragma unroll
             for (int k = 0; k < PIX; k++) {
@@ -191,7 +196,62 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
             if (AUX) rn[u] = nrm[id[u]];
         }
     };
-#if RR_FWD_S_PIPE
+#if RR_FWD_S_LDS
+    // Records staged through LDS a round of 64 NW pairs at a time, the next round's gathered into
+    // registers while this one blends (one exposed load latency per tile instead of one per group:
+    // the records are gathered from a 48-B x P array no L2 holds).  Reads are wave-uniform LDS
+    // broadcasts; the arithmetic is the scalar path's (blend_group) on VGPR operands.
+    {
+        constexpr int RND = 64 * NW;
+        __shared__ v4f s_ra[RND], s_rb[RND], s_rc[RND], s_rn[AUX ? RND : 1];
+        const cv4f_s* rbase = recs;
+        v4f pa = {}, pb = {}, pc = {}, pn = {};
+        auto fetch = [&](int j) {
+            if (j < n) {
+                const uint32_t id = ((const uint32_t*)a.point_list)[lo + j];
+                const v4f* r = (const v4f*)a.splats + 3 * (size_t)id;
+                pa = r[0];
+                pb = r[1];
+                pc = r[2];
+                if (AUX) pn = ((const v4f*)a.normals)[id];
+            }
+        };
+        (void)rbase;
+        fetch(t);
+        for (int r0 = 0; r0 < n; r0 += RND) {
+            bool mine = false;
+#pragma unroll
+            for (int k = 0; k < PIX; k++) mine |= T[k] > 0.f;
+            // every wave reaches this barrier each round (it also guards the LDS reuse)
+            if (!__syncthreads_or(mine)) break;
+            if (r0 + t < n) {
+                s_ra[t] = pa;
+                s_rb[t] = pb;
+                s_rc[t] = pc;
+                if (AUX) s_rn[t] = pn;
+            }
+            __syncthreads();
+            fetch(r0 + RND + t);  // next round in flight while this one blends
+            const int cnt = min(RND, n - r0);
+            for (int j = 0; j < cnt; j += G) {
+                if (!wave_open()) break;  // this wave's pixels all saturated
+#if RR_FWD_TRACE
+                walked = r0 + j + G;
+#endif
+                v4f ra[G], rb[G], rc[G], rn[G];
+#pragma unroll
+                for (int u = 0; u < G; u++) {
+                    const int q = min(j + u, cnt - 1);
+                    ra[u] = s_ra[q];
+                    rb[u] = s_rb[q];
+                    rc[u] = s_rc[q];
+                    if (AUX) rn[u] = s_rn[q];
+                }
+                blend_group(r0 + j, r0 + cnt, ra, rb, rc, rn);
+            }
+        }
+    }
+#elif RR_FWD_S_PIPE
     // Software pipeline over groups: while group j blends, the records of group j+1 and the ids of
     // group j+2 are in flight.  Scalar loads return out of order (the only wait is lgkmcnt(0)), so
     // the wait sits at the top of the group and sched barriers keep the compiler from hoisting the
@@ -212,7 +272,7 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
             group_recs(idn, na, nb, nc, nn);
             group_ids(j0 + 2 * G, inn, id0);
             __builtin_amdgcn_sched_barrier(0);
-            blend_group(j0, ra, rb, rc, rn);
+            blend_group(j0, n, ra, rb, rc, rn);
 #pragma unroll
             for (int u = 0; u < G; u++) {
                 ra[u] = na[u];
@@ -242,7 +302,7 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
             group_recs(idc, ra, rb, rc, rn);
             group_ids(j0 + G, idn, id0);
             __builtin_amdgcn_sched_barrier(0);
-            blend_group(j0, ra, rb, rc, rn);
+            blend_group(j0, n, ra, rb, rc, rn);
 #pragma unroll
             for (int u = 0; u < G; u++) idc[u] = idn[u];
         }
@@ -257,7 +317,7 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
         group_ids(j0, id, plist[j0]);
         v4f ra[G], rb[G], rc[G], rn[G];
         group_recs(id, ra, rb, rc, rn);
-        blend_group(j0, ra, rb, rc, rn);
+        blend_group(j0, n, ra, rb, rc, rn);
     }
 #endif
 #if RR_FWD_TRACE
