@@ -114,15 +114,15 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             // (g0 = S_v dx, g1 = S_vdy, g2 = dx g0, g3 = dx g1, g4 = S_vdy2, g5 = S_v / opacity):
             // 5 VALU per pixel instead of 11.
             const float dx = A.x - pfx;
-            const P2X px2 = blend_p2_x(A.z, A.w, dx);  // identical to the forward's values
+            const P2X px2 = blend_p2_x(A.z, A.w, Bv.y, dx);  // identical to the forward's values
             float sv = 0.f, svdy = 0.f, svdy2 = 0.f;
 #pragma unroll
             for (int q = 0; q < PPL; q++) {
                 const float dy = A.y - (float)(py0 + 4 * q);
-                const float p2 = blend_p2(px2, Bv.x, dy);
-                const float e = __builtin_amdgcn_exp2f(p2 + Bv.y);
+                const float e2 = blend_e2(px2, Bv.x, dy);
+                const float e = __builtin_amdgcn_exp2f(e2);  // o G
                 const float alpha = fminf(0.99f, e);
-                const bool act = contributor < last[q] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+                const bool act = contributor < last[q] && e2 <= Bv.y && alpha >= 1.0f / 255.0f;
                 if (act) {
                     any = true;
                     const float one_m = 1.f - alpha;

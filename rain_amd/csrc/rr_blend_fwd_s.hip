@@ -10,8 +10,8 @@
 //     as LDS broadcasts — one exposed gather latency per tile: the records come from a 48 B x P
 //     array that no L2 holds, ~1-2 us away, and the scalar-load variants (s_load per group,
 //     RR_FWD_S_BATCH / RR_FWD_S_PIPE) wait that long every group of 2-4 pairs;
-//   * alpha in log2 units from the pre-scaled conic (rr_common.hpp blend_p2): per pixel 3 fma-class
-//     ops, an add of log2(opacity) and one exp2;
+//   * alpha in log2 units from the pre-scaled conic (rr_common.hpp blend_e2): per pixel 3 fma-class
+//     ops and one exp2;
 //   * a lane owns PIX pixels of one column (rows l/16 + 4k): the x-terms of the falloff are
 //     computed once per lane and pair;
 //   * no per-pixel "open" flag: a saturated pixel keeps -T (T >= 1e-4 > 0 while open), so every
@@ -39,7 +39,7 @@ template <int NW, bool AUX>
 #define RR_FWD_S_OCC 1
 #endif
 __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdArgs a) {
-#pragma clang fp contract(off)  // blend_p2's rounding: every fma below is explicit
+#pragma clang fp contract(off)  // blend_e2's rounding: every fma below is explicit
     constexpr int PIX = 4 / NW;
 #ifndef RR_FWD_S_GROUP
 #define RR_FWD_S_GROUP 3
@@ -124,23 +124,23 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
         bool open[PIX];  // as of the group's start (only used to skip work)
 #pragma unroll
         for (int k = 0; k < PIX; k++) open[k] = T[k] > 0.f;
-        // alphas of the group (independent of T): forward.cu:329-336 as blend_p2 (rr_common.hpp)
+        // alphas of the group (independent of T): forward.cu:329-336 as blend_e2 (rr_common.hpp)
         float al[G][PIX];
         bool ok[G][PIX];
         uint64_t okm[G][PIX];  // ok as a wave mask (ballots of the compares themselves: v_cmp into SGPRs)
         P2X px2[G];
 #pragma unroll
-        for (int u = 0; u < G; u++) px2[u] = blend_p2_x(ra[u].z, ra[u].w, ra[u].x - pfx);
+        for (int u = 0; u < G; u++) px2[u] = blend_p2_x(ra[u].z, ra[u].w, rb[u].y, ra[u].x - pfx);
 #pragma unroll
         for (int k = 0; k < PIX; k++) {
 #pragma unroll
             for (int u = 0; u < G; u++) {
-                const float p2 = blend_p2(px2[u], rb[u].x, ra[u].y - pfy[k]);
-                const float a99 = fminf(0.99f, __builtin_amdgcn_exp2f(p2 + rb[u].y));
+                const float e2 = blend_e2(px2[u], rb[u].x, ra[u].y - pfy[k]);
+                const float a99 = fminf(0.99f, __builtin_amdgcn_exp2f(e2));
                 // non-short-circuit: both compares become lane masks combined on the scalar unit
-                ok[u][k] = (p2 <= 0.0f) & (a99 >= 1.0f / 255.0f) & open[k];
-                okm[u][k] = __builtin_amdgcn_ballot_w64(p2 <= 0.0f) & __builtin_amdgcn_ballot_w64(a99 >= 1.0f / 255.0f) &
-                            __builtin_amdgcn_ballot_w64(open[k]);
+                ok[u][k] = (e2 <= rb[u].y) & (a99 >= 1.0f / 255.0f) & open[k];
+                okm[u][k] = __builtin_amdgcn_ballot_w64(e2 <= rb[u].y) &
+                            __builtin_amdgcn_ballot_w64(a99 >= 1.0f / 255.0f) & __builtin_amdgcn_ballot_w64(open[k]);
                 al[u][k] = a99;
             }
         }

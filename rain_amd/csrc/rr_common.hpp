@@ -389,22 +389,24 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
 // Falloff of a (pair, pixel) (forward.cu:329-336 / backward.cu:481-491) in log2 units:
 //   power = -0.5 (cx dx^2 + cz dy^2) - cy dx dy,   p2 = log2(e) power = qa dx^2 + qb dx dy + qc dy^2,
 //   alpha = min(0.99, opacity exp(power)) = min(0.99, exp2(p2 + log2 opacity)),
-// evaluated with one fixed op sequence (blend_p2_x per pair and lane, then blend_p2 per pixel;
+// evaluated with one fixed op sequence (blend_p2_x per pair and lane, then blend_e2 per pixel;
 // explicit fmas, no contraction) by both blend kernels, so forward and backward take
-// bitwise-identical alpha decisions.  p2 <= 0 <=> power <= 0.  dx, dy = mean - pixel.
+// bitwise-identical alpha decisions.  log2 opacity is folded into the per-lane x term, so a pixel
+// gets e2 = p2 + log2 o from two fmas; the reference's power <= 0 test is e2 <= log2 o.
+// dx, dy = mean - pixel.
 constexpr float kLog2e = 1.44269504088896340736f;
 constexpr float kQHalf = -0.5f * kLog2e;          // qa = kQHalf cx, qc = kQHalf cz
 constexpr float kQFull = -kLog2e;                 // qb = kQFull cy
 constexpr float kQHalfInv = -1.38629436111989061883f;  // -2 ln 2: cx = kQHalfInv qa (back-conversion, <= 2 ulp)
 constexpr float kQFullInv = -0.69314718055994530942f;  // -ln 2
-struct P2X {  // the x terms of p2, once per (pair, lane)
+struct P2X {  // the x terms of e2, once per (pair, lane)
     float ax, bx;
 };
-__device__ __forceinline__ P2X blend_p2_x(float qa, float qb, float dx) {
+__device__ __forceinline__ P2X blend_p2_x(float qa, float qb, float lo, float dx) {
 #pragma clang fp contract(off)
-    return P2X{(qa * dx) * dx, qb * dx};
+    return P2X{(qa * dx) * dx + lo, qb * dx};
 }
-__device__ __forceinline__ float blend_p2(P2X x, float qc, float dy) {
+__device__ __forceinline__ float blend_e2(P2X x, float qc, float dy) {
     return __builtin_fmaf(__builtin_fmaf(qc, dy, x.bx), dy, x.ax);
 }
 // The raw conic (cx, cy, cz) and opacity of a record, for the tile culling and the backward's
