@@ -294,6 +294,7 @@ int set_tuning(const char* key, int value) {
     else if (k == "fwd_s_b_waves") g_fwd_s_b_waves = (value == 1 || value == 2) ? value : 4;
     else if (k == "bwd_waves") g_bwd_waves = value;
     else if (k == "sort_min_units") set_sort_min_units(value);
+    else if (k == "sort_min_units_tile") set_sort_min_units_tile(value);
     else if (k == "sort_max_rounds") set_sort_max_rounds(value);
     else return 1;
     return 0;

@@ -170,6 +170,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
 // (the depth sort hands the scan its {pairs, rect} in depth order, a contiguous array).
 const char* radix_sort_last_error();
 void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
+void set_sort_min_units_tile(int units);  // the same for the bin sorts (<= 16-bit keys; default 1024)
 void set_sort_max_rounds(int r);     // rounds cap per wave (tuning; 0 = default 16)  // which check failed in the last radix_sort_pairs call
 // Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
 // can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass

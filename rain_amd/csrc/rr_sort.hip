@@ -296,11 +296,18 @@ struct SortLayout {
 // units (rr_set_tuning "sort_min_units"; interleaved A/B on the bench step: 512 beat 1024 by 1.7%,
 // the 1M-key depth sort then runs 1024-item units)
 constexpr int kMinUnitsDefault = 512;
+// Sorts of <= 16-bit keys (the bin sorts) target more, smaller units: their first pass's units are
+// the duplicate's windows, whose workgroups are latency-bound (interleaved A/B on the bench step:
+// duplicate 0.098 -> 0.092, bin sort 0.087 -> 0.077 ms/step with 1024; the depth sort keeps 512:
+// 0.109 vs 0.129 ms with 1024)
+constexpr int kMinUnitsTileDefault = 1024;
 int g_min_units = kMinUnitsDefault;
+int g_min_units_tile = kMinUnitsTileDefault;
 int g_max_rounds = kMaxRounds;  // rr_set_tuning "sort_max_rounds" (power of two <= 16)
-int rounds_for(size_t n) {
+int rounds_for(size_t n, int bits) {
+    const size_t mu = (size_t)(bits <= 16 ? g_min_units_tile : g_min_units);
     int r = g_max_rounds;
-    while (r > 1 && (n + (size_t)64 * kWaves * r - 1) / ((size_t)64 * kWaves * r) < (size_t)g_min_units) r >>= 1;
+    while (r > 1 && (n + (size_t)64 * kWaves * r - 1) / ((size_t)64 * kWaves * r) < mu) r >>= 1;
     return r;
 }
 
@@ -308,7 +315,7 @@ template <typename K>
 SortLayout sort_layout(void* buf, size_t n, int bits) {
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     SortLayout s{};
-    const int rounds = rounds_for(n);
+    const int rounds = rounds_for(n, bits);
     const size_t units = (n + (size_t)64 * kWaves * rounds - 1) / ((size_t)64 * kWaves * rounds);
     const int passes = bits <= 0 ? 0 : (bits + 7) / 8;
     const int dmax = passes ? (bits + passes - 1) / passes : 0;
@@ -343,7 +350,7 @@ RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
     if (n == 0 || bits <= 0) return p;
     const SortLayout s = sort_layout<K>(temp, n, bits);
     const int passes = (bits + 7) / 8;
-    p.rounds = rounds_for(n);
+    p.rounds = rounds_for(n, bits);
     p.unit_items = 64 * kWaves * p.rounds;
     p.units = (int)((n + p.unit_items - 1) / p.unit_items);
     p.dbits0 = (bits + passes - 1) / passes;
@@ -352,6 +359,7 @@ RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
 }
 
 void set_sort_min_units(int units) { g_min_units = units > 0 ? units : kMinUnitsDefault; }
+void set_sort_min_units_tile(int units) { g_min_units_tile = units > 0 ? units : kMinUnitsTileDefault; }
 void set_sort_max_rounds(int r) { g_max_rounds = (r == 1 || r == 2 || r == 4 || r == 8) ? r : kMaxRounds; }
 
 thread_local const char* g_why = "";
@@ -370,7 +378,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
     const SortLayout s = sort_layout<K>(temp, n, bits);
     if (temp_bytes < s.total) return g_why = "temp too small", hipErrorInvalidValue;
     const int passes = (bits + 7) / 8;
-    const int rounds = rounds_for(n);
+    const int rounds = rounds_for(n, bits);
     const int units = (int)((n + (size_t)64 * kWaves * rounds - 1) / ((size_t)64 * kWaves * rounds));
     const K* ksrc = keys_in;
     const uint32_t* vsrc = vals_in;
