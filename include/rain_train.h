@@ -3,10 +3,11 @@
  *
  * rt_adam_step replaces the reference's optimizer.step() (train.py:145-146) on
  * torch.optim.Adam(param_groups, lr=0.0, eps=1e-15) (scene/gaussian_model.py:153-157): one launch
- * updates every parameter group, with the arithmetic of torch's fused Adam
- * (ATen/native/cuda/fused_adam_utils.cuh adam_math, ORIGINAL mode, no weight decay, no amsgrad):
- *   m = b1*m + (1-b1)*g ;  v = b2*v + (1-b2)*g*g            (double, stored fp32)
- *   p -= (lr / bc1) * m / (sqrt(v) / bc2_sqrt + eps)        (fp32)
+ * updates every parameter group, with the fp32 arithmetic of torch's default (multi-tensor,
+ * foreach) Adam that the reference's optimizer runs on GPU tensors (torch/optim/adam.py
+ * _multi_tensor_adam; no weight decay, no amsgrad; rain_amd/csrc/adam_math.hpp):
+ *   m.lerp_(g, 1 - b1) ;  v = b2*v + (1-b2)*g*g
+ *   p += (-lr / bc1) * m / (sqrt(v) / bc2_sqrt + eps)   (hardware sqrt / reciprocal, <= 1 ulp)
  * with bc1 = 1 - b1^step and bc2_sqrt = sqrt(1 - b2^step) computed by the caller per group.
  *
  * Plain device pointers and sizes; the HIP stream is passed as void*.  Returns 0 on success,

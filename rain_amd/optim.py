@@ -5,7 +5,8 @@ Drop-in for the reference's ``torch.optim.Adam(l, lr=0.0, eps=1e-15)``
 densification surgery relies on, gaussian_model.py:200-291), per-parameter state
 {"step", "exp_avg", "exp_avg_sq"} and state_dict layout — but every group is updated by ONE HIP
 launch per step instead of torch's per-group multi-tensor launches.  Arithmetic follows torch's
-fused Adam (see rain_train.h).  Parameters whose .grad is None are skipped, as in torch.
+default foreach Adam in fp32 (see rain_train.h; tests/test_fused_gpu.py checks it against both
+torch implementations).  Parameters whose .grad is None are skipped, as in torch.
 """
 from __future__ import annotations
 
