@@ -78,13 +78,17 @@ def _valu_busy(dirname):
                     d["dur"] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
         for (st, _), d in per.items():
             if d.get("dur") and "SQ_ACTIVE_INST_VALU" in d:
-                busy = 4.0 * d["SQ_ACTIVE_INST_VALU"] / (d["dur"] * CLOCK_GHZ * SIMDS)
-                out.setdefault(st, []).append(busy)
-    return {st: statistics.median(v) for st, v in out.items()}
+                o = out.setdefault(st, [0.0, 0.0])
+                o[0] += 4.0 * d["SQ_ACTIVE_INST_VALU"]
+                o[1] += d["dur"] * CLOCK_GHZ * SIMDS
+    # time-weighted over the launches of a name (both forward-blend phases, whose durations and
+    # occupancy differ a lot, count by their share of the time)
+    return {st: v[0] / v[1] for st, v in out.items() if v[1] > 0}
 
 
 def _inst_mix(dirname):
-    """Per kernel (median over launches): wave-level VALU / SALU / LDS instruction counts and the
+    """Per kernel (median over launches): wave-level VALU / SALU / LDS instruction counts, and (time-
+    weighted over launches) the
     VALU issue fraction = SQ_INSTS_VALU x 2 cycles (a wave64 VALU op occupies a SIMD-32 for two
     cycles; transcendentals longer, so this is a lower bound) / (duration x 1024 SIMDs x clock)."""
     files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
@@ -107,9 +111,13 @@ def _inst_mix(dirname):
             for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
                 if k in d:
                     r.setdefault(k, []).append(d[k])
-            r.setdefault("valu_issue_frac", []).append(2.0 * d["SQ_INSTS_VALU"] / (d["dur"] * CLOCK_GHZ * SIMDS))
-    return {st: {k.lower(): round(statistics.median(v), 4 if k == "valu_issue_frac" else 0) for k, v in r.items()}
-            for st, r in acc.items()}
+            r.setdefault("_valu_cycles", []).append(2.0 * d["SQ_INSTS_VALU"])
+            r.setdefault("_simd_cycles", []).append(d["dur"] * CLOCK_GHZ * SIMDS)
+    res = {}
+    for st, r in acc.items():
+        res[st] = {k.lower(): round(statistics.median(v), 0) for k, v in r.items() if not k.startswith("_")}
+        res[st]["valu_issue_frac"] = round(sum(r["_valu_cycles"]) / sum(r["_simd_cycles"]), 4)  # time-weighted
+    return res
 
 
 def main():
