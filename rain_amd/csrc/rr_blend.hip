@@ -116,6 +116,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             const float dx = A.x - pfx;
             const P2X px2 = blend_p2_x(A.z, A.w, Bv.y, dx);  // identical to the forward's values
             float sv = 0.f, svdy = 0.f, svdy2 = 0.f;
+            const float4 Cc = s_c[j];  // once per pair (not per active row)
 #pragma unroll
             for (int q = 0; q < PPL; q++) {
                 const float dy = A.y - (float)(py0 + 4 * q);
@@ -129,7 +130,6 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     const float inv = rcp_nr(one_m);  // both divisions by (1 - alpha) share one reciprocal
                     T[q] = T[q] * inv;                // T_i, the transmittance in front of this Gaussian
                     const float dchannel_dcolor = alpha * T[q];
-                    const float4 Cc = s_c[j];
                     const float cdp = Cc.x * dp0[q] + Cc.y * dp1[q] + Cc.z * dp2[q];
                     g6 += dchannel_dcolor * dp0[q];
                     g7 += dchannel_dcolor * dp1[q];
