@@ -54,9 +54,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     // The reference keeps accum_rec per channel (backward.cu:497-507) and only ever uses its dot
     // product with dL/dpix; by linearity the same convex-combination recurrence runs on the scalar
-    // R = accum_rec . dL/dpix, with lcdp = last_color . dL/dpix (8 fewer VALU ops and 4 fewer VGPRs
-    // per pixel and pair, and as well conditioned as the per-channel form).
-    float T[PPL], tfbg[PPL], dp0[PPL], dp1[PPL], dp2[PPL], R[PPL], lcdp[PPL], la[PPL];
+    // R = accum_rec . dL/dpix (8 fewer VALU ops and 4 fewer VGPRs per pixel and pair, and as well
+    // conditioned as the per-channel form), advanced at each contributing pair right after its use.
+    float T[PPL], tfbg[PPL], dp0[PPL], dp1[PPL], dp2[PPL], R[PPL];
     int last[PPL];
 #pragma unroll
     for (int q = 0; q < PPL; q++) {
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
         dp2[q] = inside ? a.dL_dpix[2 * HW + pix] : 0.f;
         // -T_final * (bg . dL/dpixel): numerator of the background term (backward.cu:521-524)
         tfbg[q] = -Tf * (bg0 * dp0[q] + bg1 * dp1[q] + bg2 * dp2[q]);
-        R[q] = lcdp[q] = la[q] = 0.f;
+        R[q] = 0.f;
     }
     const uint2 range = a.ranges[tile];
     const uint2 range_b = a.ranges_b[tile];
@@ -134,11 +134,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                     g6 += dchannel_dcolor * dp0[q];
                     g7 += dchannel_dcolor * dp1[q];
                     g8 += dchannel_dcolor * dp2[q];
-                    R[q] = __builtin_fmaf(la[q], lcdp[q] - R[q], R[q]);  // la lcdp + (1 - la) R
-                    lcdp[q] = cdp;
-                    la[q] = alpha;
+                    const float d = cdp - R[q];  // R: accum_rec . dL/dpix in front of this Gaussian
                     // dL/dalpha = T_i (c - accum_rec) . dL/dpix - T_final (bg . dL/dpix) / (1 - alpha)
-                    const float dL_dalpha = (cdp - R[q]) * T[q] + tfbg[q] * inv;
+                    const float dL_dalpha = d * T[q] + tfbg[q] * inv;
+                    // the reference's next accum_rec update (last_alpha = alpha, last_color = c),
+                    // applied now instead of at the next contributing pair: the same fma on the
+                    // same values, without carrying last_alpha / last_color
+                    R[q] = __builtin_fmaf(alpha, d, R[q]);
                     const float v = e * dL_dalpha;
                     const float vdy = v * dy;
                     sv += v;

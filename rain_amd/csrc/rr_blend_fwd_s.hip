@@ -107,6 +107,9 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
                 last[k] = nc & ~kDoneBit;
             }
         }
+        // retire the resume loads here: left pending, the compiler's wait analysis carries them
+        // into the pair loop and waits for the next round's record prefetch at every group
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     }
     const int n = (int)(hi - lo);
 #if RR_FWD_TRACE
