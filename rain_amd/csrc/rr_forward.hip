@@ -290,21 +290,27 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     for (int base = s0;; base += 256) {
         const int s = base + t;
         if (s < P) {
+            // two dependent load steps per Gaussian: {offsets, id} then {radius, record} (the id is
+            // part of the branch condition and the culling setup precedes the open-tile test, so
+            // the compiler cannot sink these loads behind a wait into the branches that use them)
             const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
+            const uint32_t g = idx_sorted[s];
             const uint32_t lo = max(a, w0), hi = min(b, w1);
-            if (lo < hi) {
-                const uint32_t g = idx_sorted[s];
+            if (lo < hi && g != 0xffffffffu) {
                 const int r = radii[g];
                 const float4 A = splats[g].a;
                 const float4 Bv = splats[g].b;
+                // all of the record in one round trip (the compiler otherwise fetches part of it
+                // only after waiting for the rest)
+                asm volatile("" ::"v"(r), "v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(Bv.x), "v"(Bv.w));
                 float ccx, ccy, ccz;
                 splat_conic(A, Bv, ccx, ccy, ccz);
+                const CullEll ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
                 int x0, y0, x1, y1;
                 tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
                 const bool any_open =
                     !filter || (sat[y1 * sw + x1] + sat[y0 * sw + x0] - sat[y0 * sw + x1] - sat[y1 * sw + x0]) > 0;
                 if (any_open) {
-                    const CullEll ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
                     uint32_t pos = a;
                     for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && pos < hi; Y++) {
                         int l0, h0, l1, h1, Xa, Xb;
