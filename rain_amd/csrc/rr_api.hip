@@ -74,7 +74,11 @@ struct SatAdd2 {
 // gathers while it writes idx_sorted (a transform iterator gathering inside the scan measured
 // 21 us per frame, most of it the scan blocks waiting on their random loads).
 
-size_t depth_sort_temp(int P) { return P > 0 ? radix_sort_temp_bytes<uint32_t>((size_t)P, 32) : 0; }
+size_t depth_sort_temp(int P) {  // the 3-pass (9-bit digits) sort and the 32-bit fallback
+    return P > 0 ? std::max(radix_sort_temp_bytes<uint32_t>((size_t)P, kDepthKeyBits),
+                            radix_sort_temp_bytes<uint32_t>((size_t)P, 32))
+                 : 0;
+}
 size_t scan_temp(int P) {
     // memoized: queried by every carve (forward, render, backward) with the same P
     static thread_local int last_p = -1;
@@ -104,7 +108,8 @@ struct Geom {
     uint2* offsets;       // inclusive prefix sum of tiles[] in depth order; .y of the last = num_rendered
     float4* normals;      // RR_FLAG_AUX_NORMAL: view-space normal per visible Gaussian
     uint2* block_sums;    // [ceil(P/256)] per-preprocess-block sums of tiles[] (pairs, rect tiles)
-    unsigned long long* totals;  // [2] their sums (device copy of what the mailbox publishes)
+    uint32_t* block_wide; // [ceil(P/256)] per block: a visible depth key needs more than kDepthKeyBits
+    unsigned long long* totals;  // [3] their sums and the OR of block_wide (device copy of the mailbox)
     void* temp;
     size_t temp_bytes;
     size_t total;
@@ -122,7 +127,8 @@ Geom carve_geom(void* buf, int P) {
     g.offsets = c.take<uint2>(n);
     g.normals = c.take<float4>(n);
     g.block_sums = c.take<uint2>((n + 255) / 256);
-    g.totals = c.take<unsigned long long>(2);
+    g.block_wide = c.take<uint32_t>((n + 255) / 256);
+    g.totals = c.take<unsigned long long>(3);
     g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
@@ -305,7 +311,7 @@ int check(const rr_frame* f, hipStream_t st, const char* what) {
 // is queried: a launch / kernel error is reported, and a stream that went idle without the
 // sequence number becoming visible falls back to the plain copy.
 struct Mailbox {
-    uint32_t* host = nullptr;  // [x, y, seq, pad], coherent pinned
+    uint32_t* host = nullptr;  // [x, y, seq, wide], coherent pinned
     uint32_t* dev = nullptr;   // device alias of host
     uint32_t seq = 0;
     bool failed = false;       // allocation failed: always use the copy
@@ -313,16 +319,21 @@ struct Mailbox {
 thread_local Mailbox g_mailbox;
 
 // src: the preprocess's per-block sums of {pairs, rect tiles}; one workgroup adds them in 64 bits
-// (fixed order), saturates to 32 bits (the host rejects anything above 2^31 anyway) and publishes.
-__global__ __launch_bounds__(1024) void k_publish_pair_counts(const uint2* __restrict__ src, int nb, uint32_t* box,
-                                                               uint32_t seq, unsigned long long* copy) {
+// (fixed order), saturates to 32 bits (the host rejects anything above 2^31 anyway) and publishes,
+// with the OR of the blocks' wide-depth-key flags.
+__global__ __launch_bounds__(1024) void k_publish_pair_counts(const uint2* __restrict__ src,
+                                                               const uint32_t* __restrict__ src_wide, int nb,
+                                                               uint32_t* box, uint32_t seq, unsigned long long* copy) {
     __shared__ unsigned long long s_n[16], s_r[16];
     unsigned long long n = 0, r = 0;
+    uint32_t wide = 0;
     for (int i = threadIdx.x; i < nb; i += 1024) {
         const uint2 v = src[i];
         n += v.x;
         r += v.y;
+        wide |= src_wide[i];
     }
+    wide = __syncthreads_or(wide != 0) ? 1u : 0u;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         n += __shfl_xor(n, o);
@@ -343,9 +354,11 @@ __global__ __launch_bounds__(1024) void k_publish_pair_counts(const uint2* __res
         const uint32_t y = r > 0xffffffffull ? 0xffffffffu : (uint32_t)r;
         copy[0] = x;  // device copy for the no-mailbox path
         copy[1] = y;
+        copy[2] = wide;
         if (box) {
             __hip_atomic_store(box + 0, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(box + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + 3, wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
@@ -359,8 +372,8 @@ struct PairCountRead {
     uint32_t seq = 0;  // 0: no mailbox (copy + synchronise at wait time)
 };
 
-hipError_t pair_counts_publish(const uint2* block_sums, int nb, unsigned long long* copy, PairCountRead& r,
-                               hipStream_t st) {
+hipError_t pair_counts_publish(const uint2* block_sums, const uint32_t* block_wide, int nb, unsigned long long* copy,
+                               PairCountRead& r, hipStream_t st) {
     Mailbox& mb = g_mailbox;
     r.copy = copy;
     r.seq = 0;
@@ -377,26 +390,28 @@ hipError_t pair_counts_publish(const uint2* block_sums, int nb, unsigned long lo
         }
     }
     if (!mb.failed) r.seq = ++mb.seq == 0 ? ++mb.seq : mb.seq;  // 0 is the mailbox's initial value
-    k_publish_pair_counts<<<1, 1024, 0, st>>>(block_sums, nb, mb.failed ? nullptr : mb.dev, r.seq, copy);
+    k_publish_pair_counts<<<1, 1024, 0, st>>>(block_sums, block_wide, nb, mb.failed ? nullptr : mb.dev, r.seq, copy);
     return hipGetLastError();
 }
 
-hipError_t pair_counts_copy(const unsigned long long* src, uint2* out, hipStream_t st) {
-    unsigned long long v[2] = {0ull, 0ull};
+hipError_t pair_counts_copy(const unsigned long long* src, uint2* out, bool* wide, hipStream_t st) {
+    unsigned long long v[3] = {0ull, 0ull, 0ull};
     hipError_t e = hipMemcpyAsync(v, src, sizeof(v), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     out->x = (uint32_t)v[0];
     out->y = (uint32_t)v[1];
+    *wide = v[2] != 0;
     return e;
 }
 
-hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, hipStream_t st) {
+hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, bool* wide, hipStream_t st) {
     Mailbox& mb = g_mailbox;
-    if (r.seq == 0) return pair_counts_copy(r.copy, out, st);
+    if (r.seq == 0) return pair_counts_copy(r.copy, out, wide, st);
     for (uint32_t spin = 1;; spin++) {
         if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) {
             out->x = __atomic_load_n(mb.host + 0, __ATOMIC_RELAXED);
             out->y = __atomic_load_n(mb.host + 1, __ATOMIC_RELAXED);
+            *wide = __atomic_load_n(mb.host + 3, __ATOMIC_RELAXED) != 0;
             return hipSuccess;
         }
         if ((spin & 4095u) == 0) {
@@ -404,7 +419,7 @@ hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, hipStream_t st) 
             if (q == hipSuccess) {
                 if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) continue;
                 mb.failed = true;  // idle stream, value not visible: never use the mailbox again
-                return pair_counts_copy(r.copy, out, st);
+                return pair_counts_copy(r.copy, out, wide, st);
             }
             if (q != hipErrorNotReady) return q;
         }
@@ -485,6 +500,7 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     a.shs_rest = g->shs_rest;
     a.normals = (f->flags & RR_FLAG_AUX_NORMAL) ? gm.normals : nullptr;
     a.block_sums = gm.block_sums;
+    a.block_wide = gm.block_wide;
 
     PairCountRead rd;
     {
@@ -492,27 +508,40 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
         launch_preprocess(a, st);
     }
     RR_STAGE_CHECK("preprocess");
-    RR_CHECK(pair_counts_publish(gm.block_sums, (P + 255) / 256, gm.totals, rd, st), "publish pair counts");
-    {
-        StageTimer tm(RR_STAGE_DEPTH_SORT, st);
-        size_t tb = gm.temp_bytes;
-        RR_CHECK(radix_sort_pairs<uint32_t>(gm.temp, tb, gm.depth_keys, gm.depth_keys_sorted, nullptr, gm.idx_sorted,
-                                            (size_t)P, 0, 32, st, false, nullptr, nullptr, gm.tiles, gm.tiles_sorted),
-                 "depth sort");
-    }
-    RR_STAGE_CHECK("depth sort");
-    {
-        StageTimer tm(RR_STAGE_SCAN, st);
-        size_t tb = gm.temp_bytes;
-        RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, static_cast<const uint2*>(gm.tiles_sorted), gm.offsets,
-                                         (size_t)P, SatAdd2(), st),
-                 "tile-count scan");
-    }
-    RR_STAGE_CHECK("scan");
+    RR_CHECK(pair_counts_publish(gm.block_sums, gm.block_wide, (P + 255) / 256, gm.totals, rd, st),
+             "publish pair counts");
+    // depth sort (rasterizer_impl.cu:295 sorts {tile, depth} keys; here the Gaussians by depth,
+    // then the pairs stably by bin) and the scan of the pair counts in depth order
+    auto sort_and_scan = [&](int key_bits) -> int {
+        {
+            StageTimer tm(RR_STAGE_DEPTH_SORT, st);
+            size_t tb = gm.temp_bytes;
+            RR_CHECK(radix_sort_pairs<uint32_t>(gm.temp, tb, gm.depth_keys, gm.depth_keys_sorted, nullptr,
+                                                gm.idx_sorted, (size_t)P, 0, key_bits, st, false, nullptr, nullptr,
+                                                gm.tiles, gm.tiles_sorted),
+                     "depth sort");
+        }
+        RR_STAGE_CHECK("depth sort");
+        {
+            StageTimer tm(RR_STAGE_SCAN, st);
+            size_t tb = gm.temp_bytes;
+            RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, static_cast<const uint2*>(gm.tiles_sorted), gm.offsets,
+                                             (size_t)P, SatAdd2(), st),
+                     "tile-count scan");
+        }
+        RR_STAGE_CHECK("scan");
+        return RR_OK;
+    };
+    if (int rc = sort_and_scan(kDepthKeyBits)) return rc;
     // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
     // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
     uint2 tot = make_uint2(0u, 0u);
-    RR_CHECK(pair_counts_wait(rd, &tot, st), "read L");
+    bool wide = false;
+    RR_CHECK(pair_counts_wait(rd, &tot, &wide, st), "read L");
+    // a visible depth beyond the 27-bit key range (~13107): the 3-pass order is not the depth
+    // order, so sort again on all 32 bits before anything reads the sorted arrays
+    if (wide)
+        if (int rc = sort_and_scan(32)) return rc;
     if (tot.x > 0x1fffffffu || tot.y > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^29 bin/Gaussian pairs");
     *num_rendered = (int)tot.y;
     *num_pairs = (int)tot.x;

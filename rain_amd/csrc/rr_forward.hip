@@ -21,7 +21,7 @@ namespace rr {
 // No global atomics here: per-Gaussian counts go to tiles[idx] = {pairs, rect area} and are
 // prefix-summed in depth order (the rect-area sum is the reference's num_rendered).
 template <int DEG>
-__device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
+__device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx, bool& wide) {
     a.radii[idx] = 0;
     a.tiles[idx] = make_uint2(0u, 0u);
     a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
@@ -115,7 +115,10 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
         n += bin_count(l0, h0, l1, h1);
     }
     a.tiles[idx] = make_uint2(n, (uint32_t)area);
-    a.depth_keys[idx] = __float_as_uint(p_view.z);  // > 0.2, so the bit pattern orders like the value
+    // > 0.2, so the bit pattern orders like the value, and so does its offset from kDepthKeyBase
+    const uint32_t key = __float_as_uint(p_view.z) - kDepthKeyBase;
+    a.depth_keys[idx] = key;
+    wide = key >= (1u << kDepthKeyBits);
     return make_uint2(n, (uint32_t)area);
 }
 
@@ -125,9 +128,11 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx) {
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint2 c = idx < a.P ? preprocess_one<DEG>(a, idx) : make_uint2(0u, 0u);
+    bool wide = false;
+    const uint2 c = idx < a.P ? preprocess_one<DEG>(a, idx, wide) : make_uint2(0u, 0u);
     if (!a.block_sums) return;
     __shared__ uint2 s_sum[4];
+    __shared__ uint32_t s_wide[4];
     uint32_t n = c.x, r = c.y;  // per block <= 256 * T, below 2^32 for T < 2^24
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -135,11 +140,17 @@ __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
         r += (uint32_t)__shfl_xor((int)r, o);
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (lane == 0) s_sum[w] = make_uint2(n, r);
+    const bool wave_wide = __any(wide);
+    if (lane == 0) {
+        s_sum[w] = make_uint2(n, r);
+        s_wide[w] = wave_wide ? 1u : 0u;
+    }
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         a.block_sums[blockIdx.x] = make_uint2(s_sum[0].x + s_sum[1].x + s_sum[2].x + s_sum[3].x,
                                               s_sum[0].y + s_sum[1].y + s_sum[2].y + s_sum[3].y);
+        a.block_wide[blockIdx.x] = s_wide[0] | s_wide[1] | s_wide[2] | s_wide[3];
+    }
 }
 
 // First Gaussian (depth rank) of every window of `win` consecutive pairs starting at pair0:

@@ -27,7 +27,17 @@ struct PreArgs {
     const float* shs_rest;       // raw mode: f_rest [P,M-1,3] (shs = f_dc [P,1,3])
     float4* normals;             // RR_FLAG_AUX_NORMAL: view-space unit normal per visible Gaussian, else null
     uint2* block_sums;           // optional [ceil(P/256)]: per-block sums of tiles[] (pairs, rect tiles)
+    uint32_t* block_wide;        // with block_sums: per block, 1 if a visible depth key needs > kDepthKeyBits
 };
+
+// Depth keys: the float bits of the view depth minus those of the smallest float above the near
+// plane (0.2f = 0x3E4CCCCD), so the keys of depths up to ~13107 fit 27 bits and the depth sort runs
+// 3 passes; a frame with a deeper visible Gaussian is re-sorted on all 32 bits (the preprocess
+// flags it, the host reads the flag with the pair counts).  Culled Gaussians keep 0xffffffff,
+// whose low 27 bits are the maximum: they still sort behind every visible one, and their own order
+// is irrelevant (no pairs).
+constexpr uint32_t kDepthKeyBase = 0x3E4CCCCEu;
+constexpr int kDepthKeyBits = 27;
 
 // Early-stop binning (rr_api.hip): the tile lists are built in two phases.  Phase A bins the
 // depth-ordered pairs [0, L_A) for every tile and blends them; a tile whose pixels have all

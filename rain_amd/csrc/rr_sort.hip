@@ -19,7 +19,9 @@
 // Order inside a unit is (wave, round, lane) = input order and units are scanned in order, so
 // every pass is stable.  A producer that filters its output (the early-stop duplicate pass) may
 // leave units sparse (unit_len[u] items each, positions kept) and only the device knows the total
-// (n_dev): the first pass then compacts, and every later pass reads the count from the device.  Passes = ceil(bits / 8) with the bits spread evenly (13 -> 7 + 6).
+// (n_dev): the first pass then compacts, and every later pass reads the count from the device.
+// Digits are <= 8 bits, or <= 9 bits where that saves a pass (the 27-bit depth sort: 3 x 9 instead
+// of 4 x 7); the bits are spread evenly over the passes (13 -> 7 + 6).
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
@@ -31,6 +33,16 @@ constexpr int kWaves = 4;       // waves per workgroup (unit)
 constexpr int kMaxRounds = 16;  // rounds of 64 items per wave
 constexpr int kMaxUnitItems = 64 * kWaves * kMaxRounds;  // 4096
 static_assert(kMaxUnitItems == kSortMaxUnit, "rr_kernels.hpp kSortMaxUnit");
+
+// passes of a sort of `bits` bits: 8-bit digits, or 9-bit ones for 25..27 bits (3 passes instead of
+// 4; the tile sorts, whose first-pass counts come from the duplicate's 256-digit histogram, keep
+// 8-bit digits)
+__host__ __device__ constexpr int sort_passes(int bits) {
+    return bits <= 0 ? 0 : (bits >= 25 && bits <= 27) ? 3 : (bits + 7) / 8;
+}
+__host__ __device__ constexpr int sort_max_dbits(int bits) {
+    return bits <= 0 ? 0 : (bits + sort_passes(bits) - 1) / sort_passes(bits);
+}
 
 // Items of one unit: [unit * unit_items, unit * unit_items + len).  Contiguous input has
 // len = min(unit_items, n - base) with n from the host or, when only the device knows it (a
@@ -44,11 +56,11 @@ __device__ __forceinline__ uint32_t unit_length(const uint32_t* unit_len, const 
     return base >= nn ? 0u : (uint32_t)min((size_t)unit_items, nn - base);
 }
 
-template <typename K, int MAXR>
+template <typename K, int MAXR, int DB>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ keys, size_t n, int shift, int dbits,
                                                           int rounds, uint32_t* __restrict__ counts, int units,
                                                           const uint32_t* __restrict__ n_dev) {
-    __shared__ uint32_t hist[256];
+    __shared__ uint32_t hist[1 << DB];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
     for (int d = t; d < ndig; d += 64 * kWaves) hist[d] = 0;
@@ -140,7 +152,7 @@ __global__ __launch_bounds__(256) void k_rs_scan_rows(const uint32_t* __restrict
 // MAXR: rounds the kernel is compiled for (>= the call's rounds).  Small units get a small
 // instance: the LDS staging is sized by it, so e.g. the 512-item units of a 1M-key sort fit ~4x
 // more workgroups per CU than a 4096-item staging area allows.
-template <typename K, int MAXR>
+template <typename K, int MAXR, int DB>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict__ keys_in,
                                                             const uint32_t* __restrict__ vals_in,
                                                             K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -151,10 +163,12 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
                                                             const uint32_t* __restrict__ n_dev,
                                                             const uint2* __restrict__ gather_src,
                                                             uint2* __restrict__ gather_dst) {
-    __shared__ uint32_t dbase[256];         // first output slot of each digit
-    __shared__ uint32_t wcnt[kWaves][256];  // per-wave digit counts, then per-wave cursors
-    __shared__ uint32_t dstart[256];        // block-local start of each digit's run
-    __shared__ uint32_t goff[256];          // global slot of block-local position 0 of each digit's run
+    constexpr int ND = 1 << DB;  // digits the kernel is compiled for (>= 1 << dbits)
+    constexpr int DPL = ND / 64;  // digits per lane in the digit scans
+    __shared__ uint32_t dbase[ND];         // first output slot of each digit
+    __shared__ uint32_t wcnt[kWaves][ND];  // per-wave digit counts, then per-wave cursors
+    __shared__ uint32_t dstart[ND];        // block-local start of each digit's run
+    __shared__ uint32_t goff[ND];          // global slot of block-local position 0 of each digit's run
     __shared__ uint32_t s_val[64 * kWaves * MAXR];
     __shared__ K s_key[64 * kWaves * MAXR];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -170,11 +184,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     const size_t wbase = ubase + wl;
     for (int d = lane; d < ndig; d += 64) wcnt[w][d] = 0;
     for (int d = t; d < ndig; d += 64 * kWaves) goff[d] = offsets[(size_t)d * units + unit];
-    if (w == 1) {  // digit bases: exclusive scan of the digit totals (4 per lane, then shuffles)
-        uint32_t tv[4], sum = 0;
+    if (w == 1) {  // digit bases: exclusive scan of the digit totals (DPL per lane, then shuffles)
+        uint32_t tv[DPL], sum = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int d = 4 * lane + i;
+        for (int i = 0; i < DPL; i++) {
+            const int d = DPL * lane + i;
             tv[i] = d < ndig ? totals[d] : 0u;
             sum += tv[i];
         }
@@ -186,8 +200,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
         }
         uint32_t run = incl - sum;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            dbase[4 * lane + i] = run;
+        for (int i = 0; i < DPL; i++) {
+            dbase[DPL * lane + i] = run;
             run += tv[i];
         }
     }
@@ -209,12 +223,12 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     }
     __syncthreads();
     // block-local starts: digits in order, then waves in order inside each digit.  Wave 0 scans the
-    // <= 256 digit totals: 4 consecutive digits per lane, then a 6-step shuffle scan of lane sums.
+    // <= ND digit totals: DPL consecutive digits per lane, then a 6-step shuffle scan of lane sums.
     if (w == 0) {
-        uint32_t tot[4], sum = 0;
+        uint32_t tot[DPL], sum = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int d = 4 * lane + i;
+        for (int i = 0; i < DPL; i++) {
+            const int d = DPL * lane + i;
             tot[i] = 0;
             if (d < ndig)
 #pragma unroll
@@ -229,8 +243,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
         }
         uint32_t run = incl - sum;  // exclusive prefix of this lane's first digit
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int d = 4 * lane + i;
+        for (int i = 0; i < DPL; i++) {
+            const int d = DPL * lane + i;
             if (d < ndig) {
                 dstart[d] = run;
                 goff[d] += dbase[d] - run;
@@ -288,14 +302,15 @@ struct SortLayout {
     uint32_t* vals_alt;
     uint32_t* counts;
     uint32_t* offsets;
-    uint32_t* totals;  // [256] per-digit totals of the current pass
+    uint32_t* totals;  // [512] per-digit totals of the current pass
     size_t total;
 };
 
 // rounds per wave: full 16 for large inputs, fewer for small ones so that there are >= ~g_min_units
-// units (rr_set_tuning "sort_min_units"; interleaved A/B on the bench step: 512 beat 1024 by 1.7%,
-// the 1M-key depth sort then runs 1024-item units)
-constexpr int kMinUnitsDefault = 512;
+// units (rr_set_tuning "sort_min_units"; interleaved A/B on the bench step: with 8-bit digits 512
+// beat 1024 by 1.7%; the 3-pass 9-bit depth sort of 1M keys: 0.100 ms/step with 256 (2048-item
+// units), 0.109 with 128 or 512, 0.132 with 1024)
+constexpr int kMinUnitsDefault = 256;
 // Sorts of <= 16-bit keys (the bin sorts) target more, smaller units: their first pass's units are
 // the duplicate's windows, whose workgroups are latency-bound (interleaved A/B on the bench step:
 // duplicate 0.098 -> 0.092, bin sort 0.087 -> 0.077 ms/step with 1024; the depth sort keeps 512:
@@ -317,8 +332,7 @@ SortLayout sort_layout(void* buf, size_t n, int bits) {
     SortLayout s{};
     const int rounds = rounds_for(n, bits);
     const size_t units = (n + (size_t)64 * kWaves * rounds - 1) / ((size_t)64 * kWaves * rounds);
-    const int passes = bits <= 0 ? 0 : (bits + 7) / 8;
-    const int dmax = passes ? (bits + passes - 1) / passes : 0;
+    const int dmax = sort_max_dbits(bits);
     const size_t nc = std::max<size_t>(((size_t)1 << dmax) * units, 1);
     char* p = static_cast<char*>(buf);
     size_t off = 0;
@@ -331,7 +345,7 @@ SortLayout sort_layout(void* buf, size_t n, int bits) {
     s.vals_alt = static_cast<uint32_t*>(take(n * 4));
     s.counts = static_cast<uint32_t*>(take(nc * 4));
     s.offsets = static_cast<uint32_t*>(take(nc * 4));
-    s.totals = static_cast<uint32_t*>(take(256 * 4));
+    s.totals = static_cast<uint32_t*>(take(512 * 4));
     s.total = off;
     return s;
 }
@@ -349,7 +363,7 @@ RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
     const int bits = end_bit - begin_bit;
     if (n == 0 || bits <= 0) return p;
     const SortLayout s = sort_layout<K>(temp, n, bits);
-    const int passes = (bits + 7) / 8;
+    const int passes = sort_passes(bits);
     p.rounds = rounds_for(n, bits);
     p.unit_items = 64 * kWaves * p.rounds;
     p.units = (int)((n + p.unit_items - 1) / p.unit_items);
@@ -377,7 +391,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
     if (unit_len && !n_dev) return g_why = "sparse units without n_dev", hipErrorInvalidValue;
     const SortLayout s = sort_layout<K>(temp, n, bits);
     if (temp_bytes < s.total) return g_why = "temp too small", hipErrorInvalidValue;
-    const int passes = (bits + 7) / 8;
+    const int passes = sort_passes(bits);
     const int rounds = rounds_for(n, bits);
     const int units = (int)((n + (size_t)64 * kWaves * rounds - 1) / ((size_t)64 * kWaves * rounds));
     const K* ksrc = keys_in;
@@ -394,11 +408,13 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
         if (!last && kdst == nullptr) return g_why = "no key storage", hipErrorInvalidValue;
         if (!(p == 0 && first_counts_ready)) {
             if (p == 0 && unit_len) return g_why = "sparse units need producer counts", hipErrorInvalidValue;
-            auto count = rounds <= 2 ? k_rs_count<K, 2> : rounds <= 4 ? k_rs_count<K, 4> : k_rs_count<K, kMaxRounds>;
+            auto count = dbits > 8 ? (rounds <= 2 ? k_rs_count<K, 2, 9> : rounds <= 4 ? k_rs_count<K, 4, 9> : k_rs_count<K, kMaxRounds, 9>)
+                                   : (rounds <= 2 ? k_rs_count<K, 2, 8> : rounds <= 4 ? k_rs_count<K, 4, 8> : k_rs_count<K, kMaxRounds, 8>);
             count<<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev);
         }
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
-        auto scatter = rounds <= 2 ? k_rs_scatter<K, 2> : rounds <= 4 ? k_rs_scatter<K, 4> : k_rs_scatter<K, kMaxRounds>;
+        auto scatter = dbits > 8 ? (rounds <= 2 ? k_rs_scatter<K, 2, 9> : rounds <= 4 ? k_rs_scatter<K, 4, 9> : k_rs_scatter<K, kMaxRounds, 9>)
+                                 : (rounds <= 2 ? k_rs_scatter<K, 2, 8> : rounds <= 4 ? k_rs_scatter<K, 4, 8> : k_rs_scatter<K, kMaxRounds, 8>);
         scatter<<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets, units,
                                                s.totals, p == 0 ? unit_len : nullptr, n_dev,
                                                last ? gather_src : nullptr, last ? gather_dst : nullptr);

@@ -78,23 +78,53 @@ def test_forward_backward_parity(oracle, gpu, case):
 def test_pair_order_and_image_state(oracle, gpu, monkeypatch):
     """With tile culling off, per-tile lists must hold the same Gaussians in the same
     (depth, index) order as the reference's 64-bit-key stable sort; n_contrib / final_T match."""
+    inp, st = make_scene(P=3000, W=128, H=96, sh_degree=3)
+    _check_pair_order(oracle, gpu, monkeypatch, inp, st)
+
+
+@pytest.mark.parametrize("far_every", [1, 3])
+def test_far_depths_keep_depth_order(oracle, gpu, monkeypatch, far_every):
+    """Depths beyond the 27-bit key range (rr_kernels.hpp kDepthKeyBits, ~13107): the frame is
+    re-sorted on all 32 key bits.  Every far_every-th Gaussian is moved away from the camera by
+    10^4 (position and scale about the camera centre, so it projects the same): a 3-pass order
+    would interleave the far ones by their low 27 key bits."""
+    inp, st = make_scene(P=3000, W=128, H=96, sh_degree=3)
+    c = st["campos"]
+    far = torch.zeros(inp["means3D"].shape[0], dtype=torch.bool)
+    far[::far_every] = True
+    k = 1.0e4
+    inp["means3D"][far] = c + k * (inp["means3D"][far] - c)
+    inp["scales"][far] = inp["scales"][far] * k
+    _check_pair_order(oracle, gpu, monkeypatch, inp, st)
+    dpix = _dpix(st)
+    monkeypatch.undo()
+    ref = oracle_run(oracle, inp, st, dL_dpix=dpix)
+    got = gpu_run(inp, st, gpu, dL_dpix=dpix)
+    _check_forward(ref, got)
+    _check_grads(ref, got)
+
+
+def _check_pair_order(oracle, gpu, monkeypatch, inp, st):
     from rain_amd.diff_gaussian_rasterization import _C
 
     monkeypatch.setattr(_C, "TILE_CULLING", False)
     monkeypatch.setattr(_C, "EARLY_STOP", False)  # full per-tile lists
-    inp, st = make_scene(P=3000, W=128, H=96, sh_degree=3)
     ref = oracle_run(oracle, inp, st)
     got = gpu_run(inp, st, gpu)
     geom, binning, img = got["buffers"]
     P = inp["means3D"].shape[0]
     v = _C.debug_views(geom, binning, img, got["num_rendered"], P, st["image_width"], st["image_height"])
     ri = ref["state"].internals()
-    if got["num_rendered"] == ref["num_rendered"] and np.array_equal(got["radii"], ref["radii"]):
-        pl, rg = v["point_list"].cpu().numpy().astype(np.uint32), v["ranges"].cpu().numpy().astype(np.int64)
-        rpl, rrg = ri["point_list"], ri["ranges"].astype(np.int64)
-        for tile in range(rrg.shape[0]):  # the same Gaussians in the same order, tile by tile
-            np.testing.assert_array_equal(pl[rg[tile, 0]:rg[tile, 1]], rpl[rrg[tile, 0]:rrg[tile, 1]],
-                                          err_msg=f"tile {tile}")
+    pl, rg = v["point_list"].cpu().numpy().astype(np.uint32), v["ranges"].cpu().numpy().astype(np.int64)
+    rpl, rrg = ri["point_list"], ri["ranges"].astype(np.int64)
+    exact = got["num_rendered"] == ref["num_rendered"] and np.array_equal(got["radii"], ref["radii"])
+    for tile in range(rrg.shape[0]):
+        a, b = pl[rg[tile, 0]:rg[tile, 1]], rpl[rrg[tile, 0]:rrg[tile, 1]]
+        if exact:  # the same Gaussians in the same order, tile by tile
+            np.testing.assert_array_equal(a, b, err_msg=f"tile {tile}")
+        else:  # a radius flip adds / drops a Gaussian: the common ones keep their order
+            common = np.intersect1d(a, b)
+            np.testing.assert_array_equal(a[np.isin(a, common)], b[np.isin(b, common)], err_msg=f"tile {tile}")
     nc_ref = ri["n_contrib"].astype(np.int64)
     nc = v["n_contrib"].cpu().numpy().astype(np.int64)
     assert (nc != nc_ref).mean() < 2e-3
