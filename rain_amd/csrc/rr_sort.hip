@@ -408,13 +408,25 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
         if (!last && kdst == nullptr) return g_why = "no key storage", hipErrorInvalidValue;
         if (!(p == 0 && first_counts_ready)) {
             if (p == 0 && unit_len) return g_why = "sparse units need producer counts", hipErrorInvalidValue;
-            auto count = dbits > 8 ? (rounds <= 2 ? k_rs_count<K, 2, 9> : rounds <= 4 ? k_rs_count<K, 4, 9> : k_rs_count<K, kMaxRounds, 9>)
-                                   : (rounds <= 2 ? k_rs_count<K, 2, 8> : rounds <= 4 ? k_rs_count<K, 4, 8> : k_rs_count<K, kMaxRounds, 8>);
+            auto count = dbits > 8 ? (rounds <= 2   ? k_rs_count<K, 2, 9>
+                                      : rounds <= 4 ? k_rs_count<K, 4, 9>
+                                      : rounds <= 8 ? k_rs_count<K, 8, 9>
+                                                    : k_rs_count<K, kMaxRounds, 9>)
+                                   : (rounds <= 2   ? k_rs_count<K, 2, 8>
+                                      : rounds <= 4 ? k_rs_count<K, 4, 8>
+                                      : rounds <= 8 ? k_rs_count<K, 8, 8>
+                                                    : k_rs_count<K, kMaxRounds, 8>);
             count<<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev);
         }
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
-        auto scatter = dbits > 8 ? (rounds <= 2 ? k_rs_scatter<K, 2, 9> : rounds <= 4 ? k_rs_scatter<K, 4, 9> : k_rs_scatter<K, kMaxRounds, 9>)
-                                 : (rounds <= 2 ? k_rs_scatter<K, 2, 8> : rounds <= 4 ? k_rs_scatter<K, 4, 8> : k_rs_scatter<K, kMaxRounds, 8>);
+        auto scatter = dbits > 8 ? (rounds <= 2   ? k_rs_scatter<K, 2, 9>
+                                    : rounds <= 4 ? k_rs_scatter<K, 4, 9>
+                                    : rounds <= 8 ? k_rs_scatter<K, 8, 9>
+                                                  : k_rs_scatter<K, kMaxRounds, 9>)
+                                 : (rounds <= 2   ? k_rs_scatter<K, 2, 8>
+                                    : rounds <= 4 ? k_rs_scatter<K, 4, 8>
+                                    : rounds <= 8 ? k_rs_scatter<K, 8, 8>
+                                                  : k_rs_scatter<K, kMaxRounds, 8>);
         scatter<<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets, units,
                                                s.totals, p == 0 ? unit_len : nullptr, n_dev,
                                                last ? gather_src : nullptr, last ? gather_dst : nullptr);
