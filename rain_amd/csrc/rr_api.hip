@@ -129,7 +129,7 @@ Geom carve_geom(void* buf, int P) {
     g.block_sums = c.take<uint2>((n + 255) / 256);
     g.block_wide = c.take<uint32_t>((n + 255) / 256);
     g.totals = c.take<unsigned long long>(3);
-    g.temp_bytes = std::max(depth_sort_temp(P), scan_temp(P));
+    g.temp_bytes = std::max({depth_sort_temp(P), scan_temp(P), pair_scan_temp_bytes(P)});
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
     return g;
@@ -525,9 +525,11 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
         {
             StageTimer tm(RR_STAGE_SCAN, st);
             size_t tb = gm.temp_bytes;
-            RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, static_cast<const uint2*>(gm.tiles_sorted), gm.offsets,
-                                             (size_t)P, SatAdd2(), st),
-                     "tile-count scan");
+            if (!launch_pair_scan(gm.tiles_sorted, gm.offsets, P, gm.temp, st))  // P > 16.7M: device-wide scan
+                RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, static_cast<const uint2*>(gm.tiles_sorted),
+                                                 gm.offsets, (size_t)P, SatAdd2(), st),
+                         "tile-count scan");
+            RR_CHECK(hipGetLastError(), "tile-count scan");
         }
         RR_STAGE_CHECK("scan");
         return RR_OK;

@@ -118,6 +118,14 @@ struct GaussBwdArgs {
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);
+// Inclusive scan of the per-Gaussian {pairs, rect tiles} in depth order, saturating at 2^32 - 1
+// per component (rasterizer_impl.cu:269).  Two launches: per-block totals, then each block adds
+// the totals of the blocks before it to its own scan.  temp: pair_scan_temp_bytes(P); false when
+// P is too large for this scheme (the caller then uses a device-wide scan).
+constexpr int kPairScanItems = 2048;                 // items per block (256 threads x 8)
+constexpr int kPairScanMaxBlocks = 8192;             // each block sums up to this many totals
+size_t pair_scan_temp_bytes(int P);
+bool launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_t st);
 template <typename K>
 struct DupArgs {
     int P;
