@@ -546,24 +546,38 @@ __global__ __launch_bounds__(256) void k_expand(uint32_t n_host, const uint32_t*
     const int X = bin % bgx, Y = bin / bgx;
     const uint32_t n = n_dev ? *n_dev : n_host;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    // 256-ary search: each round probes 256 evenly spaced keys at once (one load latency per round,
-    // 3 rounds for 16M pairs, instead of a 24-deep chain of dependent loads)
-    auto lower_bound = [&](uint32_t v) {
-        uint32_t l = 0, h = n;  // answer in [l, h]
-        while (h - l > 1) {
-            const uint32_t step = (h - l + 255) / 256;
-            const uint32_t idx = l + (uint32_t)t * step;
-            const int c = __syncthreads_count(idx < h && (uint32_t)keys[idx] < v);  // probes below v
-            // probes 0..c-1 are below v: the answer lies in (l + (c-1) step, l + c step]
-            const uint32_t nl = c == 0 ? l : l + (uint32_t)(c - 1) * step + 1u;
-            const uint32_t nh = min(h, l + (uint32_t)c * step);
-            l = nl;
-            h = nh;
+    // 256-ary searches for the bin's first pair and the next bin's: each round probes 256 evenly
+    // spaced keys at once (one load latency per round, 3 rounds for 16M pairs, instead of a 24-deep
+    // chain of dependent loads), and the two searches share their rounds (their loads in flight
+    // together)
+    const uint32_t v0 = (uint32_t)bin, v1 = (uint32_t)bin + 1u;
+    uint32_t l0 = 0, h0 = n, l1 = 0, h1 = n;  // answers in [l, h]
+    while (h0 - l0 > 1 || h1 - l1 > 1) {
+        const bool a0 = h0 - l0 > 1, a1 = h1 - l1 > 1;
+        const uint32_t s0 = (h0 - l0 + 255) / 256, s1 = (h1 - l1 + 255) / 256;
+        const uint32_t i0 = l0 + (uint32_t)t * s0, i1 = l1 + (uint32_t)t * s1;
+        const bool q0 = a0 && i0 < h0, q1 = a1 && i1 < h1;
+        const uint32_t k0 = q0 ? (uint32_t)keys[i0] : 0u, k1 = q1 ? (uint32_t)keys[i1] : 0u;
+        const int c0 = __syncthreads_count(q0 && k0 < v0);  // probes below v
+        const int c1 = __syncthreads_count(q1 && k1 < v1);
+        // probes 0..c-1 are below v: the answer lies in (l + (c-1) step, l + c step]
+        if (a0) {
+            const uint32_t nl = c0 == 0 ? l0 : l0 + (uint32_t)(c0 - 1) * s0 + 1u;
+            h0 = min(h0, l0 + (uint32_t)c0 * s0);
+            l0 = nl;
         }
-        if (l < h) l += (uint32_t)__syncthreads_count((uint32_t)keys[l] < v) != 0 ? 1u : 0u;
-        return l;
-    };
-    const uint32_t lo = lower_bound((uint32_t)bin), hi = lower_bound((uint32_t)bin + 1u);
+        if (a1) {
+            const uint32_t nl = c1 == 0 ? l1 : l1 + (uint32_t)(c1 - 1) * s1 + 1u;
+            h1 = min(h1, l1 + (uint32_t)c1 * s1);
+            l1 = nl;
+        }
+    }
+    {
+        const uint32_t k0 = l0 < h0 ? (uint32_t)keys[l0] : 0u, k1 = l1 < h1 ? (uint32_t)keys[l1] : 0u;
+        if (l0 < h0) l0 += k0 < v0 ? 1u : 0u;  // block-uniform: every thread read the same key
+        if (l1 < h1) l1 += k1 < v1 ? 1u : 0u;
+    }
+    const uint32_t lo = l0, hi = l1;
     const uint32_t len = hi - lo;
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t dst0 = out_base + 4u * lo;
