@@ -573,13 +573,19 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     d.gx = gx; d.gy = gy; d.cull = cull;
     // phase A (or the only phase): pairs [0, LA) for every tile
     const RadixPlan pa = tile_plan<K>(bn.temp, LA, bn.bits);
+    const RadixPlan pb = tile_plan<K>(bn.temp, LB, bn.bits);  // phase B (early-stop binning)
+    bool starts_b = false;  // phase B's window starts computed with phase A's
     if (LA > 0) {
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
             d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L = LA;
             d.zero = reinterpret_cast<uint32_t*>(im.ranges); d.nzero = (int)(im.zero_bytes / sizeof(uint32_t));
             d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
-            launch_duplicate<K>(d, st);
+            if (early && LB > 0) {
+                d.first_b = bn.first + pa.units; d.pair0_b = LA; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
+            }
+            starts_b = launch_duplicate<K>(d, st);
+            d.first_b = nullptr; d.nwin_b = 0;
         }
         RR_STAGE_CHECK("duplicate");
         {
@@ -605,7 +611,6 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     RR_STAGE_CHECK("blend forward");
     if (!early) return RR_OK;
     // phase B: pairs [LA, L), only for tiles phase A left open; positions LA.. of the arrays
-    const RadixPlan pb = tile_plan<K>(bn.temp, LB, bn.bits);
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
         launch_open_sat(gx, gy, im.open, im.sat, im.open_bits, st);
@@ -613,6 +618,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         d.keys = keys + LA; d.vals = bn.vals + LA; d.dbits = pb.dbits0; d.counts = pb.counts;
         d.sat = im.sat; d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
         d.zero = nullptr; d.nzero = 0;
+        d.starts_done = starts_b;
         launch_duplicate<K>(d, st);
     }
     RR_STAGE_CHECK("duplicate (phase B)");

@@ -284,16 +284,24 @@ bool launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_
 // First Gaussian (depth rank) of every window of `win` consecutive pairs starting at pair0:
 // window k = [pair0 + k*win, pair0 + (k+1)*win) starts inside the pair range [a, b) of exactly
 // one Gaussian.
+// A second window set (pair0_b, win_b, nwin_b, first_b; nwin_b = 0: none) is marked in the same pass.
 __global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __restrict__ offsets, uint32_t pair0,
                                                        uint32_t win, int nwin, uint32_t* __restrict__ first,
-                                                       uint32_t* __restrict__ zero, int nzero) {
+                                                       uint32_t pair0_b, uint32_t win_b, int nwin_b,
+                                                       uint32_t* __restrict__ first_b, uint32_t* __restrict__ zero,
+                                                       int nzero) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     for (int i = s; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0u;
     if (s >= P) return;
     const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
-    if (a == b || b <= pair0) return;
-    const uint32_t k0 = a <= pair0 ? 0u : (a - pair0 + win - 1) / win;
-    for (uint32_t k = k0; k <= (b - 1 - pair0) / win && k < (uint32_t)nwin; k++) first[k] = (uint32_t)s;
+    if (a == b) return;
+    auto mark = [&](uint32_t p0, uint32_t w, int nw, uint32_t* f) {
+        if (nw <= 0 || b <= p0) return;
+        const uint32_t k0 = a <= p0 ? 0u : (a - p0 + w - 1) / w;
+        for (uint32_t k = k0; k <= (b - 1 - p0) / w && k < (uint32_t)nw; k++) f[k] = (uint32_t)s;
+    };
+    mark(pair0, win, nwin, first);
+    mark(pair0_b, win_b, nwin_b, first_b);
 }
 
 // 2-D inclusive prefix sum of the open-tile flags (phase B's per-Gaussian rectangle test):
@@ -639,20 +647,24 @@ void launch_preprocess(const PreArgs& a, hipStream_t st) {
 }
 
 template <typename K>
-void launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
+bool launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
     if (d.P == 0 || d.nwin == 0 || d.win > (uint32_t)kSortMaxUnit) {  // win comes from radix_sort_plan
         if (d.zero && d.nzero > 0) (void)hipMemsetAsync(d.zero, 0, (size_t)d.nzero * sizeof(uint32_t), st);
-        return;
+        return false;
     }
-    k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.P, d.offsets, d.pair0, d.win, d.nwin, d.first, d.zero,
-                                                     d.zero ? d.nzero : 0);
+    const bool second = d.first_b && d.nwin_b > 0 && d.win_b > 0 && d.win_b <= (uint32_t)kSortMaxUnit;
+    if (!d.starts_done)
+        k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.P, d.offsets, d.pair0, d.win, d.nwin, d.first, d.pair0_b,
+                                                         second ? d.win_b : 1u, second ? d.nwin_b : 0,
+                                                         d.first_b, d.zero, d.zero ? d.nzero : 0);
     auto kern = d.sat ? k_duplicate<K, true> : k_duplicate<K, false>;
     kern<<<d.nwin, 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
                                             d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts, d.nwin,
                                             d.sat, d.open_bits, d.unit_len, d.n_total);
+    return !d.starts_done && second;
 }
-template void launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
-template void launch_duplicate<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
+template bool launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
+template bool launch_duplicate<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
 
 void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_t* open_bits, hipStream_t st) {
     if ((size_t)(gx + 1) * (gy + 1) <= (size_t)kSatLds)

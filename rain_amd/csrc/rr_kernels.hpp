@@ -153,9 +153,17 @@ struct DupArgs {
     // readback)
     uint32_t* zero;
     int nzero;
+    // optional second window set (the phase-B windows, computed in the phase-A launch of the
+    // window-starts kernel: one launch less on the path); starts_done: this pass's windows were
+    // computed that way, skip the kernel
+    uint32_t* first_b;
+    uint32_t pair0_b, win_b;
+    int nwin_b;
+    bool starts_done;
 };
+// returns whether the window starts (both sets) were computed
 template <typename K>
-void launch_duplicate(const DupArgs<K>& d, hipStream_t st);
+bool launch_duplicate(const DupArgs<K>& d, hipStream_t st);
 void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_t* open_bits, hipStream_t st);
 template <typename K>
 void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,

@@ -15,7 +15,7 @@ k = b['kernels']
 out = [f"{v}: {b['value']:.1f} it/s " + " ".join(f"{n} {k[n]['ms_per_step']*1e3:.1f}" for n in ('preprocess','depth_sort','scan','duplicate','tile_sort','ranges'))]
 for f in glob.glob(d + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if any(k in r["Name"] for k in ("k_expand",)):
+        if any(k in r["Name"] for k in ("k_window_starts", "k_duplicate")):
             out.append(f"  {r['Name'][:48]} calls {r['Calls']} avg {float(r['AverageNs'])/1e3:.2f} us")
 print("\n".join(out))
 PY
