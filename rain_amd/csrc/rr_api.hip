@@ -746,11 +746,14 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
     hipStream_t st = (hipStream_t)stream;
     const int gx = grid_x(W), gy = grid_y(H);
     float* gacc = static_cast<float*>(workspace);
+    const bool blend = L > 0 && binning_buffer;
+    uint32_t* order = blend && bwd_tile_order() ? im.order : nullptr;
     {
         StageTimer tm(RR_STAGE_MEMSET, st);
-        RR_CHECK(hipMemsetAsync(gacc, 0, (size_t)P * GACC_STRIDE * sizeof(float), st), "memset accumulators");
+        launch_bwd_prologue(gacc, (size_t)P * GACC_STRIDE, gx * gy, im.tile_max, order, st);
+        RR_CHECK(hipGetLastError(), "clear accumulators");
     }
-    if (L > 0 && binning_buffer) {
+    if (blend) {
         StageTimer tm(RR_STAGE_BLEND_BWD, st);
         BlendBwdArgs b{};
         b.W = W; b.H = H; b.gx = gx; b.gy = gy;
@@ -758,7 +761,7 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
         b.tile_max = im.tile_max;
         b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.bg = cam->background; b.dL_dpix = dL_dpix;
         b.gacc = gacc;
-        b.order = bwd_tile_order() ? im.order : nullptr;
+        b.order = order;
         launch_blend_bwd(b, st);
     }
     RR_STAGE_CHECK("blend backward");

@@ -197,9 +197,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
 // dispatched late runs alone on its SIMD after the rest of the grid has drained.  One workgroup:
 // counting sort of the tiles by descending min(tile_max / 4, 1023) (order inside a bucket free).
 // The forward blends use the same order with the tile's list length as its cost (ranges != null).
-__global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __restrict__ cost,
-                                                     const uint2* __restrict__ ranges,
-                                                     uint32_t* __restrict__ order) {
+__device__ __forceinline__ void tile_order_body(int T, const uint32_t* __restrict__ cost,
+                                                const uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
     __shared__ uint32_t hist[1024];
     __shared__ uint32_t wsum[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -237,6 +236,38 @@ __global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __re
     for (int r = 0; r < kReg; r++)
         if (t + r * 1024 < T) order[atomicAdd(&hist[bk[r]], 1u)] = (uint32_t)(t + r * 1024);
     for (int i = t + kReg * 1024; i < T; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __restrict__ cost,
+                                                     const uint2* __restrict__ ranges,
+                                                     uint32_t* __restrict__ order) {
+    tile_order_body(T, cost, ranges, order);
+}
+
+// Backward prologue: the gradient accumulators are cleared by every workgroup but the first,
+// which computes the backward's tile order meanwhile (a one-workgroup job that otherwise ran
+// alone on the GPU for ~11 us between the clear and the blend).
+__global__ __launch_bounds__(1024) void k_bwd_prologue(float4* __restrict__ gacc, size_t n4, int T,
+                                                       const uint32_t* __restrict__ tile_max,
+                                                       uint32_t* __restrict__ order) {
+    if (order) {
+        if (blockIdx.x == 0) {
+            tile_order_body(T, tile_max, nullptr, order);
+            return;
+        }
+    }
+    const size_t zb = order ? blockIdx.x - 1 : blockIdx.x, nzb = order ? gridDim.x - 1 : gridDim.x;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (size_t i = zb * 1024 + threadIdx.x; i < n4; i += nzb * 1024) gacc[i] = z;
+}
+
+void launch_bwd_prologue(float* gacc, size_t nfloats, int T, const uint32_t* tile_max, uint32_t* order,
+                         hipStream_t st) {
+    const size_t n4 = nfloats / 4;  // P * GACC_STRIDE, a multiple of 4
+    const size_t zb = std::max<size_t>(1, std::min<size_t>((n4 + 1023) / 1024, 2048));
+    const bool ord = order && T > 0;
+    k_bwd_prologue<<<(unsigned)(zb + (ord ? 1 : 0)), 1024, 0, st>>>(reinterpret_cast<float4*>(gacc), n4, T, tile_max,
+                                                                    ord ? order : nullptr);
 }
 
 namespace {
@@ -305,7 +336,7 @@ int set_tuning(const char* key, int value) {
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
-    if (a.order) k_tile_order<<<1, 1024, 0, st>>>(T, a.tile_max, nullptr, a.order);
+    // a.order was filled by the prologue (launch_bwd_prologue)
     const int nw = g_bwd_waves ? g_bwd_waves : env_waves("RAIN_BLEND_BWD_WAVES", kBwdWavesDefault);
     switch (nw) {
         case 2: k_blend_bwd<2, 1><<<T, 128, 0, st>>>(a); break;

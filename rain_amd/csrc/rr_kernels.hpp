@@ -171,7 +171,10 @@ void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint3
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
-void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);
+void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);  // a.order: from launch_bwd_prologue
+// clears the nfloats gradient accumulators and, with order, writes the backward's tile order
+void launch_bwd_prologue(float* gacc, size_t nfloats, int T, const uint32_t* tile_max, uint32_t* order,
+                         hipStream_t st);
 
 // Largest sort unit (items per workgroup) of rr_sort.hip; the duplicate kernel's LDS windows are
 // sort units, so it sizes its staging arrays with this too.
