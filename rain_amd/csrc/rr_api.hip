@@ -323,53 +323,8 @@ struct Mailbox {
 };
 thread_local Mailbox g_mailbox;
 
-// src: the preprocess's per-block sums of {pairs, rect tiles}; one workgroup adds them in 64 bits
-// (fixed order), saturates to 32 bits (the host rejects anything above 2^31 anyway) and publishes,
-// with the OR of the blocks' wide-depth-key flags.
-__global__ __launch_bounds__(1024) void k_publish_pair_counts(const uint2* __restrict__ src,
-                                                               const uint32_t* __restrict__ src_wide, int nb,
-                                                               uint32_t* box, uint32_t seq, unsigned long long* copy) {
-    __shared__ unsigned long long s_n[16], s_r[16];
-    unsigned long long n = 0, r = 0;
-    uint32_t wide = 0;
-    for (int i = threadIdx.x; i < nb; i += 1024) {
-        const uint2 v = src[i];
-        n += v.x;
-        r += v.y;
-        wide |= src_wide[i];
-    }
-    wide = __syncthreads_or(wide != 0) ? 1u : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        n += __shfl_xor(n, o);
-        r += __shfl_xor(r, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        s_n[threadIdx.x >> 6] = n;
-        s_r[threadIdx.x >> 6] = r;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        n = r = 0;
-        for (int w = 0; w < 16; w++) {
-            n += s_n[w];
-            r += s_r[w];
-        }
-        const uint32_t x = n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
-        const uint32_t y = r > 0xffffffffull ? 0xffffffffu : (uint32_t)r;
-        copy[0] = x;  // device copy for the no-mailbox path
-        copy[1] = y;
-        copy[2] = wide;
-        if (box) {
-            __hip_atomic_store(box + 0, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(box + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(box + 3, wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
-
-// The publish is enqueued right after the preprocess (whose block sums give the totals), so the
+// The publish (rr_kernels.hpp publish_pair_counts_block) runs as an extra workgroup of the depth
+// sort's first count launch, right after the preprocess whose block sums give the totals, so the
 // host learns the pair count while the depth sort and the scan still run, and has the binning
 // launches queued before the GPU gets to them.
 struct PairCountRead {
@@ -377,8 +332,8 @@ struct PairCountRead {
     uint32_t seq = 0;  // 0: no mailbox (copy + synchronise at wait time)
 };
 
-hipError_t pair_counts_publish(const uint2* block_sums, const uint32_t* block_wide, int nb, unsigned long long* copy,
-                               PairCountRead& r, hipStream_t st) {
+PublishJob pair_counts_job(const uint2* block_sums, const uint32_t* block_wide, int nb, unsigned long long* copy,
+                           PairCountRead& r) {
     Mailbox& mb = g_mailbox;
     r.copy = copy;
     r.seq = 0;
@@ -395,8 +350,7 @@ hipError_t pair_counts_publish(const uint2* block_sums, const uint32_t* block_wi
         }
     }
     if (!mb.failed) r.seq = ++mb.seq == 0 ? ++mb.seq : mb.seq;  // 0 is the mailbox's initial value
-    k_publish_pair_counts<<<1, 1024, 0, st>>>(block_sums, block_wide, nb, mb.failed ? nullptr : mb.dev, r.seq, copy);
-    return hipGetLastError();
+    return PublishJob{block_sums, block_wide, nb, mb.failed ? nullptr : mb.dev, r.seq, copy};
 }
 
 hipError_t pair_counts_copy(const unsigned long long* src, uint2* out, bool* wide, hipStream_t st) {
@@ -513,17 +467,16 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
         launch_preprocess(a, st);
     }
     RR_STAGE_CHECK("preprocess");
-    RR_CHECK(pair_counts_publish(gm.block_sums, gm.block_wide, (P + 255) / 256, gm.totals, rd, st),
-             "publish pair counts");
+    const PublishJob pub = pair_counts_job(gm.block_sums, gm.block_wide, (P + 255) / 256, gm.totals, rd);
     // depth sort (rasterizer_impl.cu:295 sorts {tile, depth} keys; here the Gaussians by depth,
     // then the pairs stably by bin) and the scan of the pair counts in depth order
-    auto sort_and_scan = [&](int key_bits) -> int {
+    auto sort_and_scan = [&](int key_bits, const PublishJob* publish) -> int {
         {
             StageTimer tm(RR_STAGE_DEPTH_SORT, st);
             size_t tb = gm.temp_bytes;
             RR_CHECK(radix_sort_pairs<uint32_t>(gm.temp, tb, gm.depth_keys, gm.depth_keys_sorted, nullptr,
                                                 gm.idx_sorted, (size_t)P, 0, key_bits, st, false, nullptr, nullptr,
-                                                gm.tiles, gm.tiles_sorted),
+                                                gm.tiles, gm.tiles_sorted, publish),
                      "depth sort");
         }
         RR_STAGE_CHECK("depth sort");
@@ -539,7 +492,7 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
         RR_STAGE_CHECK("scan");
         return RR_OK;
     };
-    if (int rc = sort_and_scan(kDepthKeyBits)) return rc;
+    if (int rc = sort_and_scan(kDepthKeyBits, &pub)) return rc;
     // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
     // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
     uint2 tot = make_uint2(0u, 0u);
@@ -548,7 +501,7 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     // a visible depth beyond the 27-bit key range (~13107): the 3-pass order is not the depth
     // order, so sort again on all 32 bits before anything reads the sorted arrays
     if (wide)
-        if (int rc = sort_and_scan(32)) return rc;
+        if (int rc = sort_and_scan(32, nullptr)) return rc;
     if (tot.x > 0x1fffffffu || tot.y > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^29 bin/Gaussian pairs");
     *num_rendered = (int)tot.y;
     *num_pairs = (int)tot.x;

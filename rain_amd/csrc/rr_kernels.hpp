@@ -5,6 +5,57 @@
 
 namespace rr {
 
+// The frame's pair counts, published to the host: the preprocess's per-block sums of {pairs, rect
+// tiles} are added in 64 bits (fixed order), saturated to 32 bits (the host rejects anything above
+// 2^31 anyway) and stored with the OR of the blocks' wide-depth-key flags into a coherent pinned
+// mailbox (system-scope release of the sequence number; rr_api.hip pair_counts_wait spins on it)
+// and into a device copy for the no-mailbox path.  One workgroup of 256 threads.
+struct PublishJob {
+    const uint2* src;
+    const uint32_t* src_wide;
+    int nb;
+    uint32_t* box;  // null: no mailbox
+    uint32_t seq;
+    unsigned long long* copy;  // [3]
+};
+__device__ inline void publish_pair_counts_block(const PublishJob& j) {
+    __shared__ unsigned long long s_n[4], s_r[4];
+    unsigned long long n = 0, r = 0;
+    uint32_t wide = 0;
+    for (int i = threadIdx.x; i < j.nb; i += 256) {
+        const uint2 v = j.src[i];
+        n += v.x;
+        r += v.y;
+        wide |= j.src_wide[i];
+    }
+    wide = __syncthreads_or(wide != 0) ? 1u : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        n += __shfl_xor(n, o);
+        r += __shfl_xor(r, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_n[threadIdx.x >> 6] = n;
+        s_r[threadIdx.x >> 6] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        n = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+        r = s_r[0] + s_r[1] + s_r[2] + s_r[3];
+        const uint32_t x = n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
+        const uint32_t y = r > 0xffffffffull ? 0xffffffffu : (uint32_t)r;
+        j.copy[0] = x;
+        j.copy[1] = y;
+        j.copy[2] = wide;
+        if (j.box) {
+            __hip_atomic_store(j.box + 0, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(j.box + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(j.box + 3, wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(j.box + 2, j.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 struct PreArgs {
     int P, D, M, W, H, gx, gy, prefiltered;
     float tanfovx, tanfovy, focal_x, focal_y, scale_modifier, low_pass;
@@ -194,7 +245,10 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
                             const uint32_t* n_dev = nullptr, const uint2* gather_src = nullptr,
-                            uint2* gather_dst = nullptr);
+                            uint2* gather_dst = nullptr, const struct PublishJob* publish = nullptr);
+// publish (optional, needs !first_counts_ready): one extra workgroup of the first count launch
+// runs the pair-count publish (rr_api.hip pair_counts_publish) beside the counting instead of a
+// launch of its own between the preprocess and the sort.
 // gather_src / gather_dst (optional): the last pass also writes gather_dst[i] = gather_src[vals_out[i]]
 // (the depth sort hands the scan its {pairs, rect} in depth order, a contiguous array).
 const char* radix_sort_last_error();

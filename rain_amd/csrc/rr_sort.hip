@@ -59,7 +59,13 @@ __device__ __forceinline__ uint32_t unit_length(const uint32_t* unit_len, const 
 template <typename K, int MAXR, int DB>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ keys, size_t n, int shift, int dbits,
                                                           int rounds, uint32_t* __restrict__ counts, int units,
-                                                          const uint32_t* __restrict__ n_dev) {
+                                                          const uint32_t* __restrict__ n_dev, PublishJob pub,
+                                                          int has_pub) {
+    static_assert(64 * kWaves == 256, "publish_pair_counts_block runs on 256 threads");
+    if (has_pub && (int)blockIdx.x == units) {  // the extra workgroup (block-uniform)
+        publish_pair_counts_block(pub);
+        return;
+    }
     __shared__ uint32_t hist[1 << DB];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
@@ -383,12 +389,13 @@ template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev,
-                            const uint2* gather_src, uint2* gather_dst) {
+                            const uint2* gather_src, uint2* gather_dst, const PublishJob* publish) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
     g_why = "";
     if (n > 0xffffffffull || bits <= 0 || bits > (int)(8 * sizeof(K))) return g_why = "bad size/bits", hipErrorInvalidValue;
     if (unit_len && !n_dev) return g_why = "sparse units without n_dev", hipErrorInvalidValue;
+    if (publish && first_counts_ready) return g_why = "publish rides on the first count launch", hipErrorInvalidValue;
     const SortLayout s = sort_layout<K>(temp, n, bits);
     if (temp_bytes < s.total) return g_why = "temp too small", hipErrorInvalidValue;
     const int passes = sort_passes(bits);
@@ -416,7 +423,9 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                                       : rounds <= 4 ? k_rs_count<K, 4, 8>
                                       : rounds <= 8 ? k_rs_count<K, 8, 8>
                                                     : k_rs_count<K, kMaxRounds, 8>);
-            count<<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev);
+            const bool pub = p == 0 && publish;
+            count<<<units + (pub ? 1 : 0), 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev,
+                                                                 pub ? *publish : PublishJob{}, pub ? 1 : 0);
         }
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
         auto scatter = dbits > 8 ? (rounds <= 2   ? k_rs_scatter<K, 2, 9>
@@ -443,10 +452,10 @@ template size_t radix_sort_temp_bytes<uint16_t>(size_t, int);
 template size_t radix_sort_temp_bytes<uint32_t>(size_t, int);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, const uint2*, uint2*);
+                                               const uint32_t*, const uint2*, uint2*, const PublishJob*);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, const uint2*, uint2*);
+                                               const uint32_t*, const uint2*, uint2*, const PublishJob*);
 template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int);
 template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int);
 
