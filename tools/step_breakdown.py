@@ -1,7 +1,9 @@
 """Per-training-step kernel breakdown from a rocprofv3 kernel trace (csv).
 
 Steps are delimited by the backward blend kernel; prints the mean step period and the mean time
-per step of every kernel name, heaviest first.
+per step of every kernel name, heaviest first.  The defaults cover bench.py's timed loop of the
+default run (10 warmup + 20 stage-profiled steps, then the 100 timed ones; the bracket and
+reference-API legs that follow run different kernels).
 
     python tools/step_breakdown.py gpurun_out/prof_x [--first 100 --count 80]
 """
@@ -15,8 +17,8 @@ import os
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--first", type=int, default=100)
-    ap.add_argument("--count", type=int, default=80)
+    ap.add_argument("--first", type=int, default=30)
+    ap.add_argument("--count", type=int, default=99)
     a = ap.parse_args()
     path = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda x: int(x["Start_Timestamp"]))
