@@ -143,14 +143,18 @@ def _free_port():
     return p
 
 
-def test_view_sharded_step_gloo_world2(oracle, tmp_path, monkeypatch):
-    """2 ranks x 1 view per step == 1 process accumulating the same 2 views' gradients (mean),
-    summing their densification statistics, then one Adam step; replicas stay identical."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_view_sharded_step_gloo(oracle, tmp_path, monkeypatch, world):
+    """N ranks x 1 view per step == 1 process accumulating the same N views' gradients (mean),
+    summing their densification statistics, then one Adam step; replicas stay identical.  World 4
+    also covers a flat layout padded to 4 slices (the driver's N = 4 / 8 runs shard the same way)."""
     out = str(tmp_path / "r")
-    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
-    r0, r1 = torch.load(out + ".0", weights_only=True), torch.load(out + ".1", weights_only=True)
-    for k in r0:
-        assert torch.equal(r0[k], r1[k]), f"replicas diverged on {k}"
+    mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    r0 = rs[0]
+    for r1 in rs[1:]:
+        for k in r0:
+            assert torch.equal(r0[k], r1[k]), f"replicas diverged on {k}"
 
     # single-process reference with the same view schedule
     monkeypatch.setattr(dgr, "_C", oracle_c)
@@ -160,7 +164,7 @@ def test_view_sharded_step_gloo_world2(oracle, tmp_path, monkeypatch):
     g = _model(800, 1, seed=3)
     opt = OptimizationParams()
     g.training_setup(opt)
-    sampler = ViewSampler(len(cams), 2, seed=5)
+    sampler = ViewSampler(len(cams), world, seed=5)
     bg = torch.zeros(3)
     for it in (1, 2, 3):
         g.update_learning_rate(it)
@@ -179,13 +183,24 @@ def test_view_sharded_step_gloo_world2(oracle, tmp_path, monkeypatch):
                 g.add_densification_stats(pkg["viewspace_points"], vis)
         with torch.no_grad():
             for acc, p in zip(grads, g.params()):
-                p.grad = acc / 2.0
+                p.grad = acc / float(world)
             g.optimizer.step()
             g.optimizer.zero_grad(set_to_none=True)
     ref = dict(zip(("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"), g.params()))
+    lrs = {grp["name"]: grp["lr"] for grp in g.optimizer.param_groups}
     for k, v in ref.items():
-        torch.testing.assert_close(r0[k], v.detach(), rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(r0["accum"], g.xyz_gradient_accum, rtol=1e-5, atol=1e-8)
+        if world == 2:  # a + b is order-free: the exchange's sums are the reference's
+            torch.testing.assert_close(r0[k], v.detach(), rtol=1e-5, atol=1e-7)
+            continue
+        # 4 views: the collective sums in its own order, so a gradient that cancels to ~0 across the
+        # views can change sign, and Adam's early steps (~ lr * sign(g)) then move that element the
+        # other way.  Bound it: few such elements, each within 2 * lr per step of the reference.
+        d = (r0[k] - v.detach()).abs()
+        off = d > 1e-7 + 1e-5 * v.detach().abs()
+        assert off.float().mean().item() <= 0.05, f"{k}: {off.sum().item()} elements off"
+        lr = lrs["xyz" if k == "xyz" else k]
+        assert d.max().item() <= 3 * 2 * 3 * lr, f"{k}: max diff {d.max().item()} vs lr {lr}"
+    torch.testing.assert_close(r0["accum"], g.xyz_gradient_accum, rtol=1e-5 if world == 2 else 1e-3, atol=1e-8)
     torch.testing.assert_close(r0["denom"], g.denom)
     torch.testing.assert_close(r0["maxr"], g.max_radii2D)
 
