@@ -1,5 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_multirank_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/t_mr.log 2>&1 || { tail -60 gpurun_out/t_mr.log; exit 1; }
-tail -5 gpurun_out/t_mr.log
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/t_gpu.log 2>&1 || { tail -40 gpurun_out/t_gpu.log; exit 1; }
+tail -1 gpurun_out/t_gpu.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
