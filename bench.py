@@ -6,10 +6,18 @@
     (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py ...)
 
 A "step" is one iteration of the reference's train.py loop (train.py:71-147) on every rank:
-lr update, render forward, L1+SSIM loss, backward through the MI355X rasterizer, (all-reduce),
-densification statistics, densify/prune every 100 iterations, Adam.  The timed window ends on an
-iteration that is a multiple of 100, so it contains floor(K/100) densify/prune events (the
-reference's 1-in-100 share).  value = iterations all ranks completed / wall time (max over ranks).
+lr update, render forward, L1+SSIM loss, backward through the MI355X rasterizer, (gradient
+exchange), densification statistics, densify/prune at every multiple of 100, Adam.  Iteration
+numbers (they drive the lr schedule and the densify/prune events, train.py:136-143):
+  warmup   W iterations ending on densify iteration 900 (allocator and densify path warm)
+  profile  901 .. 900+PW: every stage event-timed (the per-kernel breakdown)
+  999, 1000  each run alone between device syncs: an ordinary and a densify/prune iteration
+           (densify_iter_ms, densify_extra_ms)
+  timed    1001 .. 1000+K: it starts right after a densify iteration, so it holds exactly
+           floor(K/100) densify/prune events (iterations 1100, 1200, ...) — the reference's
+           1-in-100 share, rounded down; `iters_per_s_1in100` adds the measured extra cost of one
+           densify iteration per 100 to the ordinary steps of a window without one.
+value = iterations all ranks completed in the timed window / wall time (max over ranks).
 
 Data: synthetic and seeded (no datasets offline) — 1M random Gaussians (SURVEY §8(d) bench
 variant), 200 Fibonacci-sphere cameras, ground-truth images rendered from a second random model.
@@ -55,6 +63,9 @@ def parse():
                    help="forward-only leg renders the aux depth + normal outputs (BASELINE configs[4] stress)")
     p.add_argument("--binning-split", type=int, default=0,
                    help="early-stop binning: phase A = 1/N of the pairs (1 = one phase; 0 = library default)")
+    p.add_argument("--force-dist", action="store_true",
+                   help="init the RCCL process group and run the sharded exchange path even at world 1 "
+                        "(rehearses the multi-GPU code path on one GPU; not the headline configuration)")
     return p.parse_args()
 
 
@@ -104,7 +115,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    force = args.force_dist
+    if world > 1 or force:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -140,18 +152,17 @@ def main():
     gauss.spatial_lr_scale = extent
     opt = OptimizationParams()
     gauss.training_setup(opt)
-    trainer = Trainer(gauss, cams, gts, opt, pipe, TrainConfig(seed=0), scene_extent=extent)
+    trainer = Trainer(gauss, cams, gts, opt, pipe, TrainConfig(seed=0), scene_extent=extent,
+                      exchange=True if force else None)
 
     K, Wm = args.steps, args.warmup
     prof = not args.no_profile
     # untimed per-stage breakdown window (every stage event-timed) between warmup and the timed loop
     PW = min(20, K) if prof else 0
-    end_iter = max(1000, int(math.ceil((Wm + PW + K + 1) / 100.0)) * 100)
-    start_iter = end_iter - K - PW - Wm + 1
-    it = start_iter
-    for _ in range(Wm):
+    D0, D1 = 900, 1000  # densify/prune iterations (train.py:136-140: multiples of 100 in (500, 15000))
+    for it in range(D0 - Wm + 1, D0 + 1):
         trainer.step(it)
-        it += 1
+    it = D0 + 1
     breakdown, dom, step_dom = {}, None, None
     if prof:
         _native.Profiler.collect()  # drop anything recorded before the window
@@ -168,6 +179,23 @@ def main():
         step_dom = max(modeled, key=lambda k: breakdown[k][0]) if modeled else None
         hbm_bound = [k for k in modeled if k not in VALU_BOUND]
         dom = max(hbm_bound, key=lambda k: breakdown[k][0]) if hbm_bound else step_dom
+    # one ordinary and one densify/prune iteration, each alone between device syncs
+    one_ms = {}
+    for it in (D1 - 1, D1):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        info = trainer.step(it)
+        torch.cuda.synchronize()
+        one_ms[it] = 1000.0 * (time.perf_counter() - t0)
+    assert info.densified, "iteration 1000 must densify"
+    if world > 1:
+        e = torch.tensor([one_ms[D1 - 1], one_ms[D1]], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        one_ms = {D1 - 1: float(e[0]), D1: float(e[1])}
+    it = D1 + 1
+    start_iter = it
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -195,6 +223,11 @@ def main():
         elapsed = float(e.item())
     iters_per_s = world * K / elapsed
     ms_per_step = 1000.0 * elapsed / K
+    end_iter = it - 1
+    n_densify = sum(1 for i in range(start_iter, end_iter + 1) if i % 100 == 0)
+    densify_extra_ms = one_ms[D1] - one_ms[D1 - 1]
+    # the reference's share (1 densify/prune iteration in 100) on top of the measured steps
+    ms_1in100 = ms_per_step + densify_extra_ms / 100.0 if n_densify == 0 else ms_per_step
 
     # the reference's own timing bracket (train.py:71-117: iter_start before render, iter_end after
     # loss.backward()): render forward + L1/SSIM + backward, no optimizer step, no densification
@@ -202,7 +235,8 @@ def main():
 
     # the same iteration through the reference's own API (what an unchanged train.py:109-147 runs):
     # render() -> GaussianRasterizer autograd -> getters' autograd -> torch.optim.Adam
-    api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, end_iter + 1, K if K < 30 else 30, world, dev)
+    api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, (end_iter // 100 + 1) * 100 + 1, K if K < 30 else 30,
+                      world, dev)
 
     # forward-only throughput (preprocess -> blend incl. sorts and the L read-back), no autograd
     Pn = gauss.get_xyz.shape[0]
@@ -299,8 +333,13 @@ def main():
                                f"densify/prune every 100 it + Adam), {P} Gaussians, {W}x{H}, SH {D}, "
                                f"view-sharded dp{world}",
                    "gaussians": P, "width": W, "height": H, "sh_degree": D, "views": args.views,
-                   "parallelism": f"dp{world} (view-sharded, RCCL all-reduce)" if world > 1 else "dp1",
-                   "iterations": [start_iter + Wm + PW, end_iter]},
+                   "parallelism": (f"dp{world} (view-sharded, RCCL reduce-scatter + all-gather)" if world > 1 else
+                                   "dp1 (RCCL exchange forced)" if force else "dp1"),
+                   "iterations": [start_iter, end_iter], "densify_events_in_window": n_densify},
+        "densify_iter_ms": round(one_ms[D1], 3),
+        "ordinary_iter_ms_alone": round(one_ms[D1 - 1], 3),
+        "densify_extra_ms": round(densify_extra_ms, 3),
+        "iters_per_s_1in100": round(world * 1000.0 / ms_1in100, 3),
         "forward_mpix_per_s": round(fwd_mpix, 2),
         "forward_outputs": "color+depth+normal" if args.aux_normal else "color+depth",
         "views_per_s": round(iters_per_s, 3),  # one view per rank per step: = value
@@ -319,7 +358,7 @@ def main():
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or force:
         dist.destroy_process_group()
 
 

@@ -271,9 +271,14 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *                         env RAIN_FWD_TILE_ORDER),
  *   "fwd_waves" / "bwd_waves" as rr_set_blend_config,
  *   "fwd_b_waves"    0/1  phase-B forward blend on 4 waves per tile (default 1),
- *   "sort_min_units" n    radix sorts pick the largest unit with >= n units (default 512; 0 resets),
+ *   "sort_min_units" n    radix sorts pick the largest unit with >= n units (default 256; 0 resets),
  *   "sort_min_units_tile" n  the same for the bin sorts (<= 16-bit keys; default 1024),
- *   "sort_max_rounds" r   cap on 64-item rounds per wave in a sort unit, 1..16 (default 16).
+ *   "sort_max_rounds" r   cap on 64-item rounds per wave in a sort unit, 1..16 (default 16),
+ *   "pair_scan_direct_blocks" n  pair-count scans of up to n blocks of 2048 Gaussians let every
+ *                         block sum the earlier block totals itself (2 launches); larger ones scan
+ *                         the totals in one workgroup first (3 launches); default 512, <0 resets,
+ *   "wide_bin_keys" 0/1   32-bit bin keys even when the bins fit 16 bits (default 0: only frames
+ *                         with more than 65536 bins of 32x32 px use them).
  * Results are identical for every setting.  Unknown keys return RR_ERR_ARG. */
 int rr_set_tuning(const char* key, int value);
 /* Diagnostics: device buffer of >= 8 * 8 * tiles u32 receiving one timing record per forward-blend

@@ -44,7 +44,9 @@ __device__ __forceinline__ AdamC adam_consts(double lr, float bc1, float bc2s, d
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamC& c) {
     m = __builtin_fmaf(c.w1, g - m, m);                                        // lerp (weight < 0.5 branch)
-    v = __builtin_fmaf(c.w2 * g, g, v * c.b2);                                 // mul_ then addcmul_
+    // mul_ then addcmul_: torch's foreach addcmul computes a + value * (b * c), so g * g is
+    // rounded on its own before the (contracted) multiply-add
+    v = __builtin_fmaf(c.w2, mul_rounded(g, g), v * c.b2);
     const float denom = __builtin_amdgcn_sqrtf(v) * c.inv_bc2s + c.eps;        // sqrt / bc2s + eps
     p = __builtin_fmaf(c.nstep, m * __builtin_amdgcn_rcpf(denom), p);          // addcdiv_
 }

@@ -1,12 +1,8 @@
 // rr_api.hip — C-ABI entry points (include/rain_raster.h): scratch carving, stage ordering,
-// rocPRIM sorts/scans, the single device->host sync, debug checks and event timing.
+// the single device->host sync, debug checks and event timing.
 //
 // Replaces CudaRasterizer::Rasterizer::{forward,backward,markVisible}
 // (rasterizer_impl.cu:130-142,187-430) and the pybind wrappers (rasterize_points.cu:24-212).
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
-
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -18,6 +14,13 @@
 #include "rr_kernels.hpp"
 
 using namespace rr;
+
+namespace rr {
+// rr_set_tuning "wide_bin_keys": 32-bit bin keys even when the bins fit 16 bits (the layout of
+// frames with more than 65536 bins, e.g. above 8K x 8K), so tests reach that path at small sizes
+bool g_wide_bin_keys = false;
+void set_wide_bin_keys(bool on) { g_wide_bin_keys = on; }
+}  // namespace rr
 
 namespace {
 
@@ -62,35 +65,16 @@ inline int grid_x(int W) { return (W + TILE_X - 1) / TILE_X; }
 inline int grid_y(int H) { return (H + TILE_Y - 1) / TILE_Y; }
 
 // ---- temp-storage queries ----
-// Component-wise saturating sum of {pairs, rect area}: associative on non-negative counts, and a
-// saturated total (>= 2^32) is caught by the 2^31 capacity check instead of wrapping silently.
-struct SatAdd2 {
-    __host__ __device__ uint2 operator()(const uint2& a, const uint2& b) const {
-        const uint32_t x = a.x + b.x, y = a.y + b.y;
-        return make_uint2(x < a.x ? 0xffffffffu : x, y < a.y ? 0xffffffffu : y);
-    }
-};
-// The scan reads tiles[] in depth order from tiles_sorted, which the depth sort's last pass
-// gathers while it writes idx_sorted (a transform iterator gathering inside the scan measured
-// 21 us per frame, most of it the scan blocks waiting on their random loads).
+// The pair-count scan (launch_pair_scan) reads tiles[] in depth order from tiles_sorted, which the
+// depth sort's last pass gathers while it writes idx_sorted (a transform iterator gathering inside
+// a scan measured 21 us per frame, most of it the scan blocks waiting on their random loads); it
+// saturates each component at 2^32 - 1, so an overflowing total is caught by the 2^31 capacity
+// check instead of wrapping silently.
 
 size_t depth_sort_temp(int P) {  // the 3-pass (9-bit digits) sort and the 32-bit fallback
     return P > 0 ? std::max(radix_sort_temp_bytes<uint32_t>((size_t)P, kDepthKeyBits),
                             radix_sort_temp_bytes<uint32_t>((size_t)P, 32))
                  : 0;
-}
-size_t scan_temp(int P) {
-    // memoized: queried by every carve (forward, render, backward) with the same P
-    static thread_local int last_p = -1;
-    static thread_local size_t last_bytes = 0;
-    if (P == last_p) return last_bytes;
-    size_t bytes = 0;
-    if (P > 0)
-        (void)rocprim::inclusive_scan(nullptr, bytes, (const uint2*)nullptr, (uint2*)nullptr, (size_t)P, SatAdd2(),
-                                      (hipStream_t)0);
-    last_p = P;
-    last_bytes = bytes;
-    return bytes;
 }
 template <typename K>
 size_t tile_sort_temp(int L, int bits) {
@@ -129,7 +113,7 @@ Geom carve_geom(void* buf, int P) {
     g.block_sums = c.take<uint2>((n + 255) / 256);
     g.block_wide = c.take<uint32_t>((n + 255) / 256);
     g.totals = c.take<unsigned long long>(3);
-    g.temp_bytes = std::max({depth_sort_temp(P), scan_temp(P), pair_scan_temp_bytes(P)});
+    g.temp_bytes = std::max(depth_sort_temp(P), pair_scan_temp_bytes(P));
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
     return g;
@@ -209,7 +193,7 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     Carver c(buf);
     Bin b;
     const int NB = bins_x(grid_x(W)) * bins_y(grid_y(H));
-    b.wide = NB > 65536;
+    b.wide = NB > 65536 || g_wide_bin_keys;
     b.bits = std::max(1, (int)higher_msb((uint32_t)NB));  // >= 1: the duplicate windows are sort units
     b.L = (uint32_t)std::max(L, 0);
     b.LA = early_split(b.L);
@@ -482,11 +466,7 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
         RR_STAGE_CHECK("depth sort");
         {
             StageTimer tm(RR_STAGE_SCAN, st);
-            size_t tb = gm.temp_bytes;
-            if (!launch_pair_scan(gm.tiles_sorted, gm.offsets, P, gm.temp, st))  // P > 16.7M: device-wide scan
-                RR_CHECK(rocprim::inclusive_scan(gm.temp, tb, static_cast<const uint2*>(gm.tiles_sorted),
-                                                 gm.offsets, (size_t)P, SatAdd2(), st),
-                         "tile-count scan");
+            launch_pair_scan(gm.tiles_sorted, gm.offsets, P, gm.temp, st);
             RR_CHECK(hipGetLastError(), "tile-count scan");
         }
         RR_STAGE_CHECK("scan");

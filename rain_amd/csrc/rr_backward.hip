@@ -104,33 +104,19 @@ template <int N>
 __device__ __forceinline__ void adam_batch(float* const (&pp)[N], float* const (&mp)[N], float* const (&vp)[N],
                                            const float (&g)[N], const AdamC (&c)[N]) {
     float p[N], m[N], v[N];
-#ifndef RR_GB_NT
-#define RR_GB_NT 0
-#endif
 #pragma unroll
     for (int i = 0; i < N; i++) {
         p[i] = *pp[i];
-        if (RR_GB_NT) {  // moments are read and written once per step: no reuse to keep in the caches
-            m[i] = __builtin_nontemporal_load(mp[i]);
-            v[i] = __builtin_nontemporal_load(vp[i]);
-        } else {
-            m[i] = *mp[i];
-            v[i] = *vp[i];
-        }
+        m[i] = *mp[i];
+        v[i] = *vp[i];
     }
 #pragma unroll
     for (int i = 0; i < N; i++) adam_elem(p[i], g[i], m[i], v[i], c[i]);
 #pragma unroll
     for (int i = 0; i < N; i++) {
-        if (RR_GB_NT) {
-            __builtin_nontemporal_store(p[i], pp[i]);
-            __builtin_nontemporal_store(m[i], mp[i]);
-            __builtin_nontemporal_store(v[i], vp[i]);
-        } else {
-            *pp[i] = p[i];
-            *mp[i] = m[i];
-            *vp[i] = v[i];
-        }
+        *pp[i] = p[i];
+        *mp[i] = m[i];
+        *vp[i] = v[i];
     }
 }
 
@@ -490,11 +476,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     __syncthreads();
     if (t < nvalid) {
         SmallGrads sg;
-#ifdef RR_GB_SKIP_COMPUTE  // timing probe only: memory phases without the per-Gaussian arithmetic
-        for (int i = 0; i < 11; i++) sg.v[i] = a.gacc[(size_t)(i0 + t) * GACC_STRIDE + i];
-#else
         gauss_bwd_one<DEG>(a, i0 + t, stage ? s_sh + t * kShStride : nullptr, sg);
-#endif
         if (a.use_adam) adam_small(a, i0 + t, sg);
     }
     __syncthreads();

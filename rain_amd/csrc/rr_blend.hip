@@ -329,6 +329,8 @@ int set_tuning(const char* key, int value) {
     else if (k == "sort_min_units") set_sort_min_units(value);
     else if (k == "sort_min_units_tile") set_sort_min_units_tile(value);
     else if (k == "sort_max_rounds") set_sort_max_rounds(value);
+    else if (k == "pair_scan_direct_blocks") set_pair_scan_direct_blocks(value);
+    else if (k == "wide_bin_keys") set_wide_bin_keys(value != 0);
     else return 1;
     return 0;
 }

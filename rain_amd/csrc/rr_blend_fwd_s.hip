@@ -5,11 +5,11 @@
 // packed v_pk_fma_f32 costs ~2x a plain v_fma_f32 on gfx950 and needs operand shuffles, so packing
 // buys nothing here):
 //   * every lane of a wave blends the same pair at the same time, so the pair's 48-B Splat is
-//     wave-uniform.  Default (RR_FWD_S_LDS): the workgroup stages a round of 64 NW records in LDS
-//     (one per thread, gathered by id) while the previous round blends, and the waves read them
-//     as LDS broadcasts — one exposed gather latency per tile: the records come from a 48 B x P
-//     array that no L2 holds, ~1-2 us away, and the scalar-load variants (s_load per group,
-//     RR_FWD_S_BATCH / RR_FWD_S_PIPE) wait that long every group of 2-4 pairs;
+//     wave-uniform.  The workgroup stages a round of 64 NW records in LDS (one per thread,
+//     gathered by id) while the previous round blends, and the waves read them as LDS
+//     broadcasts — one exposed gather latency per tile: the records come from a 48 B x P array
+//     that no L2 holds, ~1-2 us away (round 2 measured scalar loads per group of pairs, batched
+//     or software-pipelined, at 0.203-0.229 vs 0.176 ms/step for this staging);
 //   * alpha in log2 units from the pre-scaled conic (rr_common.hpp blend_e2): per pixel 3 fma-class
 //     ops and one exp2;
 //   * a lane owns PIX pixels of one column (rows l/16 + 4k): the x-terms of the falloff are
@@ -28,8 +28,6 @@ namespace rr {
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(4))) const v4f cv4f_s;
-typedef __attribute__((address_space(4))) const uint32_t cu32_s;
 typedef __attribute__((address_space(4))) const u2v cu2v_s;
 
 // NW waves per 16x16 tile, PIX = 4/NW pixels per lane: lane l of wave w owns column l%16 and rows
@@ -43,15 +41,6 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
     constexpr int PIX = 4 / NW;
 #ifndef RR_FWD_S_GROUP
 #define RR_FWD_S_GROUP 3
-#endif
-#ifndef RR_FWD_S_PIPE
-#define RR_FWD_S_PIPE 0
-#endif
-#ifndef RR_FWD_S_LDS
-#define RR_FWD_S_LDS 1  // measured: 0.176 vs 0.203 ms/step (scalar loads batched per group)
-#endif
-#ifndef RR_FWD_S_BATCH
-#define RR_FWD_S_BATCH 1  // measured: 0.208 vs 0.222 ms/step (G = 3 vs the unbatched G = 4)
 #endif
 #ifndef RR_FWD_TRACE
 #define RR_FWD_TRACE 0
@@ -116,9 +105,6 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     int walked = 0;
 #endif
-    cu32_s* plist = (cu32_s*)a.point_list + lo;  // readable kPointListPad entries past any list end
-    cv4f_s* recs = (cv4f_s*)a.splats;
-    cv4f_s* nrm = (cv4f_s*)a.normals;
 
     // One group of G pairs: their alphas first (independent of T), then the sequential blend.
     // ra/rb/rc/rn: the pairs' records as wave-uniform values (SGPR operands).
@@ -181,25 +167,6 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
         for (int k = 0; k < PIX; k++) any_open |= __builtin_amdgcn_ballot_w64(T[k] > 0.f);
         return any_open != 0;
     };
-    // The G ids of group j0 (entries past the list end, readable thanks to kPointListPad, are
-    // replaced by a valid id of the list: their records are loaded but never blended).
-    auto group_ids = [&](int j0, uint32_t (&id)[G], uint32_t fallback) {
-#pragma unroll
-        for (int u = 0; u < G; u++) id[u] = plist[j0 + u];
-#pragma unroll
-        for (int u = 0; u < G; u++) id[u] = (j0 + u < n) ? id[u] : fallback;
-    };
-    auto group_recs = [&](const uint32_t (&id)[G], v4f (&ra)[G], v4f (&rb)[G], v4f (&rc)[G], v4f (&rn)[G]) {
-#pragma unroll
-        for (int u = 0; u < G; u++) {
-            cv4f_s* r = recs + 3 * (size_t)id[u];  // one base, immediate offsets 0 / 16 / 32
-            ra[u] = r[0];  // x, y, conic.x, conic.y
-            rb[u] = r[1];  // conic.z, opacity, depth
-            rc[u] = r[2];  // r, g, b
-            if (AUX) rn[u] = nrm[id[u]];
-        }
-    };
-#if RR_FWD_S_LDS
     // Records staged through LDS a round of 64 NW pairs at a time, the next round's gathered into
     // registers while this one blends (one exposed load latency per tile instead of one per group:
     // the records are gathered from a 48-B x P array no L2 holds).  Reads are wave-uniform LDS
@@ -207,7 +174,6 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
     {
         constexpr int RND = 64 * NW;
         __shared__ v4f s_ra[RND], s_rb[RND], s_rc[RND], s_rn[AUX ? RND : 1];
-        const cv4f_s* rbase = recs;
         v4f pa = {}, pb = {}, pc = {}, pn = {};
         auto fetch = [&](int j) {
             if (j < n) {
@@ -219,7 +185,6 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
                 if (AUX) pn = ((const v4f*)a.normals)[id];
             }
         };
-        (void)rbase;
         fetch(t);
         for (int r0 = 0; r0 < n; r0 += RND) {
             bool mine = false;
@@ -254,75 +219,6 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
             }
         }
     }
-#elif RR_FWD_S_PIPE
-    // Software pipeline over groups: while group j blends, the records of group j+1 and the ids of
-    // group j+2 are in flight.  Scalar loads return out of order (the only wait is lgkmcnt(0)), so
-    // the wait sits at the top of the group and sched barriers keep the compiler from hoisting the
-    // next group's loads above it (which would make the wait cover them too).
-    if (n > 0) {
-        uint32_t idc[G], idn[G];
-        group_ids(0, idc, 0u);
-        const uint32_t id0 = plist[0];
-        v4f ra[G], rb[G], rc[G], rn[G];
-        group_recs(idc, ra, rb, rc, rn);
-        group_ids(G, idn, id0);
-        for (int j0 = 0; j0 < n; j0 += G) {
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this group's records, next ids
-            __builtin_amdgcn_sched_barrier(0);
-            if (!wave_open()) break;  // every pixel of this wave saturated
-            v4f na[G], nb[G], nc[G], nn[G];
-            uint32_t inn[G];
-            group_recs(idn, na, nb, nc, nn);
-            group_ids(j0 + 2 * G, inn, id0);
-            __builtin_amdgcn_sched_barrier(0);
-            blend_group(j0, n, ra, rb, rc, rn);
-#pragma unroll
-            for (int u = 0; u < G; u++) {
-                ra[u] = na[u];
-                rb[u] = nb[u];
-                rc[u] = nc[u];
-                rn[u] = nn[u];
-                idn[u] = inn[u];
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // no scalar load outstanding past the loop
-    }
-#elif RR_FWD_S_BATCH
-    // Per group one scalar-memory round trip: the group's records and the next group's ids are
-    // issued together (a sched barrier keeps the compiler from interleaving them with the blend,
-    // which would put an lgkmcnt(0) wait - covering every load in flight - before each record).
-    if (n > 0) {
-        const uint32_t id0 = plist[0];
-        uint32_t idc[G];
-        group_ids(0, idc, id0);
-        for (int j0 = 0; j0 < n; j0 += G) {
-            if (!wave_open()) break;  // every pixel of this wave saturated
-#if RR_FWD_TRACE
-            walked = j0 + G;
-#endif
-            v4f ra[G], rb[G], rc[G], rn[G];
-            uint32_t idn[G];
-            group_recs(idc, ra, rb, rc, rn);
-            group_ids(j0 + G, idn, id0);
-            __builtin_amdgcn_sched_barrier(0);
-            blend_group(j0, n, ra, rb, rc, rn);
-#pragma unroll
-            for (int u = 0; u < G; u++) idc[u] = idn[u];
-        }
-    }
-#else
-    for (int j0 = 0; j0 < n; j0 += G) {
-        if (!wave_open()) break;  // every pixel of this wave saturated
-#if RR_FWD_TRACE
-        walked = j0 + G;
-#endif
-        uint32_t id[G];
-        group_ids(j0, id, plist[j0]);
-        v4f ra[G], rb[G], rc[G], rn[G];
-        group_recs(id, ra, rb, rc, rn);
-        blend_group(j0, n, ra, rb, rc, rn);
-    }
-#endif
 #if RR_FWD_TRACE
     if (a.trace && lane == 0) {  // timing record of this wave (tools/fwd_trace.py)
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();

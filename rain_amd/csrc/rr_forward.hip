@@ -192,6 +192,61 @@ __global__ __launch_bounds__(256) void k_pair_scan_totals(const uint2* __restric
     if (threadIdx.x == 0) tot[blockIdx.x] = make_ulonglong2(x, y);
 }
 
+// Exclusive scan, in place, of the nb block totals (one workgroup, 2048 per round, carried in
+// 64 bits): the large-P path, where re-summing every earlier total in each block would grow with
+// nb^2 (at P = 16.7M that is ~0.5 GB of L2 reads per frame).
+__global__ __launch_bounds__(256) void k_pair_scan_prefix(ulonglong2* __restrict__ tot, int nb) {
+    constexpr int IPT = kPairScanItems / 256;
+    __shared__ unsigned long long s_wx[4], s_wy[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    unsigned long long cx = 0, cy = 0;  // sum of all earlier rounds
+    for (int base = 0; base < nb; base += kPairScanItems) {
+        ulonglong2 v[IPT];
+        unsigned long long tx = 0, ty = 0;
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const int i = base + t * IPT + k;
+            v[k] = i < nb ? tot[i] : make_ulonglong2(0ull, 0ull);
+            tx += v[k].x;
+            ty += v[k].y;
+        }
+        unsigned long long ix = tx, iy = ty;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long ux = __shfl_up(ix, o), uy = __shfl_up(iy, o);
+            if (lane >= o) {
+                ix += ux;
+                iy += uy;
+            }
+        }
+        __syncthreads();  // the previous round's reads of s_wx / s_wy are done
+        if (lane == 63) {
+            s_wx[w] = ix;
+            s_wy[w] = iy;
+        }
+        __syncthreads();
+        unsigned long long ex = cx + ix - tx, ey = cy + iy - ty;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < w) {
+                ex += s_wx[k];
+                ey += s_wy[k];
+            }
+#pragma unroll
+        for (int k = 0; k < IPT; k++) {
+            const int i = base + t * IPT + k;
+            if (i < nb) tot[i] = make_ulonglong2(ex, ey);
+            ex += v[k].x;
+            ey += v[k].y;
+        }
+        cx += s_wx[0] + s_wx[1] + s_wx[2] + s_wx[3];
+        cy += s_wy[0] + s_wy[1] + s_wy[2] + s_wy[3];
+    }
+}
+
+// PREFIX: tot[b] already holds the exclusive prefix of the block totals (k_pair_scan_prefix);
+// otherwise it holds block b's own total and every block sums those of the blocks before it.
+template <bool PREFIX>
 __global__ __launch_bounds__(256) void k_pair_scan(const uint2* __restrict__ in, uint2* __restrict__ out, int P,
                                                    const ulonglong2* __restrict__ tot) {
     constexpr int IPT = kPairScanItems / 256;  // 8 consecutive items per thread
@@ -215,12 +270,18 @@ __global__ __launch_bounds__(256) void k_pair_scan(const uint2* __restrict__ in,
     }
     // sum of the totals of all earlier blocks
     unsigned long long bx = 0, by = 0;
-    for (int j = t; j < (int)blockIdx.x; j += 256) {
-        const ulonglong2 q = tot[j];
-        bx += q.x;
-        by += q.y;
+    if (PREFIX) {
+        const ulonglong2 q = tot[blockIdx.x];
+        bx = q.x;
+        by = q.y;
+    } else {
+        for (int j = t; j < (int)blockIdx.x; j += 256) {
+            const ulonglong2 q = tot[j];
+            bx += q.x;
+            by += q.y;
+        }
+        block_sum2_u64(bx, by, s);
     }
-    block_sum2_u64(bx, by, s);
     // exclusive scan of the thread sums (wave shuffles, then the 4 wave totals)
     unsigned long long tx = 0, ty = 0;
 #pragma unroll
@@ -271,14 +332,22 @@ size_t pair_scan_temp_bytes(int P) {
     return (size_t)std::max((P + kPairScanItems - 1) / kPairScanItems, 1) * sizeof(ulonglong2);
 }
 
-bool launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_t st) {
+namespace {
+int g_pair_scan_direct = kPairScanDirectBlocks;
+}
+void set_pair_scan_direct_blocks(int nb) { g_pair_scan_direct = nb >= 0 ? nb : kPairScanDirectBlocks; }
+
+void launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_t st) {
+    if (P <= 0) return;
     const int nb = (P + kPairScanItems - 1) / kPairScanItems;
-    if (P <= 0) return true;
-    if (nb > kPairScanMaxBlocks) return false;
     ulonglong2* tot = static_cast<ulonglong2*>(temp);
     k_pair_scan_totals<<<nb, 256, 0, st>>>(in, P, tot);
-    k_pair_scan<<<nb, 256, 0, st>>>(in, out, P, tot);
-    return true;
+    if (nb <= g_pair_scan_direct) {
+        k_pair_scan<false><<<nb, 256, 0, st>>>(in, out, P, tot);
+    } else {
+        k_pair_scan_prefix<<<1, 256, 0, st>>>(tot, nb);
+        k_pair_scan<true><<<nb, 256, 0, st>>>(in, out, P, tot);
+    }
 }
 
 // First Gaussian (depth rank) of every window of `win` consecutive pairs starting at pair0:

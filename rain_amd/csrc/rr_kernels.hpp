@@ -170,13 +170,16 @@ struct GaussBwdArgs {
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);
 // Inclusive scan of the per-Gaussian {pairs, rect tiles} in depth order, saturating at 2^32 - 1
-// per component (rasterizer_impl.cu:269).  Two launches: per-block totals, then each block adds
-// the totals of the blocks before it to its own scan.  temp: pair_scan_temp_bytes(P); false when
-// P is too large for this scheme (the caller then uses a device-wide scan).
+// per component (rasterizer_impl.cu:269).  Per-block totals, then each block scans its items on
+// top of the sum of the earlier totals: up to kPairScanDirectBlocks blocks (P <= 1,048,576) every
+// block sums those totals itself (2 launches), above it one workgroup scans them first (3
+// launches; rr_set_tuning "pair_scan_direct_blocks" moves the cut-over, tests force both paths).
+// temp: pair_scan_temp_bytes(P).
 constexpr int kPairScanItems = 2048;                 // items per block (256 threads x 8)
-constexpr int kPairScanMaxBlocks = 8192;             // each block sums up to this many totals
+constexpr int kPairScanDirectBlocks = 512;
 size_t pair_scan_temp_bytes(int P);
-bool launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_t st);
+void launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_t st);
+void set_pair_scan_direct_blocks(int nb);
 template <typename K>
 struct DupArgs {
     int P;
@@ -254,6 +257,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
 const char* radix_sort_last_error();
 void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
 void set_sort_min_units_tile(int units);  // the same for the bin sorts (<= 16-bit keys; default 1024)
+void set_wide_bin_keys(bool on);     // tuning: 32-bit bin keys at any bin count (rr_api.hip)
 void set_sort_max_rounds(int r);     // rounds cap per wave (tuning; 0 = default 16)  // which check failed in the last radix_sort_pairs call
 // Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
 // can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass

@@ -319,8 +319,8 @@ struct SortLayout {
 constexpr int kMinUnitsDefault = 256;
 // Sorts of <= 16-bit keys (the bin sorts) target more, smaller units: their first pass's units are
 // the duplicate's windows, whose workgroups are latency-bound (interleaved A/B on the bench step:
-// duplicate 0.098 -> 0.092, bin sort 0.087 -> 0.077 ms/step with 1024; the depth sort keeps 512:
-// 0.109 vs 0.129 ms with 1024)
+// duplicate 0.098 -> 0.092, bin sort 0.087 -> 0.077 ms/step with 1024; the depth sort keeps
+// kMinUnitsDefault = 256: 0.109 vs 0.129 ms with 1024)
 constexpr int kMinUnitsTileDefault = 1024;
 int g_min_units = kMinUnitsDefault;
 int g_min_units_tile = kMinUnitsTileDefault;

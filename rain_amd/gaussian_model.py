@@ -5,6 +5,13 @@ densify/clone/split/prune semantics as scene/gaussian_model.py:13-421 (RAIN-GS f
 `abe_split`), with the device made explicit (the reference hard-codes "cuda") and one extra layout
 choice for the view-sharded multi-GPU step: every parameter's gradient is a view into ONE flat fp32
 buffer (`flat_grad`) so a single all-reduce covers all of them (rain_amd/train.py).
+
+Attribution: the optimizer-state surgery (replace_tensor_to_optimizer, _prune_optimizer,
+cat_tensors_to_optimizer, densification_postfix) and the torch densify/clone/split restatement
+follow the reference's scene/gaussian_model.py (Inria 3D Gaussian Splatting, GRAPHDECO research
+group, Inria Gaussian-Splatting licence — LICENSE.md in the reference; RAIN-GS modifications by its
+authors) closely, because train.py's loop depends on their exact behaviour.  The HIP densify path
+(rain_amd/csrc/densify.hip) is an independent design.
 """
 from __future__ import annotations
 

@@ -46,33 +46,53 @@ class TrainConfig:
     densify: bool = True
 
 
-class Exchange:
-    """The step's collectives over `group`, independent of the backend.
+def _serves_cuda_with_nccl(group) -> bool:
+    """True when the group's collectives on HIP tensors go through RCCL: backend "nccl", or a
+    mixed backend string that maps cuda to nccl (e.g. "cuda:nccl,cpu:gloo")."""
+    b = str(dist.get_backend(group)).lower()
+    if ":" not in b:
+        return b == "nccl"
+    return any(part.strip() == "cuda:nccl" for part in b.split(","))
 
-    RCCL (backend "nccl") runs them on the HIP tensors directly.  Other backends (gloo: the
-    multi-process CPU tests, and the 2-rank-on-one-GPU test) do not implement every collective for
-    device tensors, so the tensors are staged through host memory and the gradient reduce-scatter
-    becomes an all-reduce + local slice — the same sums (elementwise, rank order), so the step's
-    arithmetic does not depend on the backend."""
+
+class Exchange:
+    """The step's collectives over `group`.
+
+    RCCL (the group serves HIP tensors with "nccl") runs them on the device tensors directly, in
+    RCCL's own reduction order.  Otherwise (gloo: the multi-process CPU tests and the multi-rank
+    tests on one GPU) the tensors are staged through host memory and every SUM is formed by
+    gathering all ranks' contributions and adding them in rank order, ((x_0 + x_1) + x_2) + ...:
+    deterministic, independent of how the buffer is split into collectives (the chunked exchange
+    equals the serial one bitwise), and the order in which one process accumulating the same
+    views adds them.  The two backends can therefore differ in the last bits of a sum of more
+    than two terms."""
 
     def __init__(self, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.direct = dist.get_backend(group) == "nccl"
+        self.direct = _serves_cuda_with_nccl(group)
+
+    def _gather_host(self, t: torch.Tensor):
+        h = t.detach().to("cpu", copy=True).contiguous()
+        parts = [torch.empty_like(h) for _ in range(self.world)]
+        dist.all_gather(parts, h, group=self.group)
+        return parts
 
     def reduce_scatter_sum(self, out: torch.Tensor, inp: torch.Tensor):
         """out <- slice `rank` of the elementwise SUM over ranks of inp (inp.numel() = world * out.numel())."""
         if self.direct:
             dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group)
             return
-        h = inp.detach().to("cpu", copy=True)
-        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
         S = out.numel()
-        out.copy_(h[self.rank * S:(self.rank + 1) * S])
+        parts = self._gather_host(inp)
+        acc = parts[0][self.rank * S:(self.rank + 1) * S].clone()
+        for p in parts[1:]:
+            acc += p[self.rank * S:(self.rank + 1) * S]
+        out.copy_(acc)
 
     def all_gather_inplace(self, buf: torch.Tensor, lo: int, S: int):
-        """Every rank contributes buf[lo:lo+S] (lo = rank*S); afterwards buf holds all slices."""
+        """Every rank contributes buf[lo:lo+S] (lo = rank*S within buf); afterwards buf holds all slices."""
         if self.direct:
             dist.all_gather_into_tensor(buf, buf[lo:lo + S], group=self.group)
             return
@@ -81,12 +101,19 @@ class Exchange:
         buf.copy_(out)
 
     def all_reduce(self, t: torch.Tensor, op):
-        if self.direct or t.device.type == "cpu":
+        if self.direct:
             dist.all_reduce(t, op=op, group=self.group)
             return
-        h = t.to("cpu", copy=True)
-        dist.all_reduce(h, op=op, group=self.group)
-        t.copy_(h)
+        if op != dist.ReduceOp.SUM:  # MAX / MIN: order-free
+            h = t.to("cpu", copy=True)
+            dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+            return
+        parts = self._gather_host(t)
+        acc = parts[0].clone()
+        for p in parts[1:]:
+            acc += p
+        t.copy_(acc)
 
 
 class ViewSampler:
@@ -119,7 +146,7 @@ class StepInfo:
 class Trainer:
     def __init__(self, gaussians: GaussianModel, cameras, gt_images, opt: OptimizationParams | None = None,
                  pipe: PipelineParams | None = None, cfg: TrainConfig | None = None, scene_extent: float = 1.0,
-                 group=None, loss_fn=None, fused: bool | None = None):
+                 group=None, loss_fn=None, fused: bool | None = None, exchange: bool | None = None):
         self.g = gaussians
         self.cams = cameras
         self.gt = gt_images
@@ -130,9 +157,13 @@ class Trainer:
         self.group = group
         # loss_fn(image, gt, lambda_dssim) -> scalar; default: the fused HIP L1+SSIM kernels
         self.loss_fn = loss_fn or (lambda img, gt, lam: fused_l1_ssim_loss(img, gt, lam)[0])
-        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if dist_on else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
-        self.exchange = Exchange(group) if self.world > 1 else None
+        # the sharded exchange path runs whenever world > 1; exchange=True forces it at world 1
+        # too (a one-rank group: exercises the collectives, e.g. RCCL, on a single GPU)
+        self.sharded = self.world > 1 or (bool(exchange) and dist_on)
+        self.exchange = Exchange(group) if self.sharded else None
         self.sampler = ViewSampler(len(cameras), self.world, self.cfg.seed)
         dev = gaussians.device
         self.background = torch.tensor([1, 1, 1] if self.cfg.white_background else [0, 0, 0], dtype=torch.float32,
@@ -220,9 +251,9 @@ class Trainer:
         # Single GPU, and no densify/prune or opacity reset this iteration (they replace parameter
         # tensors before the reference's optimizer.step()): the Adam step runs inside the backward
         # kernel and the gradients never exist in HBM.
-        fuse_adam = (self.world == 1 and iteration < opt.iterations and not densify_now and not reset_now
+        fuse_adam = (not self.sharded and iteration < opt.iterations and not densify_now and not reset_now
                      and hasattr(g.optimizer, "fused_step"))
-        if self.world > 1:
+        if self.sharded:
             g.pack_flat_state(self.world)
         flat = None if fuse_adam else g.bind_flat_grad(zero=False, pad_to=self.world)  # backward overwrites all
         with torch.no_grad():
@@ -254,7 +285,7 @@ class Trainer:
         runs, all-reduce the gradients if an optimizer step follows (reset only: the reference
         steps every group but the replaced opacity), then the N = 1 logic on identical replicas."""
         g, opt = self.g, self.opt
-        if self.world == 1:
+        if not self.sharded:
             return self._densify_and_adam(iteration, adam_done=adam_done)
         fp, fm, fv, _offs, n = g.pack_flat_state(self.world)
         S = n // self.world
@@ -284,7 +315,7 @@ class Trainer:
         Ranks then hold the merged values, so call it only where they are consumed and reset
         (densify), or on copies."""
         g = self.g
-        if self.world > 1:
+        if self.sharded:
             self.exchange.all_reduce(g.xyz_gradient_accum, dist.ReduceOp.SUM)
             self.exchange.all_reduce(g.denom, dist.ReduceOp.SUM)
             self.exchange.all_reduce(g.max_radii2D, dist.ReduceOp.MAX)
@@ -293,7 +324,7 @@ class Trainer:
         """All-gather the Adam moments: on ordinary sharded iterations each rank advances only its
         1/N slice of exp_avg / exp_avg_sq, so call this before reading or checkpointing the full
         optimizer state (GaussianModel.capture, train.py:148-150).  Parameters are always full."""
-        if self.world > 1:
+        if self.sharded:
             _fp, fm, fv, _offs, n = self.g.pack_flat_state(self.world)
             S = n // self.world
             self.exchange.all_gather_inplace(fm, self.rank * S, S)
@@ -305,7 +336,7 @@ class Trainer:
         vidx, cam = self._low_pass_and_view(iteration)
         densify_phase = iteration < opt.densify_until_iter
         densify_now, reset_now = self._events(iteration)
-        if self.world > 1:
+        if self.sharded:
             g.pack_flat_state(self.world)
         flat = g.bind_flat_grad(pad_to=self.world)
 

@@ -262,3 +262,29 @@ def test_hip_cov3d_is_the_reference_sigma(gpu, tag, mod):
     assert a["num_rendered"] > 0
     assert rel_l1(a["color"], b["color"]) <= 1e-5
     assert rel_l1(a["grads"]["dL_dmeans3D"], b["grads"]["dL_dmeans3D"]) <= 1e-4
+
+
+@pytest.mark.parametrize("knob,value,reset", [("pair_scan_direct_blocks", 0, -1), ("wide_bin_keys", 1, 0)])
+@pytest.mark.parametrize("split", [1, 3])
+def test_forced_large_frame_paths(oracle, gpu, monkeypatch, knob, value, reset, split):
+    """Product paths the bench sizes do not reach, forced onto a small frame by their tuning knobs
+    (include/rain_raster.h rr_set_tuning): the 3-launch pair-count scan of P > 1,048,576 (block
+    totals scanned by one workgroup first), and the 32-bit bin keys of frames with more than
+    65536 bins of 32x32 px (above ~8K x 8K).  Single-phase and early-stop (split = 3) binning.
+    Images and gradients against the oracle, then the exact per-tile lists (culling, early stop off)."""
+    from rain_amd import _native as N
+
+    L = N.raster()
+    N.check(L.rr_set_tuning(knob.encode(), value), knob)
+    N.check(L.rr_set_binning_config(split, 1), "binning config")
+    try:
+        inp, st = make_scene(P=30000, W=400, H=300, sh_degree=3)
+        dpix = _dpix(st)
+        ref = oracle_run(oracle, inp, st, dL_dpix=dpix)
+        got = gpu_run(inp, st, gpu, dL_dpix=dpix)
+        _check_forward(ref, got)
+        _check_grads(ref, got)
+        _check_pair_order(oracle, gpu, monkeypatch, inp, st)
+    finally:
+        N.check(L.rr_set_tuning(knob.encode(), reset), knob)
+        N.check(L.rr_set_binning_config(0, 0), "binning config")
