@@ -271,7 +271,9 @@ def test_forced_large_frame_paths(oracle, gpu, monkeypatch, knob, value, reset, 
     (include/rain_raster.h rr_set_tuning): the 3-launch pair-count scan of P > 1,048,576 (block
     totals scanned by one workgroup first), and the 32-bit bin keys of frames with more than
     65536 bins of 32x32 px (above ~8K x 8K).  Single-phase and early-stop (split = 3) binning.
-    Images and gradients against the oracle, then the exact per-tile lists (culling, early stop off)."""
+    Images and gradients against the oracle; then the exact per-tile lists (culling, early stop off)
+    on the pair-order test's scene (at 30k Gaussians some depths are an ulp apart, and the oracle's
+    separately rounded view-z orders such a pair the other way)."""
     from rain_amd import _native as N
 
     L = N.raster()
@@ -284,6 +286,7 @@ def test_forced_large_frame_paths(oracle, gpu, monkeypatch, knob, value, reset, 
         got = gpu_run(inp, st, gpu, dL_dpix=dpix)
         _check_forward(ref, got)
         _check_grads(ref, got)
+        inp, st = make_scene(P=3000, W=128, H=96, sh_degree=3)
         _check_pair_order(oracle, gpu, monkeypatch, inp, st)
     finally:
         N.check(L.rr_set_tuning(knob.encode(), reset), knob)
