@@ -568,10 +568,20 @@ class GaussianModel:
         self.flat_grad = None
 
     def add_densification_stats(self, viewspace_point_tensor, update_filter):
-        """gaussian_model.py:419-421 (consumes the NDC-space dL/dmeans2D the rasterizer returns)."""
-        self.xyz_gradient_accum[update_filter] += torch.norm(viewspace_point_tensor.grad[update_filter, :2], dim=-1,
-                                                             keepdim=True)
-        self.denom[update_filter] += 1
+        """gaussian_model.py:419-421 (consumes the NDC-space dL/dmeans2D the rasterizer returns).
+        The reference's boolean-mask indexing makes the host wait for the device (the mask's count
+        sizes the gather); the same update as a select keeps the step free of host syncs: masked
+        rows gain exactly the reference's norm, the others exactly 0."""
+        m = update_filter.reshape(-1, 1)
+        g = viewspace_point_tensor.grad
+        self.xyz_gradient_accum += torch.where(m, torch.norm(g[:, :2], dim=-1, keepdim=True), 0.0)
+        self.denom += m.to(self.denom.dtype)
+
+    def update_max_radii(self, radii, visibility_filter):
+        """train.py:133, max_radii2D[vis] = max(max_radii2D[vis], radii[vis]), without the host sync of
+        boolean-mask indexing (the same values)."""
+        self.max_radii2D = torch.where(visibility_filter, torch.maximum(self.max_radii2D, radii.float()),
+                                       self.max_radii2D)
 
 
 def low_pass_schedule(H, W, N, c2f_max_lowpass=300.0):

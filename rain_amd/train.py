@@ -336,9 +336,13 @@ class Trainer:
         vidx, cam = self._low_pass_and_view(iteration)
         densify_phase = iteration < opt.densify_until_iter
         densify_now, reset_now = self._events(iteration)
-        if self.sharded:
+        if self.sharded:  # gradients accumulate into the flat buffer the exchange reduces
             g.pack_flat_state(self.world)
-        flat = g.bind_flat_grad(pad_to=self.world)
+            flat = g.bind_flat_grad(pad_to=self.world)
+        else:  # the reference's zero_grad(set_to_none=True): autograd allocates fresh gradients
+            flat = None
+            for p in g.params():
+                p.grad = None
 
         pkg = render(cam, g, self.pipe, self.background, low_pass=self.low_pass)
         image, vsp, vis, radii = pkg["render"], pkg["viewspace_points"], pkg["visibility_filter"], pkg["radii"]
@@ -349,7 +353,7 @@ class Trainer:
 
         with torch.no_grad():
             if densify_phase:  # train.py:132-134, per rank (merged by _finish when densify runs)
-                g.max_radii2D[vis] = torch.max(g.max_radii2D[vis], radii[vis].float())
+                g.update_max_radii(radii, vis)
                 g.add_densification_stats(vsp, vis)
             densified = self._finish(iteration, flat, densify_now, reset_now)
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],

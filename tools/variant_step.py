@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Per-stage kernel time and step time of the bench's training step for ONE build of
+librain_raster.so (RAIN_RASTER_LIB selects a variant from tools/build_variant.py), as one JSON
+line.  Run it once per variant in the same GPU call: same box, same clocks.
+
+    RAIN_RASTER_LIB=gpurun_variants/x.so python tools/variant_step.py --tag x
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default=os.environ.get("RAIN_RASTER_LIB", "default"))
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--points", type=int, default=1_000_000)
+    ap.add_argument("--api", action="store_true", help="also time the reference-API step (Trainer(fused=False))")
+    a = ap.parse_args()
+    import torch
+
+    from rain_amd import _native, synthetic
+    from rain_amd.cameras import fibonacci_cameras
+    from rain_amd.gaussian_model import GaussianModel, OptimizationParams
+    from rain_amd.renderer import PipelineParams, render
+    from rain_amd.train import TrainConfig, Trainer
+
+    dev = torch.device("cuda:0")
+    cams = [c.to(dev) for c in fibonacci_cameras(200, 1920, 1080)]
+    gm = GaussianModel(3, device=dev)
+    gm.set_params(synthetic.random_gaussians(a.points, sh_degree=3, seed=1, bench=True, device=dev))
+    gm.active_sh_degree = 3
+    with torch.no_grad():
+        gts = [render(c, gm, PipelineParams(), torch.zeros(3, device=dev))["render"].clamp(0, 1).contiguous()
+               for c in cams[:64]]
+    del gm
+    gts = gts * 4
+    g = GaussianModel(3, divide_ratio=0.8, device=dev)
+    g.set_params(synthetic.random_gaussians(a.points, sh_degree=3, seed=0, bench=True, device=dev))
+    g.active_sh_degree = 3
+    g.spatial_lr_scale = 4.4
+    opt = OptimizationParams()
+    g.training_setup(opt)
+    tr = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(seed=0), scene_extent=4.4)
+    it = 1001
+    for _ in range(10):
+        tr.step(it)
+        it += 1
+    _native.Profiler.collect()
+    with _native.Profiler():
+        for _ in range(20):
+            tr.step(it)
+            it += 1
+    br = _native.Profiler.collect()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.step(it)
+        it += 1
+    torch.cuda.synchronize()
+    ms = 1000.0 * (time.perf_counter() - t0) / a.steps
+    out = {"tag": a.tag, "ms_per_step": round(ms, 4),
+           "stages_ms": {k: round(v[0] / 20, 4) for k, v in br.items() if v[1]}}
+    if a.api:
+        tr2 = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(seed=1), scene_extent=4.4, fused=False)
+        import torch.optim
+
+        fused_opt = g.optimizer
+        groups = [{"params": q["params"], "lr": q["lr"], "name": q["name"]} for q in fused_opt.param_groups]
+        g.optimizer = torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+        it = 2001
+        for _ in range(5):
+            tr2.step(it)
+            it += 1
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            tr2.step(it)
+            it += 1
+        torch.cuda.synchronize()
+        out["api_ms_per_step"] = round(1000.0 * (time.perf_counter() - t0) / 20, 4)
+        g.optimizer = fused_opt
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
