@@ -73,7 +73,7 @@ MODELED = ("preprocess", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd"
 VALU_BOUND = ("blend_fwd", "blend_bwd")
 
 
-def algorithmic_bytes(stage, st, P, W, H, K):
+def algorithmic_bytes(stage, st, P, W, H, K, world=1):
     """SURVEY §8(d) algorithmic bytes per frame (one training step renders one frame).  Binning
     stages are priced on the (bin, Gaussian) pairs this implementation actually sorts (num_binned:
     bins of 2 x 2 tiles, after exact culling and early-stop binning), not on the reference's larger
@@ -91,8 +91,16 @@ def algorithmic_bytes(stage, st, P, W, H, K):
         "ranges": (kw + 4) * Lb + 8 * T,
         "blend_fwd": 8 * T + 44 * Le + 24 * N,
         "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
-        "gauss_bwd": gauss_bwd_bytes(P, V, K, M),
+        "gauss_bwd": gauss_bwd_bytes(P, V, K, M) if world == 1 else gauss_bwd_views_bytes(P, K, M, world),
     }.get(stage)
+
+
+def gauss_bwd_views_bytes(P, K, M, world):
+    """The Gaussian-sharded step's per-Gaussian backward on one rank (rain_amd/sharded.py): its
+    P/N rows' parameters and both moments read and written once (Adam), statistics read + written,
+    and one 40-B record per row and view."""
+    rows = (P + world - 1) // world
+    return rows * (24 * (11 + 3 * M) + 24) + 40 * rows * world
 
 
 def gauss_bwd_bytes(P, V, K, M, fused_adam=True):
@@ -223,6 +231,9 @@ def main():
         elapsed = float(e.item())
     iters_per_s = world * K / elapsed
     ms_per_step = 1000.0 * elapsed / K
+    # the Gaussian-sharded step keeps parameters current on their owner's rows only: gather full
+    # replicas for the measurement legs below (no-op at world 1)
+    trainer.sync_state()
     end_iter = it - 1
     n_densify = sum(1 for i in range(start_iter, end_iter + 1) if i % 100 == 0)
     densify_extra_ms = one_ms[D1] - one_ms[D1 - 1]
@@ -280,7 +291,7 @@ def main():
             # per step (= per frame): early-stop binning runs the binning stages in two phases
             kernels[name] = {"ms_per_step": ms / PW, "launches_per_step": cnt / PW, "total_ms": ms}
     if dom_timed and dom_timed[1]:
-        byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2)
+        byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2, world)
         dom_ms = dom_timed[0] / dom_timed[1]  # HIP events around every launch inside the timed loop
         gbs = byts / (dom_ms * 1e-3) / 1e9
         roofline = {"kernel": dom, "step_dominant": step_dom, "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -298,7 +309,7 @@ def main():
                     "valu_issue_frac": (_pmc_field(dom, "valu_issue_frac")
                                         if (P, W, H) == (1_000_000, 1920, 1080) else None)}
         for k in kernels:
-            b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2)
+            b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2, world)
             if b is not None:
                 kernels[k]["algorithmic_GBps"] = round(b / (kernels[k]["ms_per_step"] * 1e-3) / 1e9, 1)
         # north_star states its roofline target on the per-tile blend: both blends' HBM fractions
@@ -333,8 +344,8 @@ def main():
                                f"densify/prune every 100 it + Adam), {P} Gaussians, {W}x{H}, SH {D}, "
                                f"view-sharded dp{world}",
                    "gaussians": P, "width": W, "height": H, "sh_degree": D, "views": args.views,
-                   "parallelism": (f"dp{world} (view-sharded, RCCL reduce-scatter + all-gather)" if world > 1 else
-                                   "dp1 (RCCL exchange forced)" if force else "dp1"),
+                   "parallelism": (f"dp{world} (view-parallel, Gaussian-sharded: RCCL all-to-all of per-view "
+                                   f"records)" if world > 1 else "dp1 (RCCL exchange forced)" if force else "dp1"),
                    "iterations": [start_iter, end_iter], "densify_events_in_window": n_densify},
         "densify_iter_ms": round(one_ms[D1], 3),
         "ordinary_iter_ms_alone": round(one_ms[D1 - 1], 3),

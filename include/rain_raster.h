@@ -206,6 +206,69 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
                 int num_rendered, const float* dL_dpix, void* workspace, size_t workspace_bytes,
                 const rr_grads* out, void* stream);
 
+/*
+ * ---- Gaussian-sharded view-parallel training step (N ranks; no reference counterpart: the
+ * reference is single-GPU).  Rank r owns the Gaussian rows
+ * [r*Q, (r+1)*Q) (Q a multiple of 256, N*Q >= P) and renders one view per step; the bytes that
+ * cross xGMI per step are per-(Gaussian, view) records, not parameters or gradients:
+ *   1. owner:  rr_preprocess_rows for each of the step's N views over its rows -> that view's
+ *              splat records, pair counts, depth keys, radii, per-256-row block sums;
+ *   2. all-to-all: rank v receives view v's arrays of every row block, assembling them at
+ *              rr_geometry_layout's offsets of a P_pad = N*Q geometry buffer (+ radii [P_pad]);
+ *   3. rank v: rr_forward_from_geometry (depth sort, binning, blend: rr_forward minus the
+ *              preprocess), loss, rr_backward_records -> one 10-float record per Gaussian
+ *              (the blend backward's dmean2D.xy, dconic.xyz, dopacity, dcolor.rgb and the radius);
+ *   4. all-to-all: the owner receives its rows' records of all N views;
+ *   5. owner:  rr_gauss_backward_views: per Gaussian, the reference's per-view gradient
+ *              (cov2D / projection / SH / cov3D backward, raw-parameter chain) for each view in
+ *              order, summed per element in that order, scaled by grad_scale (1/N, rounded like
+ *              grad.mul_(1/N)), then Adam on the owner's rows and the densification statistics.
+ * The arithmetic of one step equals one process rendering the N views, summing their raw-parameter
+ * gradients in view order, dividing by N and stepping Adam (up to the blend backward's float-atomic
+ * order).  Parameters and moments are current only on their owner's rows between steps; callers
+ * all-gather them where a full replica is read (densification, checkpoints, evaluation).
+ */
+#define RR_MAX_VIEWS 16
+typedef struct rr_view {
+    const float* viewmatrix; /* [16] device, column-major world->view (as rr_camera) */
+    const float* projmatrix; /* [16] device, full projection */
+    const float* campos;     /* [3] device */
+    float tan_fovx, tan_fovy, low_pass;
+    int width, height;
+} rr_view;
+/* Byte offsets, inside a geometry buffer carved for P rows (rr_geometry_bytes(P)), of the arrays
+ * the preprocess writes: offsets[0] splat records (48 B each), [1] pair counts (uint2),
+ * [2] depth keys (u32), [3] per-256-row block sums (uint2), [4] per-block wide-key flags (u32). */
+int rr_geometry_layout(int P, size_t* offsets);
+/* Preprocess of one row block for one camera: frame.P valid rows (gaussians pointers offset to the
+ * block's first row), n_rows (a multiple of 256, >= P) rows written; rows P..n_rows-1 are culled
+ * padding.  Outputs are the caller's arrays of n_rows entries (block sums: n_rows/256). */
+int rr_preprocess_rows(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int n_rows, int* radii,
+                       void* splats, void* tiles, void* depth_keys, void* block_sums, void* block_wide, void* stream);
+/* rr_forward over a geometry buffer whose preprocess arrays are already filled (frame.P rows, a
+ * multiple of 256; radii [P]); same outputs, same RR_INCOMPLETE / binning_needed protocol, with
+ * rr_forward_render_geometry as the second stage. */
+int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
+                             size_t geom_bytes, void* image_buffer, size_t image_bytes, void* binning_buffer,
+                             size_t binning_bytes, int* num_rendered, int* num_pairs, size_t* binning_needed,
+                             float* out_color, float* out_depth, void* stream);
+int rr_forward_render_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
+                               void* image_buffer, void* binning_buffer, size_t binning_bytes, int num_pairs,
+                               float* out_color, float* out_depth, void* stream);
+/* Blend backward of a frame into records [P][10] (floats: dmean2D.xy, dconic.xyz, dopacity,
+ * dcolor.rgb, radius); workspace as rr_backward. */
+int rr_backward_records(const rr_frame* f, const rr_camera* cam, const int* radii, const void* geom_buffer,
+                        const void* image_buffer, const void* binning_buffer, int num_rendered, const float* dL_dpix,
+                        void* workspace, size_t workspace_bytes, float* records, void* stream);
+/* Per-Gaussian backward of a row block over num_views views (records [num_views][record_rows][10]),
+ * RR_FLAG_RAW_PARAMS only: frame.P rows, frame.D / M / scale_modifier; gaussians = raw parameters
+ * offset to the block.  out: no gradient arrays; optional densification statistics (offset to the
+ * block); optional Adam (param pointers = the matching inputs; a group whose param is NULL is not
+ * stepped, e.g. the replaced opacity of an opacity-reset iteration). */
+int rr_gauss_backward_views(const rr_frame* f, const rr_view* views, int num_views, const rr_gaussians* g,
+                            const float* records, int record_rows, float grad_scale, const rr_grads* out,
+                            void* stream);
+
 /* markVisible (rasterize_points.cu:193-212, rasterizer_impl.cu:43-55,130-142): present[P] as 0/1 bytes. */
 int rr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                     uint8_t* present, void* stream);

@@ -66,6 +66,15 @@ class RRGrads(ctypes.Structure):
                [("adam", ctypes.POINTER(RRAdam))]
 
 
+class RRView(ctypes.Structure):
+    _fields_ = [("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p), ("campos", ctypes.c_void_p),
+                ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float), ("low_pass", ctypes.c_float),
+                ("width", ctypes.c_int), ("height", ctypes.c_int)]
+
+
+RR_MAX_VIEWS = 16
+
+
 class RRFrameStats(ctypes.Structure):
     _fields_ = [("num_rendered", ctypes.c_int64), ("num_visible", ctypes.c_int64), ("l_eff", ctypes.c_int64),
                 ("tiles", ctypes.c_int64), ("num_pairs", ctypes.c_int64), ("num_binned", ctypes.c_int64)]
@@ -81,7 +90,9 @@ RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr
                   "rr_forward_geometry", "rr_forward_render", "rr_forward_render_aux", "rr_forward", "rr_backward", "rr_mark_visible", "rr_last_error",
                   "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
                   "rr_set_binning_config", "rr_set_tuning", "rr_debug_set_fwd_trace", "rr_profile_enable",
-                  "rr_profile_select", "rr_profile_collect", "rr_stage_name"]
+                  "rr_profile_select", "rr_profile_collect", "rr_stage_name", "rr_geometry_layout",
+                  "rr_preprocess_rows", "rr_forward_from_geometry", "rr_forward_render_geometry",
+                  "rr_backward_records", "rr_gauss_backward_views"]
 
 _raster = None
 _knn = None
@@ -144,6 +155,21 @@ def raster():
         L.rr_profile_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
         L.rr_stage_name.restype = ctypes.c_char_p
         L.rr_stage_name.argtypes = [ci]
+        # Gaussian-sharded step (rain_amd/sharded.py)
+        L.rr_geometry_layout.restype = ci
+        L.rr_geometry_layout.argtypes = [ci, ctypes.POINTER(sz)]
+        L.rr_preprocess_rows.restype = ci
+        L.rr_preprocess_rows.argtypes = [fp, cp, gp, ci, vp, vp, vp, vp, vp, vp, vp]
+        L.rr_forward_from_geometry.restype = ci
+        L.rr_forward_from_geometry.argtypes = [fp, cp, vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(ci), ctypes.POINTER(ci),
+                                               ctypes.POINTER(sz), vp, vp, vp]
+        L.rr_forward_render_geometry.restype = ci
+        L.rr_forward_render_geometry.argtypes = [fp, cp, vp, vp, vp, vp, sz, ci, vp, vp, vp]
+        L.rr_backward_records.restype = ci
+        L.rr_backward_records.argtypes = [fp, cp, vp, vp, vp, vp, ci, vp, vp, sz, vp, vp]
+        L.rr_gauss_backward_views.restype = ci
+        L.rr_gauss_backward_views.argtypes = [fp, ctypes.POINTER(RRView), ci, gp, vp, ci, ctypes.c_float,
+                                              ctypes.POINTER(RRGrads), vp]
         _raster = L
     return _raster
 

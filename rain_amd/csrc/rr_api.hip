@@ -397,60 +397,29 @@ int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, boo
     return RR_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-const char* rr_last_error(void) { return g_err.c_str(); }
-const char* rr_version(void) { return "rain_amd-raster 0.1 gfx950"; }
-
-size_t rr_geometry_bytes(int P) { return carve_geom(nullptr, P).total; }
-size_t rr_image_bytes(int width, int height) { return carve_img(nullptr, width, height).total; }
-size_t rr_binning_bytes(int num_rendered, int width, int height) {
-    return carve_bin(nullptr, num_rendered, width, height).total;
-}
-size_t rr_backward_workspace_bytes(int P) { return align_up((size_t)std::max(P, 1) * GACC_STRIDE * sizeof(float)); }
-
-int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii, void* geom_buffer,
-                        size_t geom_bytes, void* image_buffer, size_t image_bytes, int* num_rendered,
-                        int* num_pairs, void* stream) {
-    int rc = validate(f, cam, g, true);
-    if (rc) return rc;
-    if (!num_rendered || !num_pairs) return fail(RR_ERR_ARG, "num_rendered / num_pairs is null");
-    *num_rendered = 0;
-    *num_pairs = 0;
-    const int P = f->P, W = f->width, H = f->height;
-    if (P == 0) return RR_OK;
-    if (!radii || !geom_buffer || !image_buffer) return fail(RR_ERR_ARG, "null output buffer");
-    const Geom gm = carve_geom(geom_buffer, P);
-    const Img im = carve_img(image_buffer, W, H);
-    if (geom_bytes < gm.total || image_bytes < im.total) return fail(RR_ERR_CAPACITY, "scratch buffer too small");
-    hipStream_t st = (hipStream_t)stream;
-
+// Preprocess arguments of a frame (the output arrays are set by the caller).
+PreArgs pre_args(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g) {
     PreArgs a{};
-    a.P = P; a.D = f->D; a.M = f->M; a.W = W; a.H = H; a.gx = grid_x(W); a.gy = grid_y(H);
+    a.P = f->P; a.D = f->D; a.M = f->M; a.W = f->width; a.H = f->height;
+    a.gx = grid_x(f->width); a.gy = grid_y(f->height);
     a.prefiltered = f->prefiltered;
     a.tanfovx = f->tan_fovx; a.tanfovy = f->tan_fovy;
-    a.focal_y = H / (2.0f * f->tan_fovy);
-    a.focal_x = W / (2.0f * f->tan_fovx);
+    a.focal_y = f->height / (2.0f * f->tan_fovy);
+    a.focal_x = f->width / (2.0f * f->tan_fovx);
     a.scale_modifier = f->scale_modifier; a.low_pass = f->low_pass;
     a.means3D = g->means3D; a.shs = g->shs; a.colors_precomp = g->colors_precomp; a.opacities = g->opacities;
     a.scales = g->scales; a.rotations = g->rotations; a.cov3D_precomp = g->cov3D_precomp;
     a.view = cam->viewmatrix; a.proj = cam->projmatrix; a.campos = cam->campos;
-    a.radii = radii; a.splats = gm.splats; a.tiles = gm.tiles; a.depth_keys = gm.depth_keys;
     a.cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
     a.raw = (f->flags & RR_FLAG_RAW_PARAMS) ? 1 : 0;
     a.shs_rest = g->shs_rest;
-    a.normals = (f->flags & RR_FLAG_AUX_NORMAL) ? gm.normals : nullptr;
-    a.block_sums = gm.block_sums;
-    a.block_wide = gm.block_wide;
+    return a;
+}
 
+// Depth sort -> pair-count scan -> the one device->host read of the forward, over a geometry buffer
+// whose per-Gaussian arrays (splats, tiles, depth keys, block sums) are filled.
+int count_pairs(const rr_frame* f, const Geom& gm, int P, hipStream_t st, int* num_rendered, int* num_pairs) {
     PairCountRead rd;
-    {
-        StageTimer tm(RR_STAGE_PREPROCESS, st);
-        launch_preprocess(a, st);
-    }
-    RR_STAGE_CHECK("preprocess");
     const PublishJob pub = pair_counts_job(gm.block_sums, gm.block_wide, (P + 255) / 256, gm.totals, rd);
     // depth sort (rasterizer_impl.cu:295 sorts {tile, depth} keys; here the Gaussians by depth,
     // then the pairs stably by bin) and the scan of the pair counts in depth order
@@ -486,6 +455,48 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
     *num_rendered = (int)tot.y;
     *num_pairs = (int)tot.x;
     return RR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rr_last_error(void) { return g_err.c_str(); }
+const char* rr_version(void) { return "rain_amd-raster 0.1 gfx950"; }
+
+size_t rr_geometry_bytes(int P) { return carve_geom(nullptr, P).total; }
+size_t rr_image_bytes(int width, int height) { return carve_img(nullptr, width, height).total; }
+size_t rr_binning_bytes(int num_rendered, int width, int height) {
+    return carve_bin(nullptr, num_rendered, width, height).total;
+}
+size_t rr_backward_workspace_bytes(int P) { return align_up((size_t)std::max(P, 1) * GACC_STRIDE * sizeof(float)); }
+
+int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii, void* geom_buffer,
+                        size_t geom_bytes, void* image_buffer, size_t image_bytes, int* num_rendered,
+                        int* num_pairs, void* stream) {
+    int rc = validate(f, cam, g, true);
+    if (rc) return rc;
+    if (!num_rendered || !num_pairs) return fail(RR_ERR_ARG, "num_rendered / num_pairs is null");
+    *num_rendered = 0;
+    *num_pairs = 0;
+    const int P = f->P, W = f->width, H = f->height;
+    if (P == 0) return RR_OK;
+    if (!radii || !geom_buffer || !image_buffer) return fail(RR_ERR_ARG, "null output buffer");
+    const Geom gm = carve_geom(geom_buffer, P);
+    const Img im = carve_img(image_buffer, W, H);
+    if (geom_bytes < gm.total || image_bytes < im.total) return fail(RR_ERR_CAPACITY, "scratch buffer too small");
+    hipStream_t st = (hipStream_t)stream;
+    PreArgs a = pre_args(f, cam, g);
+    a.radii = radii; a.splats = gm.splats; a.tiles = gm.tiles; a.depth_keys = gm.depth_keys;
+    a.normals = (f->flags & RR_FLAG_AUX_NORMAL) ? gm.normals : nullptr;
+    a.block_sums = gm.block_sums;
+    a.block_wide = gm.block_wide;
+    {
+        StageTimer tm(RR_STAGE_PREPROCESS, st);
+        launch_preprocess(a, st);
+    }
+    RR_STAGE_CHECK("preprocess");
+    return count_pairs(f, gm, P, st, num_rendered, num_pairs);
 }
 
 }  // extern "C"
@@ -578,6 +589,43 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     return RR_OK;
 }
 
+int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
+                 void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
+                 float* out_normal, void* stream);
+
+// Accumulator clear (+ the backward's tile order) and the blend backward: gacc [P][GACC_STRIDE]
+// receives every Gaussian's dmean2D / dconic / dopacity / dcolor sums of the frame.
+int blend_backward(const rr_frame* f, const rr_camera* cam, const void* geom_buffer, const void* image_buffer,
+                   const void* binning_buffer, int L, const float* dL_dpix, float* gacc, hipStream_t st) {
+    const int P = f->P, W = f->width, H = f->height;
+    const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
+    const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
+    // point_list sits at the start of the binning buffer, so its position does not depend on the
+    // pair count; tiles whose forward blended nothing (tile_max 0) never read it
+    const Bin bn = carve_bin(const_cast<void*>(binning_buffer), 0, W, H);
+    const int gx = grid_x(W), gy = grid_y(H);
+    const bool blend = L > 0 && binning_buffer;
+    uint32_t* order = blend && bwd_tile_order() ? im.order : nullptr;
+    {
+        StageTimer tm(RR_STAGE_MEMSET, st);
+        launch_bwd_prologue(gacc, (size_t)P * GACC_STRIDE, gx * gy, im.tile_max, order, st);
+        RR_CHECK(hipGetLastError(), "clear accumulators");
+    }
+    if (blend) {
+        StageTimer tm(RR_STAGE_BLEND_BWD, st);
+        BlendBwdArgs b{};
+        b.W = W; b.H = H; b.gx = gx; b.gy = gy;
+        b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.point_list = bn.point_list; b.splats = gm.splats;
+        b.tile_max = im.tile_max;
+        b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.bg = cam->background; b.dL_dpix = dL_dpix;
+        b.gacc = gacc;
+        b.order = order;
+        launch_blend_bwd(b, st);
+    }
+    RR_STAGE_CHECK("blend backward");
+    return RR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -597,6 +645,18 @@ int rr_forward_render_aux(const rr_frame* f, const rr_camera* cam, const rr_gaus
     if (rc) return rc;
     if (((f->flags & RR_FLAG_AUX_NORMAL) != 0) != (out_normal != nullptr))
         return fail(RR_ERR_ARG, "out_normal must be given exactly when RR_FLAG_AUX_NORMAL is set");
+    return render_frame(f, cam, radii, geom_buffer, image_buffer, binning_buffer, binning_bytes, num_pairs, out_color,
+                        out_depth, out_normal, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+// Binning + blend of a frame whose geometry buffer holds the sorted, scanned per-Gaussian arrays.
+int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
+                 void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
+                 float* out_normal, void* stream) {
     const int P = f->P, W = f->width, H = f->height, L = num_pairs;
     const int cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
     if (P == 0) return RR_OK;
@@ -623,6 +683,10 @@ int rr_forward_render_aux(const rr_frame* f, const rr_camera* cam, const rr_gaus
     return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
                    : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
 }
+
+}  // namespace
+
+extern "C" {
 
 int rr_forward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii, void* geom_buffer,
                size_t geom_bytes, void* image_buffer, size_t image_bytes, void* binning_buffer, size_t binning_bytes,
@@ -671,33 +735,9 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
     if (out->grad_accum && (!raw || !out->denom || !out->max_radii2D))
         return fail(RR_ERR_ARG, "densification statistics need raw mode and grad_accum, denom, max_radii2D");
     if (workspace_bytes < rr_backward_workspace_bytes(P)) return fail(RR_ERR_CAPACITY, "workspace too small");
-    const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
-    const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
-    // point_list sits at the start of the binning buffer, so its position does not depend on the
-    // pair count; tiles whose forward blended nothing (tile_max 0) never read it
-    const Bin bn = carve_bin(const_cast<void*>(binning_buffer), 0, W, H);
     hipStream_t st = (hipStream_t)stream;
-    const int gx = grid_x(W), gy = grid_y(H);
     float* gacc = static_cast<float*>(workspace);
-    const bool blend = L > 0 && binning_buffer;
-    uint32_t* order = blend && bwd_tile_order() ? im.order : nullptr;
-    {
-        StageTimer tm(RR_STAGE_MEMSET, st);
-        launch_bwd_prologue(gacc, (size_t)P * GACC_STRIDE, gx * gy, im.tile_max, order, st);
-        RR_CHECK(hipGetLastError(), "clear accumulators");
-    }
-    if (blend) {
-        StageTimer tm(RR_STAGE_BLEND_BWD, st);
-        BlendBwdArgs b{};
-        b.W = W; b.H = H; b.gx = gx; b.gy = gy;
-        b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.point_list = bn.point_list; b.splats = gm.splats;
-        b.tile_max = im.tile_max;
-        b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.bg = cam->background; b.dL_dpix = dL_dpix;
-        b.gacc = gacc;
-        b.order = order;
-        launch_blend_bwd(b, st);
-    }
-    RR_STAGE_CHECK("blend backward");
+    if (int rc2 = blend_backward(f, cam, geom_buffer, image_buffer, binning_buffer, L, dL_dpix, gacc, st)) return rc2;
     {
         StageTimer tm(RR_STAGE_GAUSS_BWD, st);
         GaussBwdArgs a{};
@@ -721,6 +761,155 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
     }
     RR_STAGE_CHECK("gaussian backward");
     return RR_OK;
+}
+
+// ---- Gaussian-sharded multi-GPU step (include/rain_raster.h, "row blocks") ----
+
+int rr_geometry_layout(int P, size_t* offsets) {
+    if (P < 0 || !offsets) return fail(RR_ERR_ARG, "bad P / null offsets");
+    // carve over a stand-in base address (a null base carves null pointers) and subtract it
+    constexpr uintptr_t kBase = 1u << 20;
+    const Geom gm = carve_geom(reinterpret_cast<void*>(kBase), P);
+    auto off = [](const void* p) { return (size_t)(reinterpret_cast<uintptr_t>(p) - kBase); };
+    offsets[0] = off(gm.splats);
+    offsets[1] = off(gm.tiles);
+    offsets[2] = off(gm.depth_keys);
+    offsets[3] = off(gm.block_sums);
+    offsets[4] = off(gm.block_wide);
+    return RR_OK;
+}
+
+int rr_preprocess_rows(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int n_rows, int* radii,
+                       void* splats, void* tiles, void* depth_keys, void* block_sums, void* block_wide, void* stream) {
+    int rc = validate(f, cam, g, true);
+    if (rc) return rc;
+    if (n_rows < f->P || (n_rows % 256) != 0) return fail(RR_ERR_ARG, "n_rows must be >= P and a multiple of 256");
+    if (n_rows == 0) return RR_OK;
+    if (!radii || !splats || !tiles || !depth_keys || !block_sums || !block_wide)
+        return fail(RR_ERR_ARG, "null output array");
+    if (f->flags & RR_FLAG_AUX_NORMAL) return fail(RR_ERR_ARG, "row blocks carry no aux normals");
+    hipStream_t st = (hipStream_t)stream;
+    PreArgs a = pre_args(f, cam, g);
+    a.radii = radii;
+    a.splats = static_cast<Splat*>(splats);
+    a.tiles = static_cast<uint2*>(tiles);
+    a.depth_keys = static_cast<uint32_t*>(depth_keys);
+    a.block_sums = static_cast<uint2*>(block_sums);
+    a.block_wide = static_cast<uint32_t*>(block_wide);
+    a.n_out = n_rows;
+    {
+        StageTimer tm(RR_STAGE_PREPROCESS, st);
+        launch_preprocess(a, st);
+    }
+    RR_STAGE_CHECK("preprocess (rows)");
+    return RR_OK;
+}
+
+int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
+                             size_t geom_bytes, void* image_buffer, size_t image_bytes, void* binning_buffer,
+                             size_t binning_bytes, int* num_rendered, int* num_pairs, size_t* binning_needed,
+                             float* out_color, float* out_depth, void* stream) {
+    if (!f || !cam || !num_rendered || !num_pairs || !binning_needed) return fail(RR_ERR_ARG, "null argument");
+    *num_rendered = 0;
+    *num_pairs = 0;
+    *binning_needed = 0;
+    const int P = f->P, W = f->width, H = f->height;
+    if (P < 0 || W <= 0 || H <= 0 || (P % 256) != 0) return fail(RR_ERR_ARG, "P must be a multiple of 256");
+    if (f->flags & RR_FLAG_AUX_NORMAL) return fail(RR_ERR_ARG, "row blocks carry no aux normals");
+    if (P == 0) return RR_OK;
+    if (!radii || !geom_buffer || !image_buffer || !out_color || !out_depth || !cam->background)
+        return fail(RR_ERR_ARG, "null buffer");
+    const Geom gm = carve_geom(geom_buffer, P);
+    const Img im = carve_img(image_buffer, W, H);
+    if (geom_bytes < gm.total || image_bytes < im.total) return fail(RR_ERR_CAPACITY, "scratch buffer too small");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = count_pairs(f, gm, P, st, num_rendered, num_pairs)) return rc;
+    const size_t need = *num_pairs > 0 ? carve_bin(nullptr, *num_pairs, W, H).total : 0;
+    *binning_needed = need;
+    if (binning_bytes < need) return RR_INCOMPLETE;
+    return render_frame(f, cam, radii, geom_buffer, image_buffer, binning_buffer, binning_bytes, *num_pairs, out_color,
+                        out_depth, nullptr, stream);
+}
+
+int rr_forward_render_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
+                               void* image_buffer, void* binning_buffer, size_t binning_bytes, int num_pairs,
+                               float* out_color, float* out_depth, void* stream) {
+    if (!f || !cam || (f->flags & RR_FLAG_AUX_NORMAL)) return fail(RR_ERR_ARG, "bad frame / camera");
+    if (f->P == 0) return RR_OK;
+    if (!radii || !cam->background) return fail(RR_ERR_ARG, "null buffer");
+    return render_frame(f, cam, radii, geom_buffer, image_buffer, binning_buffer, binning_bytes, num_pairs, out_color,
+                        out_depth, nullptr, stream);
+}
+
+int rr_backward_records(const rr_frame* f, const rr_camera* cam, const int* radii, const void* geom_buffer,
+                        const void* image_buffer, const void* binning_buffer, int num_rendered, const float* dL_dpix,
+                        void* workspace, size_t workspace_bytes, float* records, void* stream) {
+    if (!f || !cam) return fail(RR_ERR_ARG, "null frame / camera");
+    const int P = f->P;
+    if (P < 0) return fail(RR_ERR_ARG, "bad P");
+    if (P == 0) return RR_OK;
+    if (!radii || !geom_buffer || !image_buffer || !dL_dpix || !workspace || !records || !cam->background)
+        return fail(RR_ERR_ARG, "null buffer");
+    if (workspace_bytes < rr_backward_workspace_bytes(P)) return fail(RR_ERR_CAPACITY, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    float* gacc = static_cast<float*>(workspace);
+    if (int rc = blend_backward(f, cam, geom_buffer, image_buffer, binning_buffer, num_rendered, dL_dpix, gacc, st))
+        return rc;
+    launch_pack_records(gacc, radii, P, records, st);
+    return check(f, st, "pack records");
+}
+
+int rr_gauss_backward_views(const rr_frame* f, const rr_view* views, int num_views, const rr_gaussians* g,
+                            const float* records, int record_rows, float grad_scale, const rr_grads* out,
+                            void* stream) {
+    if (!f || !views || !g || !out) return fail(RR_ERR_ARG, "null argument");
+    if (num_views < 1 || num_views > RR_MAX_VIEWS) return fail(RR_ERR_ARG, "1 <= num_views <= RR_MAX_VIEWS");
+    const int P = f->P;
+    if (P < 0 || record_rows < P) return fail(RR_ERR_ARG, "bad P / record_rows");
+    if (!(f->flags & RR_FLAG_RAW_PARAMS)) return fail(RR_ERR_ARG, "the sharded backward runs in raw-parameter mode");
+    if (f->M < 1 || f->M > 16 || f->D < 0 || f->D > 3 || f->M < (f->D + 1) * (f->D + 1))
+        return fail(RR_ERR_ARG, "sh_degree must be 0..3 and M >= (degree+1)^2, M <= 16");
+    if (P == 0) return RR_OK;
+    if (!records || !g->means3D || !g->shs || !g->opacities || !g->scales || !g->rotations || (f->M > 1 && !g->shs_rest))
+        return fail(RR_ERR_ARG, "raw parameters and records are required");
+    if (out->dL_dmeans2D || out->dL_dcolors || out->dL_dopacity || out->dL_dmeans3D || out->dL_dcov3D || out->dL_dsh ||
+        out->dL_dscales || out->dL_drotations || out->dL_dsh_rest)
+        return fail(RR_ERR_ARG, "the sharded backward writes no gradient arrays (Adam and statistics only)");
+    if (out->grad_accum && (!out->denom || !out->max_radii2D))
+        return fail(RR_ERR_ARG, "densification statistics need grad_accum, denom, max_radii2D");
+    const rr_adam* ad = out->adam;
+    if (ad) {
+        const rr_adam_group* gs[6] = {&ad->xyz, &ad->f_dc, &ad->f_rest, &ad->opacity, &ad->scaling, &ad->rotation};
+        const void* in[6] = {g->means3D, g->shs, g->shs_rest, g->opacities, g->scales, g->rotations};
+        for (int i = 0; i < 6; i++) {
+            if (!gs[i]->param || (i == 2 && f->M <= 1)) continue;  // a group without param is not stepped
+            if (!gs[i]->exp_avg || !gs[i]->exp_avg_sq) return fail(RR_ERR_ARG, "null Adam moment array");
+            if (gs[i]->param != in[i]) return fail(RR_ERR_ARG, "Adam group param must be the matching input array");
+        }
+    }
+    ViewCam cams[RR_MAX_VIEWS];
+    for (int v = 0; v < num_views; v++) {
+        const rr_view& w = views[v];
+        if (!w.viewmatrix || !w.projmatrix || !w.campos || w.width <= 0 || w.height <= 0)
+            return fail(RR_ERR_ARG, "bad view");
+        cams[v] = ViewCam{w.viewmatrix, w.projmatrix, w.campos, w.tan_fovx, w.tan_fovy,
+                          w.width / (2.0f * w.tan_fovx), w.height / (2.0f * w.tan_fovy), w.low_pass};
+    }
+    hipStream_t st = (hipStream_t)stream;
+    GaussBwdArgs a{};
+    a.P = P; a.D = f->D; a.M = f->M;
+    a.scale_modifier = f->scale_modifier;
+    a.means3D = g->means3D; a.shs = g->shs; a.scales = g->scales; a.rotations = g->rotations;
+    a.raw = 1; a.opacities = g->opacities; a.shs_rest = g->shs_rest;
+    a.grad_accum = out->grad_accum; a.denom = out->denom; a.max_radii2D = out->max_radii2D;
+    a.use_adam = ad ? 1 : 0;
+    if (ad) a.adam = *ad;
+    {
+        StageTimer tm(RR_STAGE_GAUSS_BWD, st);
+        if (launch_gauss_bwd_views(a, cams, num_views, records, record_rows, grad_scale, st))
+            return fail(RR_ERR_ARG, "bad number of views");
+    }
+    return check(f, st, "gaussian backward (views)");
 }
 
 int rr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,

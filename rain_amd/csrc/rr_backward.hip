@@ -55,12 +55,19 @@ __device__ __forceinline__ v3 sh_dir_grad(v3 dir, const float* rest, v3 dL_dRGB)
 }
 
 template <int DEG>
-__device__ __forceinline__ void sh_coeff_grads(v3 dir, v3 dL_dRGB, float* row, int M) {
+__device__ __forceinline__ void sh_coeff_grads(v3 dir, v3 dL_dRGB, float* row, int M, bool acc) {
     const float x = dir.x, y = dir.y, z = dir.z;
     auto W = [&](int k, float s) {
-        row[3 * k + 0] = s * dL_dRGB.x;
-        row[3 * k + 1] = s * dL_dRGB.y;
-        row[3 * k + 2] = s * dL_dRGB.z;
+        const float g0 = s * dL_dRGB.x, g1 = s * dL_dRGB.y, g2 = s * dL_dRGB.z;
+        if (acc) {  // the multi-view kernel: add this view's gradient (rounded on its own first)
+            row[3 * k + 0] += g0;
+            row[3 * k + 1] += g1;
+            row[3 * k + 2] += g2;
+        } else {
+            row[3 * k + 0] = g0;
+            row[3 * k + 1] = g1;
+            row[3 * k + 2] = g2;
+        }
     };
     W(0, RR_SH_C0);
     if (DEG > 0) {
@@ -86,7 +93,8 @@ __device__ __forceinline__ void sh_coeff_grads(v3 dir, v3 dL_dRGB, float* row, i
         }
     }
     constexpr int K = (DEG + 1) * (DEG + 1);
-    for (int i = 3 * K; i < 3 * M; i++) row[i] = 0.f;
+    if (!acc)
+        for (int i = 3 * K; i < 3 * M; i++) row[i] = 0.f;
 }
 
 // The 11 per-Gaussian gradients of the small groups (xyz 3, opacity 1, scaling 3, rotation 4),
@@ -148,23 +156,50 @@ __device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const
         cc[7 + i] = c_rot;
         e[7 + i] = 4 * (size_t)idx + i;
     }
-    float* pp[11];
-    float* mp[11];
-    float* vp[11];
+    if (ad.xyz.param && ad.scaling.param && ad.opacity.param && ad.rotation.param) {  // the usual case
+        float* pp[11];
+        float* mp[11];
+        float* vp[11];
+#pragma unroll
+        for (int i = 0; i < 11; i++) {
+            pp[i] = gr[i]->param + e[i];
+            mp[i] = gr[i]->exp_avg + e[i];
+            vp[i] = gr[i]->exp_avg_sq + e[i];
+        }
+        adam_batch<11>(pp, mp, vp, sg.v, cc);
+        return;
+    }
+    // a group without param is not stepped (the sharded step of an opacity-reset iteration)
 #pragma unroll
     for (int i = 0; i < 11; i++) {
-        pp[i] = gr[i]->param + e[i];
-        mp[i] = gr[i]->exp_avg + e[i];
-        vp[i] = gr[i]->exp_avg_sq + e[i];
+        if (!gr[i]->param) continue;
+        float p = gr[i]->param[e[i]], m = gr[i]->exp_avg[e[i]], v = gr[i]->exp_avg_sq[e[i]];
+        adam_elem(p, sg.v[i], m, v, cc[i]);
+        gr[i]->param[e[i]] = p;
+        gr[i]->exp_avg[e[i]] = m;
+        gr[i]->exp_avg_sq[e[i]] = v;
     }
-    adam_batch<11>(pp, mp, vp, sg.v, cc);
 }
 
-// One Gaussian.  `row` is this thread's LDS row holding its SH coefficients (staged by the
-// kernel; coefficient k at row[3k..3k+2]) and receiving its SH gradients in the same layout; it is
-// nullptr when there are neither SH inputs nor SH gradients.
-template <int DEG>
-__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, float* row, SmallGrads& sg) {
+// What the per-Gaussian backward needs of one view: its camera, and the Gaussian's accumulators
+// from that view's blend backward (GACC layout: dmean2D.xy, dconic.xyz, dopacity, dcolor.rgb) with
+// its radius.
+struct GaccRec {
+    const float* gp;  // GACC_STRIDE floats (single view) or a packed kRecFloats record (read when radius > 0)
+    int radius;
+};
+__device__ __forceinline__ ViewCam view_cam(const GaussBwdArgs& a) {
+    return ViewCam{a.view, a.proj, a.campos, a.tanfovx, a.tanfovy, a.focal_x, a.focal_y, a.low_pass};
+}
+
+// One Gaussian, one view.  `coef` is this thread's LDS row holding its SH coefficients (staged by
+// the kernel; coefficient k at coef[3k..3k+2]); the SH gradients go to `gsh` in the same layout,
+// stored (acc_sh false) or added (acc_sh true: the multi-view kernel sums the views in order).
+// coef == gsh (the single-view kernel) is allowed: every coefficient is read before the first
+// gradient is written.  Both are nullptr when there are neither SH inputs nor SH gradients.
+template <int DEG, bool PACKED>
+__device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, const ViewCam& c, int idx, const GaccRec& rec,
+                                              const float* coef, float* gsh, bool acc_sh, SmallGrads& sg) {
     const int M = a.M;
     float* dmean2 = a.dL_dmeans2D ? a.dL_dmeans2D + 3 * (size_t)idx : nullptr;
     float* dcol = a.dL_dcolors ? a.dL_dcolors + 3 * (size_t)idx : nullptr;
@@ -193,7 +228,7 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         put(a.dL_dopacity, idx, g);
     };
 
-    const int radius = a.radii[idx];
+    const int radius = rec.radius;
     if (!(radius > 0)) {  // untouched Gaussians: exact zeros (backward.cu:146,357)
         if (dmean2) dmean2[0] = dmean2[1] = dmean2[2] = 0.f;
         if (dcol) dcol[0] = dcol[1] = dcol[2] = 0.f;
@@ -202,17 +237,26 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         if (dcov)
 #pragma unroll
             for (int i = 0; i < 6; i++) dcov[i] = 0.f;
-        if (row)
-            for (int i = 0; i < 3 * M; i++) row[i] = 0.f;
+        if (gsh && !acc_sh)
+            for (int i = 0; i < 3 * M; i++) gsh[i] = 0.f;
         emit3(a.dL_dscales, 4, mk(0.f, 0.f, 0.f));
         emit_rot(make_float4(0.f, 0.f, 0.f, 0.f));
         return;
     }
 
-    const float* gp = a.gacc + (size_t)idx * GACC_STRIDE;
-    const float4 ga = *reinterpret_cast<const float4*>(gp);
-    const float4 gb = *reinterpret_cast<const float4*>(gp + 4);
-    const float g8 = gp[8];
+    float4 ga, gb;
+    float g8;
+    if (PACKED) {  // 40-B record, 8-B aligned
+        const float2* q = reinterpret_cast<const float2*>(rec.gp);
+        const float2 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+        ga = make_float4(q0.x, q0.y, q1.x, q1.y);
+        gb = make_float4(q2.x, q2.y, q3.x, q3.y);
+        g8 = q4.x;
+    } else {
+        ga = *reinterpret_cast<const float4*>(rec.gp);
+        gb = *reinterpret_cast<const float4*>(rec.gp + 4);
+        g8 = rec.gp[8];
+    }
     const float dm2x = ga.x, dm2y = ga.y;
     const float dcx = ga.z, dcy = ga.w, dcz = gb.x;
     if (dmean2) {
@@ -256,13 +300,13 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
     }
 
     // ---- computeCov2DCUDA (backward.cu:154-263) ----
-    const Proj2D pr = ewa_setup(mean, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view);
+    const Proj2D pr = ewa_setup(mean, c.focal_x, c.focal_y, c.tanfovx, c.tanfovy, c.view);
     const float x_grad_mul = pr.txtz < -pr.limx || pr.txtz > pr.limx ? 0.f : 1.f;
     const float y_grad_mul = pr.tytz < -pr.limy || pr.tytz > pr.limy ? 0.f : 1.f;
     float ca, cb, cc;
     ewa_cov2d(pr, cov, ca, cb, cc);
-    ca += a.low_pass;
-    cc += a.low_pass;
+    ca += c.low_pass;
+    cc += c.low_pass;
     const float denom = ca * cc - cb * cb;
     float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
@@ -298,21 +342,21 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
                           (T[0][0] * V[1][0] + T[0][1] * V[1][1] + T[0][2] * V[1][2]) * dL_db;
     const float dL_dT12 = 2 * (T[1][0] * V[2][0] + T[1][1] * V[2][1] + T[1][2] * V[2][2]) * dL_dc +
                           (T[0][0] * V[2][0] + T[0][1] * V[2][1] + T[0][2] * V[2][2]) * dL_db;
-    const float* vm = a.view;  // glm W[i][j] == vm[4j+i]
+    const float* vm = c.view;  // glm W[i][j] == vm[4j+i]
     const float dL_dJ00 = vm[0] * dL_dT00 + vm[4] * dL_dT01 + vm[8] * dL_dT02;
     const float dL_dJ02 = vm[2] * dL_dT00 + vm[6] * dL_dT01 + vm[10] * dL_dT02;
     const float dL_dJ11 = vm[1] * dL_dT10 + vm[5] * dL_dT11 + vm[9] * dL_dT12;
     const float dL_dJ12 = vm[2] * dL_dT10 + vm[6] * dL_dT11 + vm[10] * dL_dT12;
     const v3 t = pr.t;
     const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
-    const float dL_dtx = x_grad_mul * -a.focal_x * tz2 * dL_dJ02;
-    const float dL_dty = y_grad_mul * -a.focal_y * tz2 * dL_dJ12;
-    const float dL_dtz = -a.focal_x * tz2 * dL_dJ00 - a.focal_y * tz2 * dL_dJ11 +
-                         (2 * a.focal_x * t.x) * tz3 * dL_dJ02 + (2 * a.focal_y * t.y) * tz3 * dL_dJ12;
-    v3 dmean = xform_vec_4x3_T(mk(dL_dtx, dL_dty, dL_dtz), a.view);
+    const float dL_dtx = x_grad_mul * -c.focal_x * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -c.focal_y * tz2 * dL_dJ12;
+    const float dL_dtz = -c.focal_x * tz2 * dL_dJ00 - c.focal_y * tz2 * dL_dJ11 +
+                         (2 * c.focal_x * t.x) * tz3 * dL_dJ02 + (2 * c.focal_y * t.y) * tz3 * dL_dJ12;
+    v3 dmean = xform_vec_4x3_T(mk(dL_dtx, dL_dty, dL_dtz), c.view);
 
     // ---- preprocessCUDA bwd: mean2D -> mean3D (backward.cu:360-377) ----
-    const float* pj = a.proj;
+    const float* pj = c.proj;
     const float4 m_hom = xform_point_4x4(mean, pj);
     const float m_w = 1.0f / (m_hom.w + 0.0000001f);
     const float mul1 = (pj[0] * mean.x + pj[4] * mean.y + pj[8] * mean.z + pj[12]) * m_w * m_w;
@@ -323,9 +367,9 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 
     // ---- SH bwd (backward.cu:9-128); the clamp mask is recomputed from the forward SH value ----
     if (a.shs) {
-        const float* dc = row;  // staged coefficients (same values as shs / f_dc + f_rest)
-        const float* rest = row + 3;
-        const v3 cp = load3(a.campos);
+        const float* dc = coef;  // staged coefficients (same values as shs / f_dc + f_rest)
+        const float* rest = coef + 3;
+        const v3 cp = load3(c.campos);
         const v3 dir_orig = mean - cp;
         const float len = sqrtf(dot(dir_orig, dir_orig));
         const v3 dir = mk(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
@@ -335,7 +379,7 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         dL_dRGB.y *= rgb.y < 0 ? 0.f : 1.f;
         dL_dRGB.z *= rgb.z < 0 ? 0.f : 1.f;
         const v3 dL_ddir = sh_dir_grad<DEG>(dir, rest, dL_dRGB);  // last read of the staged coefficients
-        sh_coeff_grads<DEG>(dir, dL_dRGB, row, M);                // overwrite them with dL/dsh
+        sh_coeff_grads<DEG>(dir, dL_dRGB, gsh, M, acc_sh);        // (may overwrite them with dL/dsh)
         // dnormvdv (auxiliary.h:96-106)
         const v3 v = dir_orig;
         const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
@@ -343,8 +387,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
         dmean.x += ((+sum2 - v.x * v.x) * dL_ddir.x - v.y * v.x * dL_ddir.y - v.z * v.x * dL_ddir.z) * invsum32;
         dmean.y += (-v.x * v.y * dL_ddir.x + (sum2 - v.y * v.y) * dL_ddir.y - v.z * v.y * dL_ddir.z) * invsum32;
         dmean.z += (-v.x * v.z * dL_ddir.x - v.y * v.z * dL_ddir.y + (sum2 - v.z * v.z) * dL_ddir.z) * invsum32;
-    } else if (row) {
-        for (int i = 0; i < 3 * M; i++) row[i] = 0.f;
+    } else if (gsh && !acc_sh) {
+        for (int i = 0; i < 3 * M; i++) gsh[i] = 0.f;
     }
     emit3(a.dL_dmeans3D, 0, dmean);
 
@@ -413,9 +457,44 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, int idx, fl
 constexpr int kGB = RR_GB_THREADS;
 constexpr int kShStride = 49;
 
+// The per-Gaussian backward of one workgroup of kGB Gaussians.  Single view (MULTI false): the
+// gradients of this view, written out and / or stepped by the fused Adam; s_gr == s_sh.
+// MULTI (k_gauss_bwd_views, the Gaussian-sharded multi-GPU step): every view of va->cams in
+// order, each from its packed accumulator record, summed per element in view order into registers
+// (11 small-group values) and into s_gr (the SH gradients; s_sh keeps the coefficients), then
+// scaled by va->grad_scale (1/N, rounded like grad.mul_(1/N)) before the Adam step.
+struct GaussBwdViewsArgs;
+template <int DEG, bool MULTI>
+__device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const GaussBwdViewsArgs* va, float* s_sh,
+                                                float* s_gr);
+
 template <int DEG>
 __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     __shared__ float s_sh[kGB * kShStride];
+    gauss_bwd_block<DEG, false>(a, nullptr, s_sh, s_sh);
+}
+
+constexpr int kMaxViews = 16;
+constexpr int kRecFloats = 10;  // packed accumulator record: GACC slots 0..8, radius (as a float)
+struct GaussBwdViewsArgs {
+    GaussBwdArgs g;  // the row block: P rows, raw parameters / Adam / statistics offset to it
+    ViewCam cams[kMaxViews];
+    int V;
+    const float* records;  // [V][rec_rows][kRecFloats]
+    int rec_rows;
+    float grad_scale;
+};
+
+template <int DEG>
+__global__ __launch_bounds__(kGB) void k_gauss_bwd_views(GaussBwdViewsArgs va) {
+    __shared__ float s_sh[kGB * kShStride];
+    __shared__ float s_gr[kGB * kShStride];
+    gauss_bwd_block<DEG, true>(va.g, &va, s_sh, s_gr);
+}
+
+template <int DEG, bool MULTI>
+__device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const GaussBwdViewsArgs* va, float* s_sh,
+                                                float* s_gr) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int i0 = blockIdx.x * kGB;
     const int nvalid = min(kGB, a.P - i0);
@@ -476,7 +555,24 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     __syncthreads();
     if (t < nvalid) {
         SmallGrads sg;
-        gauss_bwd_one<DEG>(a, i0 + t, stage ? s_sh + t * kShStride : nullptr, sg);
+        const int idx = i0 + t;
+        float* row = stage ? s_sh + t * kShStride : nullptr;
+        if (!MULTI) {
+            const GaccRec rec{a.gacc + (size_t)idx * GACC_STRIDE, a.radii[idx]};
+            gauss_bwd_one<DEG, false>(a, view_cam(a), idx, rec, row, row, false, sg);
+        } else {
+            float* grow = stage ? s_gr + t * kShStride : nullptr;
+            for (int v = 0; v < va->V; v++) {
+                const float* rp = va->records + ((size_t)v * va->rec_rows + idx) * kRecFloats;
+                const GaccRec rec{rp, (int)rp[9]};
+                SmallGrads gv;
+                gauss_bwd_one<DEG, true>(a, va->cams[v], idx, rec, row, grow, v > 0, gv);
+#pragma unroll
+                for (int i = 0; i < 11; i++) sg.v[i] = v > 0 ? sg.v[i] + gv.v[i] : gv.v[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 11; i++) sg.v[i] = mul_rounded(sg.v[i], va->grad_scale);
+        }
         if (a.use_adam) adam_small(a, i0 + t, sg);
     }
     __syncthreads();
@@ -495,7 +591,8 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
             constexpr int kB = RR_GB_ADAM_BATCH;  // Adam elements per batch of loads
             auto grad_at = [&](int e) {
                 const int j = (int)(((float)e + 0.5f) * inv);
-                return s_sh[j * kShStride + koff + (e - j * w)];
+                const float g = s_gr[j * kShStride + koff + (e - j * w)];
+                return MULTI ? mul_rounded(g, va->grad_scale) : g;
             };
             const size_t gb = (size_t)i0 * w;
             const uintptr_t al = (grp ? ((uintptr_t)(grp->param + gb) | (uintptr_t)(grp->exp_avg + gb) |
@@ -559,8 +656,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
                     const int e = e0 + q * kGB;
                     const bool ok = e < total;
                     const int ee = ok ? e : e0;  // e0 < total: a valid dummy for the unused lanes of the batch
-                    const int j = (int)(((float)ee + 0.5f) * inv);
-                    g[q] = s_sh[j * kShStride + koff + (ee - j * w)];
+                    g[q] = grad_at(ee);
                     const size_t ge = (size_t)i0 * w + ee;
                     if (ok) put(dst, ge, g[q]);
                     n += ok;
@@ -594,6 +690,54 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
             if (nf > 3) stage_out(a.dL_dsh_rest, ad ? &ad->f_rest : nullptr, nf - 3, 3);
         }
     }
+}
+
+int launch_gauss_bwd_views(const GaussBwdArgs& a, const ViewCam* cams, int V, const float* records, int rec_rows,
+                           float grad_scale, hipStream_t st) {
+    if (V < 1 || V > kMaxViews) return 1;
+    if (a.P == 0) return 0;
+    GaussBwdViewsArgs va{};
+    va.g = a;
+    for (int v = 0; v < V; v++) va.cams[v] = cams[v];
+    va.V = V;
+    va.records = records;
+    va.rec_rows = rec_rows;
+    va.grad_scale = grad_scale;
+    const int nb = (a.P + kGB - 1) / kGB;
+    switch (a.shs ? a.D : 0) {
+        case 0: k_gauss_bwd_views<0><<<nb, kGB, 0, st>>>(va); break;
+        case 1: k_gauss_bwd_views<1><<<nb, kGB, 0, st>>>(va); break;
+        case 2: k_gauss_bwd_views<2><<<nb, kGB, 0, st>>>(va); break;
+        default: k_gauss_bwd_views<3><<<nb, kGB, 0, st>>>(va); break;
+    }
+    return 0;
+}
+
+// Packed per-(Gaussian, view) record for the sharded step: accumulator slots 0..8 and the radius.
+__global__ __launch_bounds__(256) void k_pack_records(const float* __restrict__ gacc, const int* __restrict__ radii,
+                                                      int P, float* __restrict__ rec) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    const int r = radii[i];
+    float v[kRecFloats];
+    if (r > 0) {
+        const float4 a = reinterpret_cast<const float4*>(gacc + (size_t)i * GACC_STRIDE)[0];
+        const float4 b = reinterpret_cast<const float4*>(gacc + (size_t)i * GACC_STRIDE)[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        v[8] = gacc[(size_t)i * GACC_STRIDE + 8];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; k++) v[k] = 0.f;
+    }
+    v[9] = (float)r;
+    float2* o = reinterpret_cast<float2*>(rec + (size_t)i * kRecFloats);
+#pragma unroll
+    for (int k = 0; k < kRecFloats / 2; k++) o[k] = make_float2(v[2 * k], v[2 * k + 1]);
+}
+
+void launch_pack_records(const float* gacc, const int* radii, int P, float* rec, hipStream_t st) {
+    if (P > 0) k_pack_records<<<(P + 255) / 256, 256, 0, st>>>(gacc, radii, P, rec);
 }
 
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st) {

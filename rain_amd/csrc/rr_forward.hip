@@ -129,7 +129,14 @@ template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     bool wide = false;
-    const uint2 c = idx < a.P ? preprocess_one<DEG>(a, idx, wide) : make_uint2(0u, 0u);
+    uint2 c = make_uint2(0u, 0u);
+    if (idx < a.P) {
+        c = preprocess_one<DEG>(a, idx, wide);
+    } else if (idx < a.n_out) {  // padding row of a row block: culled
+        a.radii[idx] = 0;
+        a.tiles[idx] = make_uint2(0u, 0u);
+        a.depth_keys[idx] = 0xffffffffu;
+    }
     if (!a.block_sums) return;
     __shared__ uint2 s_sum[4];
     __shared__ uint32_t s_wide[4];
@@ -704,8 +711,9 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 static inline int blocks_for(long n, int b = 256) { return (int)((n + b - 1) / b); }
 
 void launch_preprocess(const PreArgs& a, hipStream_t st) {
-    if (a.P == 0) return;
-    const int nb = blocks_for(a.P);
+    const int rows = a.n_out > a.P ? a.n_out : a.P;
+    if (rows == 0) return;
+    const int nb = blocks_for(rows);
     // (staging the SH coefficients through LDS was measured slower: 1.68 vs 1.66 ms per step)
     switch (a.colors_precomp ? 0 : a.D) {
         case 0: k_preprocess<0><<<nb, 256, 0, st>>>(a); break;

@@ -79,6 +79,8 @@ struct PreArgs {
     float4* normals;             // RR_FLAG_AUX_NORMAL: view-space unit normal per visible Gaussian, else null
     uint2* block_sums;           // optional [ceil(P/256)]: per-block sums of tiles[] (pairs, rect tiles)
     uint32_t* block_wide;        // with block_sums: per block, 1 if a visible depth key needs > kDepthKeyBits
+    int n_out;                   // rows written (>= P): rows P..n_out-1 get the culled outputs (radius 0,
+                                 // no pairs, the largest depth key) — the padding rows of a row block
 };
 
 // Depth keys: the float bits of the view depth minus those of the smallest float above the near
@@ -269,6 +271,18 @@ struct RadixPlan {
 template <typename K>
 RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
+// The Gaussian-sharded multi-GPU step (rr_gauss_backward_views): one view's camera as the
+// per-Gaussian backward reads it.
+struct ViewCam {
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float tanfovx, tanfovy, focal_x, focal_y, low_pass;
+};
+// rows a.P of a row block, V <= 16 views (records [V][rec_rows][10]); returns 1 on a bad V
+int launch_gauss_bwd_views(const GaussBwdArgs& a, const ViewCam* cams, int V, const float* records, int rec_rows,
+                           float grad_scale, hipStream_t st);
+void launch_pack_records(const float* gacc, const int* radii, int P, float* rec, hipStream_t st);
 
 }  // namespace rr
 

@@ -34,16 +34,20 @@ class FusedAdam(torch.optim.Optimizer):
         raise KeyError("parameter is not managed by this optimizer")
 
     @torch.no_grad()
-    def fused_step(self, model):
+    def fused_step(self, model, skip=()):
         """Book-keeping of one Adam step over the six GaussianModel groups done by the backward
         kernel itself (include/rain_raster.h rr_adam): advances each parameter's step count exactly
-        as step() would and returns the rr_adam block (lrs, bias corrections, moment buffers)."""
+        as step() would and returns the rr_adam block (lrs, bias corrections, moment buffers).
+        Groups named in `skip` are not stepped: their step count stays and their rr_adam entry is
+        left empty (param NULL), as torch's step() leaves a parameter whose .grad is None."""
         names = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
         params = (model._xyz, model._features_dc, model._features_rest, model._opacity, model._scaling,
                   model._rotation)
         ad = N.RRAdam()
         betas = None
         for name, p in zip(names, params):
+            if name in skip:
+                continue
             group = self._param_group(p)
             b1, b2 = group["betas"]
             if betas is None:

@@ -1,0 +1,211 @@
+"""Gaussian-sharded, view-parallel training step for N ranks (include/rain_raster.h "row blocks").
+
+The reference trains on one GPU, one view per iteration (train.py:87-147).  With N ranks one step
+renders N views (rank v renders view v of the shared permutation, rain_amd.train.ViewSampler) and
+applies ONE Adam step to the mean of their gradients — the SURVEY §8(e) contract.  The replicated
+design (every rank holds every parameter, reduce-scatter the 236 MB of gradients, all-gather the
+236 MB of parameters) moves ~2x(N-1)/N x 236 B per Gaussian over xGMI each step.  Here the bytes that
+cross the links are per-(Gaussian, view) records instead:
+
+  rank r owns the Gaussian rows [r*Q, (r+1)*Q) (Q: ceil(P/N) rounded up to 256):
+  1. owner preprocess: for each of the step's N views, its rows' splat records (48 B), pair
+     counts, depth keys, radii and per-256-row block sums (rr_preprocess_rows), ~64 B per row;
+  2. all-to-all (RCCL over xGMI, every pair of GPUs on its own link): rank v receives view v's
+     arrays of every block straight into its geometry buffer (rr_geometry_layout);
+  3. rank v renders view v from that geometry (rr_forward_from_geometry: depth sort, binning,
+     blend), computes the L1+SSIM loss and its gradient, and runs the blend backward into one
+     40-B record per Gaussian (rr_backward_records);
+  4. all-to-all: the owner receives its rows' records of all N views;
+  5. owner: the per-Gaussian backward of every view in view order, summed, x 1/N, Adam on its rows,
+     densification statistics (rr_gauss_backward_views).
+So ~2 x (N-1)/N x 104 B per Gaussian per step cross xGMI (all-to-all: each GPU's share leaves on
+its seven direct links at once), the per-Gaussian backward and Adam of a rank cover 1/N of the
+rows, and no collective carries parameters or gradients.  The sum over views is formed per element
+in view order, like one process accumulating the same N views: the step's arithmetic is that of
+the single-GPU step on N views (tests/test_multirank_gpu.py).
+
+Parameters, Adam moments and statistics are current on their owner's rows only;
+`sync_replicas` all-gathers the row blocks where a full replica is read: densify / prune, opacity
+reset, checkpoints, evaluation, the end of training.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import _native as N
+
+REC_FLOATS = 10
+SPLAT_BYTES = 48
+
+
+def _p(t, byte_offset=0):
+    return None if t is None or t.numel() == 0 else ctypes.c_void_p(t.data_ptr() + byte_offset)
+
+
+def row_blocks(P: int, world: int):
+    """(Q, P_pad): rows per rank (a multiple of 256) and the padded row count N*Q."""
+    Q = max(256, int(math.ceil(P / float(world) / 256.0)) * 256)
+    return Q, world * Q
+
+
+class ShardedStep:
+    """One rank's side of the Gaussian-sharded step (see the module docstring)."""
+
+    def __init__(self, exchange, rank: int, world: int):
+        self.ex = exchange
+        self.rank, self.world = rank, world
+        self._bufs = {}
+
+    def _buf(self, key, numel, dtype, dev):
+        t = self._bufs.get(key)
+        if t is None or t.numel() != numel or t.dtype != dtype or t.device != dev:
+            t = self._bufs[key] = torch.empty((numel,), dtype=dtype, device=dev)
+        return t
+
+    def layout(self, P):
+        Q, P_pad = row_blocks(P, self.world)
+        lo = self.rank * Q
+        return Q, P_pad, lo, max(0, min(Q, P - lo))
+
+    # ---- parameters of the owned rows --------------------------------------------------------
+    @staticmethod
+    def _row_params(model, lo):
+        M = 1 + model._features_rest.shape[1]
+        xyz, f_dc, f_rest = model._xyz, model._features_dc, model._features_rest
+        op, sc, rot = model._opacity, model._scaling, model._rotation
+        return N.RRGaussians(_p(xyz, 12 * lo), _p(f_dc, 12 * lo), None, _p(op, 4 * lo), _p(sc, 12 * lo),
+                             _p(rot, 16 * lo), None, _p(f_rest, 12 * (M - 1) * lo) if M > 1 else None), M
+
+    def _frame(self, model, P, cam, low_pass, flags):
+        D = model.active_sh_degree
+        M = 1 + model._features_rest.shape[1]
+        return N.RRFrame(int(P), D, M, int(cam.image_width), int(cam.image_height), math.tan(cam.FoVx * 0.5),
+                         math.tan(cam.FoVy * 0.5), 1.0, float(low_pass), 0, 0, flags)
+
+    def step(self, model, cams, bg, low_pass, flags, loss_fn, adam, stats):
+        """One step of this rank: `cams` = the step's N cameras (rank order); `loss_fn(image, v)`
+        -> dL/dimage for view v (this rank's); `adam` = rr_adam block (FusedAdam.fused_step) or None;
+        `stats` = (grad_accum, denom, max_radii2D) or None.  Returns (image, loss tensor or None)."""
+        L = N.raster()
+        dev = model._xyz.device
+        P = model._xyz.shape[0]
+        Nw = self.world
+        Q, P_pad, lo, nv = self.layout(P)
+        stream = N.stream_of(model._xyz)
+        u8 = torch.uint8
+
+        # 1. owner preprocess of every view over the owned rows -> send buffers [N][Q]
+        gs, M = self._row_params(model, lo)
+        nb = Q // 256
+        s_spl = self._buf("s_spl", Nw * Q * SPLAT_BYTES, u8, dev)
+        s_til = self._buf("s_til", Nw * Q * 8, u8, dev)
+        s_key = self._buf("s_key", Nw * Q * 4, u8, dev)
+        s_rad = self._buf("s_rad", Nw * Q * 4, u8, dev)
+        s_bsm = self._buf("s_bsm", Nw * nb * 8, u8, dev)
+        s_bwd = self._buf("s_bwd", Nw * nb * 4, u8, dev)
+        keep = []
+        for v, cam in enumerate(cams):
+            fr = self._frame(model, nv, cam, low_pass, flags | N.RR_FLAG_RAW_PARAMS)
+            k = (bg.contiguous(), cam.world_view_transform.contiguous(), cam.full_proj_transform.contiguous(),
+                 cam.camera_center.contiguous())
+            keep.append(k)
+            rc = N.RRCamera(*[_p(t) for t in k])
+            N.check(L.rr_preprocess_rows(ctypes.byref(fr), ctypes.byref(rc), ctypes.byref(gs), Q,
+                                         _p(s_rad, 4 * v * Q), _p(s_spl, SPLAT_BYTES * v * Q), _p(s_til, 8 * v * Q),
+                                         _p(s_key, 4 * v * Q), _p(s_bsm, 8 * v * nb), _p(s_bwd, 4 * v * nb), stream),
+                    "sharded preprocess")
+
+        # 2. all-to-all into this rank's geometry buffer (rows in global order)
+        geom = self._buf("geom", int(L.rr_geometry_bytes(P_pad)), u8, dev)
+        offs = (ctypes.c_size_t * 5)()
+        N.check(L.rr_geometry_layout(P_pad, offs), "geometry layout")
+        radii = self._buf("radii", P_pad, torch.int32, dev)
+        for send, off, nbytes in ((s_spl, offs[0], P_pad * SPLAT_BYTES), (s_til, offs[1], P_pad * 8),
+                                  (s_key, offs[2], P_pad * 4), (s_bsm, offs[3], (P_pad // 256) * 8),
+                                  (s_bwd, offs[4], (P_pad // 256) * 4)):
+            self.ex.all_to_all(geom[off:off + nbytes], send)
+        self.ex.all_to_all(radii.view(u8), s_rad)
+
+        # 3. render this rank's view from the geometry, loss, blend backward -> records
+        cam = cams[self.rank]
+        fr = self._frame(model, P_pad, cam, low_pass, flags)
+        k = keep[self.rank]
+        rc = N.RRCamera(*[_p(t) for t in k])
+        H, W = int(cam.image_height), int(cam.image_width)
+        img = torch.empty((int(L.rr_image_bytes(W, H)),), dtype=u8, device=dev)
+        color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+        depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
+        binning = self._bufs.get("binning")
+        if binning is None or binning.device != dev:
+            binning = torch.empty((0,), dtype=u8, device=dev)
+        nr, npairs, need = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_size_t(0)
+        r = L.rr_forward_from_geometry(ctypes.byref(fr), ctypes.byref(rc), _p(radii), _p(geom), geom.numel(), _p(img),
+                                       img.numel(), _p(binning), binning.numel(), ctypes.byref(nr),
+                                       ctypes.byref(npairs), ctypes.byref(need), _p(color), _p(depth), stream)
+        if r == N.RR_INCOMPLETE:
+            binning = self._bufs["binning"] = torch.empty((int(need.value * 1.25) + 4096,), dtype=u8, device=dev)
+            r = L.rr_forward_render_geometry(ctypes.byref(fr), ctypes.byref(rc), _p(radii), _p(geom), _p(img),
+                                             _p(binning), binning.numel(), npairs.value, _p(color), _p(depth), stream)
+        N.check(r, "sharded forward")
+        self.last = dict(num_rendered=nr.value, num_pairs=npairs.value, P_pad=P_pad, Q=Q)
+        dimg, loss = loss_fn(color)
+        dimg = dimg.contiguous()
+        ws = self._buf("ws", int(L.rr_backward_workspace_bytes(P_pad)), u8, dev)
+        recs = self._buf("recs", P_pad * REC_FLOATS, torch.float32, dev)
+        N.check(L.rr_backward_records(ctypes.byref(fr), ctypes.byref(rc), _p(radii), _p(geom), _p(img), _p(binning),
+                                      nr.value, _p(dimg), _p(ws), ws.numel(), _p(recs), stream), "sharded backward")
+
+        # 4. all-to-all of the records: chunk v of recv = view v's records of the owned rows
+        recv = self._buf("recv", Nw * Q * REC_FLOATS, torch.float32, dev)
+        self.ex.all_to_all(recv, recs)
+
+        # 5. owner: per-Gaussian backward of all views, summed in view order, x 1/N, Adam, statistics
+        if nv > 0:
+            views = (N.RRView * Nw)()
+            for v, c in enumerate(cams):
+                kv = keep[v]
+                views[v] = N.RRView(_p(kv[1]), _p(kv[2]), _p(kv[3]), math.tan(c.FoVx * 0.5), math.tan(c.FoVy * 0.5),
+                                    float(low_pass), int(c.image_width), int(c.image_height))
+            frb = self._frame(model, nv, cams[0], low_pass, N.RR_FLAG_RAW_PARAMS)
+            acc, den, mr = stats if stats is not None else (None, None, None)
+            ad = _offset_adam(adam, model, lo) if adam is not None else None
+            out = N.RRGrads(None, None, None, None, None, None, None, None, None, _p(acc, 4 * lo), _p(den, 4 * lo),
+                            _p(mr, 4 * lo), ctypes.pointer(ad) if ad is not None else None)
+            N.check(L.rr_gauss_backward_views(ctypes.byref(frb), views, Nw, ctypes.byref(gs), _p(recv), Q,
+                                              1.0 / Nw, ctypes.byref(out), stream), "sharded gaussian backward")
+        return color, loss
+
+    # ---- replicas ------------------------------------------------------------------------------
+    def sync_replicas(self, model):
+        """All-gather every row block of the parameters, Adam moments and densification statistics,
+        so that every rank holds the full, current state."""
+        P = model._xyz.shape[0]
+        Q, _P_pad, lo, _nv = self.layout(P)
+        ts = list(model.params())
+        for p in model.params():
+            st = model.optimizer.state.get(p)
+            if st and "exp_avg" in st:
+                ts += [st["exp_avg"], st["exp_avg_sq"]]
+        ts += [model.xyz_gradient_accum, model.denom, model.max_radii2D]
+        for t in ts:
+            self.ex.all_gather_rows(t.data if isinstance(t, torch.nn.Parameter) else t, Q, lo)
+
+
+def _offset_adam(ad, model, lo):
+    """rr_adam of FusedAdam.fused_step with every group's arrays moved to row `lo`."""
+    out = N.RRAdam()
+    out.beta1, out.beta2, out.eps = ad.beta1, ad.beta2, ad.eps
+    widths = dict(xyz=3, f_dc=3, f_rest=3 * model._features_rest.shape[1], opacity=1, scaling=3, rotation=4)
+    for name, w in widths.items():
+        src = getattr(ad, name)
+        dst = getattr(out, name)
+        if src.param:
+            d = 4 * w * lo
+            dst.param, dst.exp_avg, dst.exp_avg_sq = src.param + d, src.exp_avg + d, src.exp_avg_sq + d
+            dst.lr, dst.bias_correction1, dst.bias_correction2_sqrt = src.lr, src.bias_correction1, \
+                src.bias_correction2_sqrt
+    return out

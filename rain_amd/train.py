@@ -100,6 +100,33 @@ class Exchange:
         dist.all_gather_into_tensor(out, buf[lo:lo + S].to("cpu", copy=True), group=self.group)
         buf.copy_(out)
 
+    def all_to_all(self, recv: torch.Tensor, send: torch.Tensor):
+        """Chunk j of `send` (N equal chunks) goes to rank j; chunk i of `recv` comes from rank i."""
+        if self.direct:
+            dist.all_to_all_single(recv, send, group=self.group)
+            return
+        h = send.detach().to("cpu", copy=True).contiguous()
+        out = torch.empty_like(h)
+        dist.all_to_all_single(out, h, group=self.group)
+        recv.copy_(out)
+
+    def all_gather_rows(self, t: torch.Tensor, Q: int, lo: int):
+        """Rank r contributes rows [r*Q, r*Q + Q) of t (rows past t's end as padding); afterwards
+        every rank's t holds every rank's rows."""
+        P = t.shape[0]
+        flat = t.view(P, -1)
+        n = max(0, min(Q, P - lo))
+        send = torch.zeros((Q, flat.shape[1]), dtype=t.dtype, device=t.device)
+        if n:
+            send[:n].copy_(flat[lo:lo + n])
+        if self.direct:
+            out = torch.empty((self.world * Q, flat.shape[1]), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, send, group=self.group)
+        else:
+            out = torch.empty((self.world * Q, flat.shape[1]), dtype=t.dtype)
+            dist.all_gather_into_tensor(out, send.cpu(), group=self.group)
+        flat.copy_(out[:P])
+
     def all_reduce(self, t: torch.Tensor, op):
         if self.direct:
             dist.all_reduce(t, op=op, group=self.group)
@@ -181,6 +208,13 @@ class Trainer:
         self._bin_cache = None
         self.reuse_binning = True  # fused step: one native forward call over a reused binning buffer
         self._shard = None
+        # the fused step on N > 1 ranks (or a forced exchange): Gaussian-sharded, view-parallel
+        # (rain_amd/sharded.py); the autograd step keeps the replicated gradient exchange
+        self._owner = None
+        if self.sharded and self.fused:
+            from .sharded import ShardedStep
+
+            self._owner = ShardedStep(self.exchange, self.rank, self.world)
         if self.fused and not (dev.type == "cuda" and loss_fn is None and plain_pipe):
             raise ValueError("fused step needs a HIP device, the default loss and the default pipeline")
 
@@ -193,6 +227,7 @@ class Trainer:
         elif iteration % 1000 == 0:
             g.oneupSHdegree()
         views = self.sampler.next_group()
+        self._views = views
         vidx = views[self.rank]
         cam = self.cams[vidx]
         if cfg.c2f:
@@ -238,9 +273,58 @@ class Trainer:
             return self._step_fused(iteration, sync_loss)
         return self._step_autograd(iteration, sync_loss)
 
+    def _step_owner(self, iteration: int, sync_loss: bool) -> StepInfo:
+        """The fused step on the Gaussian-sharded ranks (rain_amd/sharded.py): one view per rank, Adam
+        of the owned rows inside the per-Gaussian backward.  Densify / prune and opacity reset
+        (train.py:136-143) gather full replicas first and run identically on every rank; on a
+        densify iteration the reference's optimizer.step() finds only replaced parameters (no step),
+        on a reset-only iteration it steps every group but the replaced opacity."""
+        from .diff_gaussian_rasterization import _C
+        from .loss import l1_ssim_backward, l1_ssim_forward
+
+        g, opt = self.g, self.opt
+        vidx, _cam = self._low_pass_and_view(iteration)
+        cams = [self.cams[v] for v in self._views]
+        densify_phase = iteration < opt.densify_until_iter
+        densify_now, reset_now = self._events(iteration)
+        adam = None
+        if iteration < opt.iterations and not densify_now:
+            adam = g.optimizer.fused_step(g, skip=("opacity",) if reset_now else ())
+        stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D) if densify_phase else None
+        gt = self.gt[vidx]
+        lam = opt.lambda_dssim
+
+        def loss_fn(image):
+            loss, _parts, lws = l1_ssim_forward(image, gt, lam)
+            return l1_ssim_backward(image, gt, lam, lws), loss
+
+        with torch.no_grad():
+            _image, loss = self._owner.step(g, cams, self.background, self.low_pass, _C.frame_flags(), loss_fn, adam,
+                                            stats)
+            densified = False
+            if densify_now or reset_now:
+                self._owner.sync_replicas(g)
+                densified = self._densify_and_adam(iteration, adam_done=True)
+        return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
+                        view=vidx, low_pass=self.low_pass, densified=densified)
+
+    def sync_state(self):
+        """Make every rank's GaussianModel a full, current replica (parameters, Adam moments,
+        densification statistics), e.g. before a checkpoint, an evaluation render or the end of
+        training.  Gaussian-sharded fused step: all-gather the row blocks.  Replicated (autograd)
+        step: merge the statistics (SUM / MAX: consumes them, like densify) and gather the moments."""
+        if self._owner is not None:
+            self._owner.sync_replicas(self.g)
+        elif self.sharded:
+            self.sync_densify_stats()
+            self.sync_optimizer_state()
+
     def _step_fused(self, iteration: int, sync_loss: bool) -> StepInfo:
         from . import fused
         from .loss import l1_ssim_backward, l1_ssim_forward
+
+        if self._owner is not None:
+            return self._step_owner(iteration, sync_loss)
 
         if self._bin_cache is None:
             self._bin_cache = fused.BinningCache()

@@ -16,11 +16,16 @@ Scenes:
   clone/split boundary, opacities far from the prune threshold), so the comparison below is of
   values, not of a coin flip at a threshold.
 
-Bars: replicas bit-identical (every parameter, Adam moment and statistic), and
-equal to one process that renders the same views, sums their gradients in rank order, divides by
-N and steps, to <= 1e-4 relative L1 per tensor for parameters and both moments.  What remains
-between the two is the blend backward's float atomics (run-dependent order) and Adam turning a
-last-bit change of a cancelling gradient into a full lr step.
+The fused step on N ranks is the Gaussian-sharded one (rain_amd/sharded.py): each rank renders its
+view from geometry the row owners preprocessed, and the owners run every view's per-Gaussian
+backward, the sum over views in view order, and Adam on their rows.
+
+Bars: replicas bit-identical after Trainer.sync_state (every parameter, Adam
+moment and statistic), and equal to one process that renders the same views, sums their
+raw-parameter gradients in view order, divides by N and steps, to <= 1e-4 relative L1 per tensor
+for parameters and both moments.  What remains between the two is the blend backward's float
+atomics (run-dependent order) and Adam turning a last-bit change of a cancelling gradient into a
+full lr step.
 """
 import hashlib
 import os
@@ -123,10 +128,9 @@ def _worker(rank, world, port, out_path, name):
     torch.cuda.set_device(dev)
     g, opt, cams, gts = _scene(dev, name)
     tr = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=False, seed=5), scene_extent=4.4)
-    assert tr.fused and tr.world == world and not tr.exchange.direct
+    assert tr.fused and tr.world == world and not tr.exchange.direct and tr._owner is not None
     flags = [tr.step(it).densified for it in SCENES[name]["iters"]]
-    tr.sync_densify_stats()  # merge what accumulated since the last densify
-    tr.sync_optimizer_state()  # the last iteration advanced only this rank's slice of the moments
+    tr.sync_state()  # parameters, moments and statistics are current only on their owner's rows
     torch.cuda.synchronize()
     snap = _snapshot(g)
     digests = {k: _digest(v) for k, v in snap.items()}
@@ -148,10 +152,9 @@ def _free_port():
 
 
 def _reference(dev, world, name):
-    """One process: the world's views of each step through the fused forward/backward, gradients
-    summed in rank order then divided by the world size, statistics kept per view slot and summed
-    in slot order where the sharded step merges them (densify, and at the end), then the world-1
-    densify/Adam logic."""
+    """One process: the world's views of each step through the fused forward/backward, raw-parameter
+    gradients summed in view order then divided by the world size, statistics accumulated view
+    after view, then the world-1 densify/Adam logic."""
     from rain_amd import fused
     from rain_amd.loss import l1_ssim_backward, l1_ssim_forward
     from rain_amd.train import TrainConfig, Trainer, ViewSampler
@@ -161,31 +164,17 @@ def _reference(dev, world, name):
     sampler = ViewSampler(len(cams), world, seed=5)
     bg = torch.zeros(3, device=dev)
     flags = []
-    slots = None
-
-    def merge():
-        g.xyz_gradient_accum = slots[0][0].clone()
-        g.denom = slots[0][1].clone()
-        g.max_radii2D = slots[0][2].clone()
-        for a, d, m in slots[1:]:
-            g.xyz_gradient_accum += a
-            g.denom += d
-            torch.maximum(g.max_radii2D, m, out=g.max_radii2D)
-
     for it in SCENES[name]["iters"]:
-        if slots is None or slots[0][0].shape[0] != g.get_xyz.shape[0]:
-            P = g.get_xyz.shape[0]
-            slots = [(torch.zeros(P, 1, device=dev), torch.zeros(P, 1, device=dev), torch.zeros(P, device=dev))
-                     for _ in range(world)]
         g.update_learning_rate(it)
         views = sampler.next_group()
         acc = None
-        for r, v in enumerate(views):
+        for v in views:
             color, radii, depth, st = fused.forward(g, cams[v], bg, 0.3)
             _, _, ws = l1_ssim_forward(color, gts[v], opt.lambda_dssim)
             dimg = l1_ssim_backward(color, gts[v], opt.lambda_dssim, ws)
             grads = {n: torch.empty_like(p) for n, p in zip(NAMES, g.params())}
-            fused.backward(st, dimg, grads, slots[r] if it < opt.densify_until_iter else None)
+            stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D) if it < opt.densify_until_iter else None
+            fused.backward(st, dimg, grads, stats)
             if acc is None:
                 acc = [grads[n].clone() for n in NAMES]
             else:
@@ -193,14 +182,8 @@ def _reference(dev, world, name):
                     a += grads[n]
         g.bind_flat_grad()
         for a, p in zip(acc, g.params()):
-            p.grad.copy_(a / float(world))
-        densify, _reset = tr._events(it)
-        if densify:
-            merge()
-            slots = None
+            p.grad.copy_(a * (1.0 / world))
         flags.append(tr._densify_and_adam(it))
-    if slots is not None:
-        merge()
     torch.cuda.synchronize()
     return {k: v.cpu() for k, v in _snapshot(g).items()}, flags
 
@@ -266,20 +249,20 @@ def _worker_rccl(rank, world, port, out_path):
 
     g, opt, cams, gts = _scene(dev, "small")
     tr = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=False, seed=5), scene_extent=4.4, exchange=True)
-    assert tr.fused and tr.sharded and tr.exchange.direct
+    assert tr.fused and tr.sharded and tr.exchange.direct and tr._owner is not None
     flags = [tr.step(it).densified for it in SCENES["small"]["iters"]]
-    tr.sync_densify_stats()
-    tr.sync_optimizer_state()
+    tr.sync_state()
     torch.cuda.synchronize()
     torch.save({"snap": {k: v.cpu() for k, v in _snapshot(g).items()}, "flags": flags}, f"{out_path}.{rank}")
     torch.distributed.destroy_process_group()
 
 
 def test_rccl_exchange_path_one_rank(tmp_path):
-    """The RCCL branch of Trainer.Exchange (reduce_scatter_tensor / all_gather_into_tensor /
-    all_reduce on device tensors) and bench.py's init_process_group("nccl", device_id=...) on a
-    one-rank group (the box has one GPU): the sharded step, forced at world 1, must equal the plain
-    single-GPU step (Adam fused into the backward) through ordinary, densify and reset iterations."""
+    """The RCCL branch of Trainer.Exchange (all_to_all_single / all_gather_into_tensor on device
+    tensors) and bench.py's init_process_group("nccl", device_id=...) on a one-rank group (the box
+    has one GPU): the Gaussian-sharded step (rain_amd/sharded.py), forced at world 1, must equal the
+    plain single-GPU step (Adam fused into the backward) through ordinary, densify and reset
+    iterations."""
     if torch.cuda.device_count() < 1:
         pytest.skip("no HIP device")
     out = str(tmp_path / "rccl")

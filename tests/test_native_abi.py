@@ -45,6 +45,34 @@ def test_size_queries():
     assert L.rr_version().decode().startswith("rain_amd")
 
 
+def test_geometry_layout_and_sharded_step_validation():
+    """rr_geometry_layout: the preprocess arrays' offsets inside a geometry buffer (the sharded
+    step's all-to-all writes there): distinct, ordered, 256-B aligned, inside rr_geometry_bytes.
+    The sharded entry points refuse bad row blocks / views before touching a device."""
+    L = N.raster()
+    for P in (256, 20480, 1000192):
+        o = (ctypes.c_size_t * 5)()
+        assert L.rr_geometry_layout(P, o) == 0
+        offs = list(o)
+        assert offs == sorted(offs) and len(set(offs)) == 5 and all(x % 256 == 0 for x in offs)
+        assert offs[1] - offs[0] >= 48 * P and offs[2] - offs[1] >= 8 * P and offs[3] - offs[2] >= 4 * P
+        assert offs[4] + 4 * (P // 256) <= L.rr_geometry_bytes(P)
+    assert L.rr_geometry_layout(-1, (ctypes.c_size_t * 5)()) == 1
+    f = N.RRFrame(300, 3, 16, 64, 48, 0.5, 0.4, 1.0, 0.3, 0, 0, N.RR_FLAG_RAW_PARAMS)
+    cam = N.RRCamera(1, 1, 1, 1)
+    g = N.RRGaussians(1, 1, None, 1, 1, 1, None, 1)
+    rc = L.rr_preprocess_rows(ctypes.byref(f), ctypes.byref(cam), ctypes.byref(g), 300, 1, 1, 1, 1, 1, 1, None)
+    assert rc == 1 and b"multiple of 256" in L.rr_last_error()
+    views = (N.RRView * 17)()
+    out = N.RRGrads()
+    rc = L.rr_gauss_backward_views(ctypes.byref(f), views, 17, ctypes.byref(g), None, 300, 1.0, ctypes.byref(out), None)
+    assert rc == 1 and b"num_views" in L.rr_last_error()
+    nr, npairs, need = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_size_t(0)
+    rc = L.rr_forward_from_geometry(ctypes.byref(f), ctypes.byref(cam), None, None, 0, None, 0, None, 0,
+                                    ctypes.byref(nr), ctypes.byref(npairs), ctypes.byref(need), None, None, None)
+    assert rc == 1 and b"multiple of 256" in L.rr_last_error()
+
+
 def test_validation_errors_without_gpu():
     L = N.raster()
     f = N.RRFrame(10, 3, 16, 64, 48, 0.5, 0.4, 1.0, 0.3, 0, 0)
