@@ -11,7 +11,8 @@ cross the links are per-(Gaussian, view) records instead:
   1. owner preprocess: for each of the step's N views, its rows' splat records (48 B), pair
      counts, depth keys, radii and per-256-row block sums (rr_preprocess_rows), ~64 B per row;
   2. all-to-all (RCCL over xGMI, every pair of GPUs on its own link): rank v receives view v's
-     arrays of every block straight into its geometry buffer (rr_geometry_layout);
+     arrays of every block in one collective (one packed chunk per view) and copies each field
+     into its geometry buffer (rr_geometry_layout);
   3. rank v renders view v from that geometry (rr_forward_from_geometry: depth sort, binning,
      blend), computes the L1+SSIM loss and its gradient, and runs the blend backward into one
      40-B record per Gaussian (rr_backward_records);
@@ -98,15 +99,18 @@ class ShardedStep:
         stream = N.stream_of(model._xyz)
         u8 = torch.uint8
 
-        # 1. owner preprocess of every view over the owned rows -> send buffers [N][Q]
+        # 1. owner preprocess of every view over the owned rows -> send buffer: one chunk per view,
+        #    [splat records Q x 48 B | pair counts Q x 8 | depth keys Q x 4 | radii Q x 4 |
+        #     block sums Q/256 x 8 | wide flags Q/256 x 4]
         gs, M = self._row_params(model, lo)
         nb = Q // 256
-        s_spl = self._buf("s_spl", Nw * Q * SPLAT_BYTES, u8, dev)
-        s_til = self._buf("s_til", Nw * Q * 8, u8, dev)
-        s_key = self._buf("s_key", Nw * Q * 4, u8, dev)
-        s_rad = self._buf("s_rad", Nw * Q * 4, u8, dev)
-        s_bsm = self._buf("s_bsm", Nw * nb * 8, u8, dev)
-        s_bwd = self._buf("s_bwd", Nw * nb * 4, u8, dev)
+        fields = ((SPLAT_BYTES, Q), (8, Q), (4, Q), (4, Q), (8, nb), (4, nb))
+        starts, c = [], 0
+        for w, n in fields:
+            starts.append(c)
+            c += w * n
+        chunk = c
+        send = self._buf("g_send", Nw * chunk, u8, dev)
         keep = []
         for v, cam in enumerate(cams):
             fr = self._frame(model, nv, cam, low_pass, flags | N.RR_FLAG_RAW_PARAMS)
@@ -114,21 +118,27 @@ class ShardedStep:
                  cam.camera_center.contiguous())
             keep.append(k)
             rc = N.RRCamera(*[_p(t) for t in k])
+            b = v * chunk
             N.check(L.rr_preprocess_rows(ctypes.byref(fr), ctypes.byref(rc), ctypes.byref(gs), Q,
-                                         _p(s_rad, 4 * v * Q), _p(s_spl, SPLAT_BYTES * v * Q), _p(s_til, 8 * v * Q),
-                                         _p(s_key, 4 * v * Q), _p(s_bsm, 8 * v * nb), _p(s_bwd, 4 * v * nb), stream),
+                                         _p(send, b + starts[3]), _p(send, b + starts[0]), _p(send, b + starts[1]),
+                                         _p(send, b + starts[2]), _p(send, b + starts[4]), _p(send, b + starts[5]),
+                                         stream),
                     "sharded preprocess")
 
-        # 2. all-to-all into this rank's geometry buffer (rows in global order)
+        # 2. one all-to-all: chunk i of recv = rank i's rows for this rank's view; then each field
+        #    into its array of the geometry buffer (rows in global order)
+        recv = self._buf("g_recv", Nw * chunk, u8, dev)
+        self.ex.all_to_all(recv, send)
         geom = self._buf("geom", int(L.rr_geometry_bytes(P_pad)), u8, dev)
         offs = (ctypes.c_size_t * 5)()
         N.check(L.rr_geometry_layout(P_pad, offs), "geometry layout")
         radii = self._buf("radii", P_pad, torch.int32, dev)
-        for send, off, nbytes in ((s_spl, offs[0], P_pad * SPLAT_BYTES), (s_til, offs[1], P_pad * 8),
-                                  (s_key, offs[2], P_pad * 4), (s_bsm, offs[3], (P_pad // 256) * 8),
-                                  (s_bwd, offs[4], (P_pad // 256) * 4)):
-            self.ex.all_to_all(geom[off:off + nbytes], send)
-        self.ex.all_to_all(radii.view(u8), s_rad)
+        rv = recv.view(Nw, chunk)
+        dsts = (geom[offs[0]:offs[0] + P_pad * SPLAT_BYTES], geom[offs[1]:offs[1] + P_pad * 8],
+                geom[offs[2]:offs[2] + P_pad * 4], radii.view(u8), geom[offs[3]:offs[3] + (P_pad // 256) * 8],
+                geom[offs[4]:offs[4] + (P_pad // 256) * 4])
+        for (w, n), st0, dst in zip(fields, starts, dsts):
+            dst.view(Nw, w * n).copy_(rv[:, st0:st0 + w * n])
 
         # 3. render this rank's view from the geometry, loss, blend backward -> records
         cam = cams[self.rank]
