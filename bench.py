@@ -247,9 +247,9 @@ def main():
     # the same iteration through the reference's own API (what an unchanged train.py:109-147 runs):
     # render() -> GaussianRasterizer autograd -> getters' autograd -> torch.optim.Adam
     api_it0 = (end_iter // 100 + 1) * 100 + 1
-    api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0, K if K < 30 else 30, world, dev)
-    api_fa_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0 + 40, K if K < 30 else 30, world, dev,
-                         torch_adam=False)
+    api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0, K if K < 30 else 30, world, dev,
+                      torch_adam=False)
+    api_ta_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0 + 40, K if K < 30 else 30, world, dev)
 
     # forward-only throughput (preprocess -> blend incl. sorts and the L read-back), no autograd
     Pn = gauss.get_xyz.shape[0]
@@ -296,8 +296,13 @@ def main():
         byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2, world)
         dom_ms = dom_timed[0] / dom_timed[1]  # HIP events around every launch inside the timed loop
         gbs = byts / (dom_ms * 1e-3) / 1e9
+        rmw_gbs = _rmw_peak(dev)
         roofline = {"kernel": dom, "step_dominant": step_dom, "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "measured_copy_GBps": _copy_peak(dev),
+                    # gauss_bwd's bytes are mostly the fused Adam's in-place read-modify-write of
+                    # (param, exp_avg, exp_avg_sq): priced against that pattern measured alone
+                    "measured_rmw_GBps": rmw_gbs,
+                    "frac_of_measured_rmw": round(gbs / rmw_gbs, 4),
                     "ms_per_launch": round(dom_ms, 5), "launches": int(dom_timed[1]),
                     "frac": round(gbs / HBM_PEAK_GBS, 4),
                     # PMC passes are committed for the headline workload only (tools/pmc_workload.py)
@@ -360,11 +365,13 @@ def main():
         "bracket_ms": round(bracket_ms, 4),
         "api_iters_per_s": round(world * 1000.0 / api_ms, 3),
         "api_ms_per_step": round(api_ms, 4),
-        "api_path": "render() -> GaussianRasterizer (autograd) -> GaussianModel getters (autograd) -> HIP L1+SSIM "
-                    "(autograd) -> torch.optim.Adam (foreach); no densify event in the window",
-        # the same path with this package's GaussianModel optimizer (FusedAdam): torch's foreach Adam
-        # alone takes ~1.5 ms of device time per step on ROCm (profiles/r03_api_step_trace.txt)
-        "api_fusedadam_iters_per_s": round(world * 1000.0 / api_fa_ms, 3),
+        "api_path": "unchanged train.py loop over this package's modules: render() -> GaussianRasterizer (autograd) "
+                    "-> GaussianModel getters (autograd) -> HIP L1+SSIM (autograd) -> the optimizer "
+                    "GaussianModel.training_setup builds (FusedAdam: torch.optim.Adam's state and arithmetic, one "
+                    "launch); no densify event in the window",
+        # the same loop with the stock torch.optim.Adam swapped in (foreach on ROCm: ~1.5 ms of
+        # device time per step at 59M parameters, profiles/r03_api_step_trace.txt)
+        "api_torch_adam_iters_per_s": round(world * 1000.0 / api_ta_ms, 3),
         "gaussians_after": int(Pn),
         "frame_stats": {k: int(v) for k, v in mean_stats.items()},
         "roofline": roofline,
@@ -495,6 +502,38 @@ def _copy_peak(dev):
     ms = e0.elapsed_time(e1) / 10
     del a, b
     return round(2 * (1 << 30) / (ms * 1e-3) / 1e9, 1)
+
+
+def _rmw_peak(dev):
+    """Achievable rate of Adam's in-place access pattern: read + write bytes / time of the
+    library's three-array read-modify-write stream (rt_stream_rmw: param, exp_avg, exp_avg_sq of
+    59M floats, the bench model's parameter count), HIP events on its stream.  The fused-Adam
+    backward moves mostly these bytes; on MI355X this pattern runs well below a copy."""
+    import torch
+
+    from rain_amd import _native
+
+    L = _native.train_lib()
+    n = 59_000_000
+    buf = torch.zeros(3 * n, dtype=torch.float32, device=dev)
+    p, m, v = buf[:n], buf[n:2 * n], buf[2 * n:]
+    st = _native.stream_of(buf)
+
+    def rmw():
+        if L.rt_stream_rmw(p.data_ptr(), m.data_ptr(), v.data_ptr(), n, st) != 0:
+            raise RuntimeError(L.rt_last_error().decode())
+
+    for _ in range(3):
+        rmw()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        rmw()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    del buf
+    return round(6 * 4 * n / (ms * 1e-3) / 1e9, 1)
 
 
 def _host_cpus():

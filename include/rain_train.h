@@ -107,6 +107,13 @@ int rt_densify_apply(const rt_densify_params* p, const float* scaling, const flo
  * float4 copy, ~6.3 TB/s read + write on MI355X). */
 int rt_stream_copy(void* dst, const void* src, size_t n_bytes, void* stream);
 
+/* In-place read-modify-write stream over three arrays of n_floats (multiple of 4; 16-B aligned):
+ * the access pattern of an Adam step (param, exp_avg, exp_avg_sq read and written back) with a
+ * few FMAs for arithmetic.  Not on the training path: the achievable rate for that pattern
+ * (~5.3-5.5 TB/s read + write on MI355X, below the copy's ~6.6: tools/rmw_probe.hip), which
+ * bench.py prices the fused-Adam backward kernel against. */
+int rt_stream_rmw(float* p, float* m, float* v, size_t n_floats, void* stream);
+
 const char* rt_last_error(void);
 
 #ifdef __cplusplus

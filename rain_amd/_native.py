@@ -197,7 +197,7 @@ def loss_lib():
 
 TRAIN_LIB = os.path.join(LIB_DIR, "librain_train.so")
 TRAIN_SYMBOLS = ["rt_adam_step", "rt_adam_step_scaled", "rt_densify_workspace_bytes", "rt_densify_plan",
-                 "rt_densify_apply", "rt_stream_copy", "rt_last_error"]
+                 "rt_densify_apply", "rt_stream_copy", "rt_stream_rmw", "rt_last_error"]
 RT_MAX_GROUPS = 8
 _train = None
 
@@ -245,6 +245,8 @@ def train_lib():
                                        vp]
         L.rt_stream_copy.restype = ctypes.c_int
         L.rt_stream_copy.argtypes = [vp, vp, ctypes.c_size_t, vp]
+        L.rt_stream_rmw.restype = ctypes.c_int
+        L.rt_stream_rmw.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
         L.rt_last_error.restype = ctypes.c_char_p
         _train = L
     return _train

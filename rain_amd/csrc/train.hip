@@ -94,6 +94,20 @@ __global__ __launch_bounds__(256) void k_stream_copy(v4f* __restrict__ dst, cons
     if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
+// Adam's access pattern with the arithmetic reduced to a few FMAs: three arrays read and written
+// back in place, one float4 of each per lane (the best of the layouts tools/rmw_probe.hip tried).
+__global__ __launch_bounds__(256) void k_stream_rmw(v4f* __restrict__ p, v4f* __restrict__ m, v4f* __restrict__ v,
+                                                    int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    v4f a = p[i], b = m[i], c = v[i];
+    b = b * 0.9f + a * 0.1f;
+    c = c * 0.999f + a * a * 0.001f;
+    p[i] = a - b * 1e-3f;
+    m[i] = b;
+    v[i] = c;
+}
+
 }  // namespace
 
 namespace rt_internal {
@@ -154,6 +168,18 @@ int rt_stream_copy(void* dst, const void* src, size_t n_bytes, void* stream) {
     k_stream_copy<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>((v4f*)dst, (const v4f*)src, n);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(std::string("stream copy launch: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int rt_stream_rmw(float* p, float* m, float* v, size_t n_floats, void* stream) {
+    if ((n_floats & 3u) || !aligned16(p) || !aligned16(m) || !aligned16(v))
+        return fail("stream rmw: 4-float multiples, 16-B aligned arrays only");
+    const int64_t n = (int64_t)(n_floats / 4);
+    if (n == 0) return 0;
+    if (n > (int64_t)0xffffffff * 256) return fail("stream rmw: too large");
+    k_stream_rmw<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>((v4f*)p, (v4f*)m, (v4f*)v, n);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(std::string("stream rmw launch: ") + hipGetErrorString(e));
     return 0;
 }
 
