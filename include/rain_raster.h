@@ -255,11 +255,16 @@ int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int*
 int rr_forward_render_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
                                void* image_buffer, void* binning_buffer, size_t binning_bytes, int num_pairs,
                                float* out_color, float* out_depth, void* stream);
-/* Blend backward of a frame into records [P][10] (floats: dmean2D.xy, dconic.xyz, dopacity,
- * dcolor.rgb, radius); workspace as rr_backward. */
+/* Blend backward of a frame into one record of 10 floats per row (dmean2D.xy, dconic.xyz,
+ * dopacity, dcolor.rgb, radius); workspace as rr_backward.  rows_per_rank = 0: records [P][10].
+ * rows_per_rank = Q > 0 (dividing P = N*Q): grouped for an exchange in row chunks of chunk_rows —
+ * chunk c (owner rows [r0, r0 + n_c), r0 = c*chunk_rows, n_c = min(chunk_rows, Q - r0)) is the
+ * contiguous block [N][n_c][10] at row offset N*r0, so that its all-to-all can start while the
+ * owners already run the previous chunk (rr_gauss_backward_views on n_c rows, record_rows n_c). */
 int rr_backward_records(const rr_frame* f, const rr_camera* cam, const int* radii, const void* geom_buffer,
                         const void* image_buffer, const void* binning_buffer, int num_rendered, const float* dL_dpix,
-                        void* workspace, size_t workspace_bytes, float* records, void* stream);
+                        void* workspace, size_t workspace_bytes, int rows_per_rank, int chunk_rows, float* records,
+                        void* stream);
 /* Per-Gaussian backward of a row block over num_views views (records [num_views][record_rows][10]),
  * RR_FLAG_RAW_PARAMS only: frame.P rows, frame.D / M / scale_modifier; gaussians = raw parameters
  * offset to the block.  out: no gradient arrays; optional densification statistics (offset to the

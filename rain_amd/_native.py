@@ -166,7 +166,7 @@ def raster():
         L.rr_forward_render_geometry.restype = ci
         L.rr_forward_render_geometry.argtypes = [fp, cp, vp, vp, vp, vp, sz, ci, vp, vp, vp]
         L.rr_backward_records.restype = ci
-        L.rr_backward_records.argtypes = [fp, cp, vp, vp, vp, vp, ci, vp, vp, sz, vp, vp]
+        L.rr_backward_records.argtypes = [fp, cp, vp, vp, vp, vp, ci, vp, vp, sz, ci, ci, vp, vp]
         L.rr_gauss_backward_views.restype = ci
         L.rr_gauss_backward_views.argtypes = [fp, ctypes.POINTER(RRView), ci, gp, vp, ci, ctypes.c_float,
                                               ctypes.POINTER(RRGrads), vp]

@@ -843,10 +843,13 @@ int rr_forward_render_geometry(const rr_frame* f, const rr_camera* cam, const in
 
 int rr_backward_records(const rr_frame* f, const rr_camera* cam, const int* radii, const void* geom_buffer,
                         const void* image_buffer, const void* binning_buffer, int num_rendered, const float* dL_dpix,
-                        void* workspace, size_t workspace_bytes, float* records, void* stream) {
+                        void* workspace, size_t workspace_bytes, int rows_per_rank, int chunk_rows, float* records,
+                        void* stream) {
     if (!f || !cam) return fail(RR_ERR_ARG, "null frame / camera");
     const int P = f->P;
     if (P < 0) return fail(RR_ERR_ARG, "bad P");
+    if (rows_per_rank < 0 || (rows_per_rank > 0 && (P % rows_per_rank != 0 || chunk_rows < 1)))
+        return fail(RR_ERR_ARG, "rows_per_rank must divide P (and chunk_rows >= 1), or be 0");
     if (P == 0) return RR_OK;
     if (!radii || !geom_buffer || !image_buffer || !dL_dpix || !workspace || !records || !cam->background)
         return fail(RR_ERR_ARG, "null buffer");
@@ -855,7 +858,8 @@ int rr_backward_records(const rr_frame* f, const rr_camera* cam, const int* radi
     float* gacc = static_cast<float*>(workspace);
     if (int rc = blend_backward(f, cam, geom_buffer, image_buffer, binning_buffer, num_rendered, dL_dpix, gacc, st))
         return rc;
-    launch_pack_records(gacc, radii, P, records, st);
+    launch_pack_records(gacc, radii, P, rows_per_rank, rows_per_rank > 0 ? std::min(chunk_rows, rows_per_rank) : 1,
+                        records, st);
     return check(f, st, "pack records");
 }
 

@@ -714,10 +714,17 @@ int launch_gauss_bwd_views(const GaussBwdArgs& a, const ViewCam* cams, int V, co
 }
 
 // Packed per-(Gaussian, view) record for the sharded step: accumulator slots 0..8 and the radius.
+// Q > 0: rows are grouped for a chunked exchange (rr_backward_records) — row i = j*Q + r of owner
+// j lands in chunk c = r / CR at N*r0 + j*rows_c + (r - r0) (r0 = c*CR, rows_c = min(CR, Q - r0)).
 __global__ __launch_bounds__(256) void k_pack_records(const float* __restrict__ gacc, const int* __restrict__ radii,
-                                                      int P, float* __restrict__ rec) {
+                                                      int P, int Q, int CR, float* __restrict__ rec) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= P) return;
+    size_t pos = (size_t)i;
+    if (Q > 0) {
+        const int j = i / Q, r = i - j * Q, r0 = (r / CR) * CR;
+        pos = (size_t)(P / Q) * r0 + (size_t)j * min(CR, Q - r0) + (r - r0);
+    }
     const int r = radii[i];
     float v[kRecFloats];
     if (r > 0) {
@@ -731,13 +738,14 @@ __global__ __launch_bounds__(256) void k_pack_records(const float* __restrict__ 
         for (int k = 0; k < 9; k++) v[k] = 0.f;
     }
     v[9] = (float)r;
-    float2* o = reinterpret_cast<float2*>(rec + (size_t)i * kRecFloats);
+    float2* o = reinterpret_cast<float2*>(rec + pos * kRecFloats);
 #pragma unroll
     for (int k = 0; k < kRecFloats / 2; k++) o[k] = make_float2(v[2 * k], v[2 * k + 1]);
 }
 
-void launch_pack_records(const float* gacc, const int* radii, int P, float* rec, hipStream_t st) {
-    if (P > 0) k_pack_records<<<(P + 255) / 256, 256, 0, st>>>(gacc, radii, P, rec);
+void launch_pack_records(const float* gacc, const int* radii, int P, int Q, int chunk_rows, float* rec,
+                         hipStream_t st) {
+    if (P > 0) k_pack_records<<<(P + 255) / 256, 256, 0, st>>>(gacc, radii, P, Q, chunk_rows, rec);
 }
 
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st) {

@@ -282,7 +282,8 @@ struct ViewCam {
 // rows a.P of a row block, V <= 16 views (records [V][rec_rows][10]); returns 1 on a bad V
 int launch_gauss_bwd_views(const GaussBwdArgs& a, const ViewCam* cams, int V, const float* records, int rec_rows,
                            float grad_scale, hipStream_t st);
-void launch_pack_records(const float* gacc, const int* radii, int P, float* rec, hipStream_t st);
+void launch_pack_records(const float* gacc, const int* radii, int P, int Q, int chunk_rows, float* rec,
+                         hipStream_t st);
 
 }  // namespace rr
 

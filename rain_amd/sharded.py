@@ -16,7 +16,9 @@ cross the links are per-(Gaussian, view) records instead:
   3. rank v renders view v from that geometry (rr_forward_from_geometry: depth sort, binning,
      blend), computes the L1+SSIM loss and its gradient, and runs the blend backward into one
      40-B record per Gaussian (rr_backward_records);
-  4. all-to-all: the owner receives its rows' records of all N views;
+  4. all-to-all: the owner receives its rows' records of all N views (in row chunks when the row
+     block is large enough that each chunk's owner launch still fills the GPU: chunk c's
+     exchange then overlaps the owner kernel on chunk c-1);
   5. owner: the per-Gaussian backward of every view in view order, summed, x 1/N, Adam on its rows,
      densification statistics (rr_gauss_backward_views).
 So ~2 x (N-1)/N x 104 B per Gaussian per step cross xGMI (all-to-all: each GPU's share leaves on
@@ -56,10 +58,25 @@ def row_blocks(P: int, world: int):
 class ShardedStep:
     """One rank's side of the Gaussian-sharded step (see the module docstring)."""
 
-    def __init__(self, exchange, rank: int, world: int):
+    # rows one owner-kernel launch needs to fill the GPU: 256 CUs x 6 resident workgroups x 128 rows
+    FILL_ROWS = 256 * 6 * 128
+
+    def __init__(self, exchange, rank: int, world: int, rec_chunk_rows: int | None = None):
         self.ex = exchange
         self.rank, self.world = rank, world
         self._bufs = {}
+        self.rec_chunk_rows = rec_chunk_rows
+
+    def chunk_rows(self, Q: int) -> int:
+        """Rows per chunk of the record exchange (a multiple of 256).  Chunk c's all-to-all runs while
+        the owners process chunk c-1, but every chunk is a launch of its own, so chunks are only
+        cut where each still fills the GPU (Q >= 2 x FILL_ROWS, i.e. several million Gaussians at
+        N = 8); rec_chunk_rows overrides (tests)."""
+        if self.rec_chunk_rows:
+            return max(256, int(self.rec_chunk_rows) // 256 * 256)
+        units = Q // 256
+        C = max(1, min(4, Q // self.FILL_ROWS))
+        return 256 * -(-units // C)
 
     def _buf(self, key, numel, dtype, dev):
         t = self._bufs.get(key)
@@ -166,28 +183,59 @@ class ShardedStep:
         dimg = dimg.contiguous()
         ws = self._buf("ws", int(L.rr_backward_workspace_bytes(P_pad)), u8, dev)
         recs = self._buf("recs", P_pad * REC_FLOATS, torch.float32, dev)
+        CR = self.chunk_rows(Q)
         N.check(L.rr_backward_records(ctypes.byref(fr), ctypes.byref(rc), _p(radii), _p(geom), _p(img), _p(binning),
-                                      nr.value, _p(dimg), _p(ws), ws.numel(), _p(recs), stream), "sharded backward")
+                                      nr.value, _p(dimg), _p(ws), ws.numel(), Q, CR, _p(recs), stream),
+                "sharded backward")
 
-        # 4. all-to-all of the records: chunk v of recv = view v's records of the owned rows
-        recv = self._buf("recv", Nw * Q * REC_FLOATS, torch.float32, dev)
-        self.ex.all_to_all(recv, recs)
-
-        # 5. owner: per-Gaussian backward of all views, summed in view order, x 1/N, Adam, statistics
-        if nv > 0:
-            views = (N.RRView * Nw)()
-            for v, c in enumerate(cams):
-                kv = keep[v]
-                views[v] = N.RRView(_p(kv[1]), _p(kv[2]), _p(kv[3]), math.tan(c.FoVx * 0.5), math.tan(c.FoVy * 0.5),
-                                    float(low_pass), int(c.image_width), int(c.image_height))
-            frb = self._frame(model, nv, cams[0], low_pass, N.RR_FLAG_RAW_PARAMS)
-            acc, den, mr = stats if stats is not None else (None, None, None)
-            ad = _offset_adam(adam, model, lo) if adam is not None else None
-            out = N.RRGrads(None, None, None, None, None, None, None, None, None, _p(acc, 4 * lo), _p(den, 4 * lo),
-                            _p(mr, 4 * lo), ctypes.pointer(ad) if ad is not None else None)
-            N.check(L.rr_gauss_backward_views(ctypes.byref(frb), views, Nw, ctypes.byref(gs), _p(recv), Q,
-                                              1.0 / Nw, ctypes.byref(out), stream), "sharded gaussian backward")
+        self.exchange_and_own(model, cams, keep, recs, low_pass, adam, stats)
         return color, loss
+
+    def exchange_and_own(self, model, cams, keep, recs, low_pass, adam, stats):
+        """Steps 4-5 of step(): the record exchange and the owners' per-Gaussian backward + Adam.
+        `recs`: this rank's records in rr_backward_records' chunked layout for chunk_rows(Q);
+        `keep[v]`: (bg, view, proj, campos) tensors of view v."""
+        L = N.raster()
+        dev = model._xyz.device
+        P = model._xyz.shape[0]
+        Nw = self.world
+        Q, _P_pad, lo, nv = self.layout(P)
+        stream = N.stream_of(model._xyz)
+        CR = self.chunk_rows(Q)
+        # 4. all-to-all of the records in row chunks (rr_backward_records lays chunk c out as
+        #    [N][n_c][10] at row N*r0): chunk c of recv = view v's records of the owned rows
+        #    [r0, r0 + n_c) for v = 0..N-1; all chunks are issued before the first owner launch
+        recv = self._buf("recv", Nw * Q * REC_FLOATS, torch.float32, dev)
+        chunks, r0 = [], 0
+        while r0 < Q:
+            n_c = min(CR, Q - r0)
+            a, b = Nw * r0 * REC_FLOATS, Nw * (r0 + n_c) * REC_FLOATS
+            chunks.append((r0, n_c, a, self.ex.all_to_all(recv[a:b], recs[a:b], async_op=True)))
+            r0 += n_c
+
+        # 5. owner, per chunk once its records are in: per-Gaussian backward of all views, summed in
+        #    view order, x 1/N, Adam, statistics (rows are independent: any chunking gives the same
+        #    bits)
+        views = (N.RRView * Nw)()
+        for v, c in enumerate(cams):
+            kv = keep[v]
+            views[v] = N.RRView(_p(kv[1]), _p(kv[2]), _p(kv[3]), math.tan(c.FoVx * 0.5), math.tan(c.FoVy * 0.5),
+                                float(low_pass), int(c.image_width), int(c.image_height))
+        acc, den, mr = stats if stats is not None else (None, None, None)
+        for r0, n_c, a, work in chunks:
+            if work is not None:
+                work.wait()
+            nv_c = max(0, min(n_c, nv - r0))
+            if nv_c == 0:
+                continue
+            row = lo + r0
+            gs_c, _M = self._row_params(model, row)
+            frb = self._frame(model, nv_c, cams[0], low_pass, N.RR_FLAG_RAW_PARAMS)
+            ad = _offset_adam(adam, model, row) if adam is not None else None
+            out = N.RRGrads(None, None, None, None, None, None, None, None, None, _p(acc, 4 * row), _p(den, 4 * row),
+                            _p(mr, 4 * row), ctypes.pointer(ad) if ad is not None else None)
+            N.check(L.rr_gauss_backward_views(ctypes.byref(frb), views, Nw, ctypes.byref(gs_c), _p(recv, 4 * a), n_c,
+                                              1.0 / Nw, ctypes.byref(out), stream), "sharded gaussian backward")
 
     # ---- replicas ------------------------------------------------------------------------------
     def sync_replicas(self, model):

@@ -100,15 +100,17 @@ class Exchange:
         dist.all_gather_into_tensor(out, buf[lo:lo + S].to("cpu", copy=True), group=self.group)
         buf.copy_(out)
 
-    def all_to_all(self, recv: torch.Tensor, send: torch.Tensor):
-        """Chunk j of `send` (N equal chunks) goes to rank j; chunk i of `recv` comes from rank i."""
+    def all_to_all(self, recv: torch.Tensor, send: torch.Tensor, async_op: bool = False):
+        """Chunk j of `send` (N equal chunks) goes to rank j; chunk i of `recv` comes from rank i.
+        async_op (RCCL only): returns the collective's work handle; its wait() makes the current
+        stream wait for it.  Otherwise the exchange is complete on return (None)."""
         if self.direct:
-            dist.all_to_all_single(recv, send, group=self.group)
-            return
+            return dist.all_to_all_single(recv, send, group=self.group, async_op=async_op)
         h = send.detach().to("cpu", copy=True).contiguous()
         out = torch.empty_like(h)
         dist.all_to_all_single(out, h, group=self.group)
         recv.copy_(out)
+        return None
 
     def all_gather_rows(self, t: torch.Tensor, Q: int, lo: int):
         """Rank r contributes rows [r*Q, r*Q + Q) of t (rows past t's end as padding); afterwards

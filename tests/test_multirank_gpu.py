@@ -119,7 +119,7 @@ def _digest(t):
     return hashlib.blake2b(t.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes(), digest_size=16).hexdigest()
 
 
-def _worker(rank, world, port, out_path, name):
+def _worker(rank, world, port, out_path, name, chunk_rows=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     from rain_amd.train import TrainConfig, Trainer
@@ -129,6 +129,7 @@ def _worker(rank, world, port, out_path, name):
     g, opt, cams, gts = _scene(dev, name)
     tr = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=False, seed=5), scene_extent=4.4)
     assert tr.fused and tr.world == world and not tr.exchange.direct and tr._owner is not None
+    tr._owner.rec_chunk_rows = chunk_rows
     flags = [tr.step(it).densified for it in SCENES[name]["iters"]]
     tr.sync_state()  # parameters, moments and statistics are current only on their owner's rows
     torch.cuda.synchronize()
@@ -194,11 +195,12 @@ def _rel_l1(x, y):
     return float((x - y).abs().sum()) / den if den > 0 else float((x - y).abs().sum())
 
 
-def _run(tmp_path, world, name):
+def _run(tmp_path, world, name, chunk_rows=None):
     if torch.cuda.device_count() < 1:  # does not initialise the GPU in this process
         pytest.skip("no HIP device")
     out = str(tmp_path / "rank")
-    mp.start_processes(_worker, args=(world, _free_port(), out, name), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), out, name, chunk_rows), nprocs=world, join=True,
+                       start_method="spawn")
     rs = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     for r in rs[1:]:
         assert r["digests"] == rs[0]["digests"], [k for k in r["digests"] if r["digests"][k] != rs[0]["digests"][k]]
@@ -225,6 +227,12 @@ def _run(tmp_path, world, name):
 
 def test_view_sharded_fused_step_two_ranks(tmp_path):
     _run(tmp_path, 2, "small")
+
+
+def test_view_sharded_fused_step_two_ranks_chunked_exchange(tmp_path):
+    """The record exchange in row chunks of 256 (40 chunks per owner; rr_backward_records' chunked
+    layout, one all-to-all and one owner launch per chunk) against the same bars."""
+    _run(tmp_path, 2, "small", chunk_rows=256)
 
 
 def test_view_sharded_fused_step_four_ranks(tmp_path):
