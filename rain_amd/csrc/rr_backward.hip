@@ -185,8 +185,9 @@ __device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const
 // from that view's blend backward (GACC layout: dmean2D.xy, dconic.xyz, dopacity, dcolor.rgb) with
 // its radius.
 struct GaccRec {
-    const float* gp;  // GACC_STRIDE floats (single view) or a packed kRecFloats record (read when radius > 0)
+    const float* gp;  // GACC_STRIDE floats (single view, read when radius > 0)
     int radius;
+    const float2* q;  // a packed kRecFloats record already in registers (multi-view kernel)
 };
 __device__ __forceinline__ ViewCam view_cam(const GaussBwdArgs& a) {
     return ViewCam{a.view, a.proj, a.campos, a.tanfovx, a.tanfovy, a.focal_x, a.focal_y, a.low_pass};
@@ -246,8 +247,8 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, const ViewC
 
     float4 ga, gb;
     float g8;
-    if (PACKED) {  // 40-B record, 8-B aligned
-        const float2* q = reinterpret_cast<const float2*>(rec.gp);
+    if (PACKED) {  // 40-B record, loaded by the caller
+        const float2* q = rec.q;
         const float2 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
         ga = make_float4(q0.x, q0.y, q1.x, q1.y);
         gb = make_float4(q2.x, q2.y, q3.x, q3.y);
@@ -558,13 +559,26 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
         const int idx = i0 + t;
         float* row = stage ? s_sh + t * kShStride : nullptr;
         if (!MULTI) {
-            const GaccRec rec{a.gacc + (size_t)idx * GACC_STRIDE, a.radii[idx]};
+            const GaccRec rec{a.gacc + (size_t)idx * GACC_STRIDE, a.radii[idx], nullptr};
             gauss_bwd_one<DEG, false>(a, view_cam(a), idx, rec, row, row, false, sg);
         } else {
             float* grow = stage ? s_gr + t * kShStride : nullptr;
+            // each view's 40-B record is loaded while the previous view is processed (one record
+            // in flight ahead instead of a radius load then a dependent record load per view)
+            const float2* rp = reinterpret_cast<const float2*>(va->records) + (size_t)idx * (kRecFloats / 2);
+            const size_t vstride = (size_t)va->rec_rows * (kRecFloats / 2);
+            float2 nq[kRecFloats / 2];
+#pragma unroll
+            for (int k = 0; k < kRecFloats / 2; k++) nq[k] = rp[k];
             for (int v = 0; v < va->V; v++) {
-                const float* rp = va->records + ((size_t)v * va->rec_rows + idx) * kRecFloats;
-                const GaccRec rec{rp, (int)rp[9]};
+                float2 cq[kRecFloats / 2];
+#pragma unroll
+                for (int k = 0; k < kRecFloats / 2; k++) cq[k] = nq[k];
+                if (v + 1 < va->V) {
+#pragma unroll
+                    for (int k = 0; k < kRecFloats / 2; k++) nq[k] = rp[(size_t)(v + 1) * vstride + k];
+                }
+                const GaccRec rec{nullptr, (int)cq[4].y, cq};
                 SmallGrads gv;
                 gauss_bwd_one<DEG, true>(a, va->cams[v], idx, rec, row, grow, v > 0, gv);
 #pragma unroll
