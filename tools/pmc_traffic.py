@@ -120,12 +120,45 @@ def _inst_mix(dirname):
     return res
 
 
+def _trans(dirname):
+    """Per kernel, time-weighted over launches: VALU issue fraction with transcendentals priced at
+    twice a plain VALU op (MI355X_MICROARCH.md constants: v_exp / v_rcp / v_sqrt 8 cycles vs
+    v_fma 4 for one wave's stream), (2 (VALU - TRANS) + 4 TRANS) cycles / (duration x SIMDs x clock),
+    and the transcendental share of the VALU instructions."""
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
+    acc = {}
+    for fn in files:
+        per = {}
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                st = _stage(row.get("Kernel_Name", ""))
+                if st is None:
+                    continue
+                d = per.setdefault((st, row.get("Dispatch_Id")), {"dur": None})
+                d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                if row.get("End_Timestamp") and row.get("Start_Timestamp"):
+                    d["dur"] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+        for (st, _), d in per.items():
+            if not d.get("dur") or "SQ_INSTS_VALU" not in d or "SQ_INSTS_VALU_TRANS_F32" not in d:
+                continue
+            r = acc.setdefault(st, [0.0, 0.0, 0.0, 0.0])
+            v, t = d["SQ_INSTS_VALU"], d["SQ_INSTS_VALU_TRANS_F32"]
+            r[0] += 2.0 * (v - t) + 4.0 * t
+            r[1] += d["dur"] * CLOCK_GHZ * SIMDS
+            r[2] += t
+            r[3] += v
+    return {st: {"valu_issue_frac_trans_weighted": round(r[0] / r[1], 4),
+                 "trans_share_of_valu": round(r[2] / r[3], 4) if r[3] else None}
+            for st, r in acc.items() if r[1] > 0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--sq-dir", default=None, help="a third pass with SQ_ACTIVE_INST_VALU (VALU busy)")
     ap.add_argument("--inst-dir", default=None, help="a pass with SQ_INSTS_VALU/SALU/LDS and SQ_WAVES")
+    ap.add_argument("--trans-dir", default=None, help="a pass with SQ_INSTS_VALU and SQ_INSTS_VALU_TRANS_F32")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
@@ -151,6 +184,11 @@ def main():
         out["inst_note"] = ("wave-level instruction counts per launch (SQ_INSTS_*); valu_issue_frac = "
                             f"SQ_INSTS_VALU x 2 cycles / (duration x 1024 SIMDs x {CLOCK_GHZ} GHz)")
         for st, v in _inst_mix(a.inst_dir).items():
+            out["kernels"].setdefault(st, {}).update(v)
+    if a.trans_dir:
+        out["trans_note"] = ("valu_issue_frac_trans_weighted = (2 x non-transcendental + 4 x transcendental "
+                             f"VALU wave instructions) cycles / (duration x 1024 SIMDs x {CLOCK_GHZ} GHz)")
+        for st, v in _trans(a.trans_dir).items():
             out["kernels"].setdefault(st, {}).update(v)
     with open(a.out, "w") as fo:
         json.dump(out, fo, indent=1)

@@ -19,6 +19,15 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_ACTIVE_INST_VALU --kernel-trace -d
     --output-format csv -- python3 tools/pmc_workload.py > "$OUT/sq.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --kernel-trace \
     -d "$OUT/pmc_inst" -o run --output-format csv -- python3 tools/pmc_workload.py > "$OUT/inst.log" 2>&1
+# transcendental VALU instructions (v_exp / v_rcp / v_sqrt issue at twice a v_fma's cost), so the
+# issue fraction of the blends can price them; optional: a counter this ROCm does not know fails fast
+TRANS=""
+if timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES --kernel-trace \
+    -d "$OUT/pmc_trans" -o run --output-format csv -- python3 tools/pmc_workload.py > "$OUT/trans.log" 2>&1; then
+  TRANS="--trans-dir $OUT/pmc_trans"
+else
+  echo "transcendental counter pass failed (see $OUT/trans.log)"
+fi
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --sq-dir "$OUT/pmc_sq" --inst-dir "$OUT/pmc_inst" \
-    --out "$OUT/pmc_traffic.json" > /dev/null
+    $TRANS --out "$OUT/pmc_traffic.json" > /dev/null
 echo "profile passes done: $OUT"
