@@ -181,8 +181,15 @@ __device__ __forceinline__ void block_sum2_u64(unsigned long long& x, unsigned l
     y = s[4] + s[5] + s[6] + s[7];
 }
 
+// n_dev (may be null): only the first min(P, *n_dev) items are read, the rest count as {0, 0}
+// (the depth sort that dropped the culled Gaussians leaves its output past its count unwritten)
+__device__ __forceinline__ int scan_len(int P, const uint32_t* n_dev) {
+    return n_dev ? (int)min((uint32_t)P, *n_dev) : P;
+}
+
 __global__ __launch_bounds__(256) void k_pair_scan_totals(const uint2* __restrict__ in, int P,
-                                                          ulonglong2* __restrict__ tot) {
+                                                          ulonglong2* __restrict__ tot, const uint32_t* n_dev) {
+    P = scan_len(P, n_dev);
     __shared__ unsigned long long s[8];
     const size_t b0 = (size_t)blockIdx.x * kPairScanItems;
     unsigned long long x = 0, y = 0;
@@ -255,15 +262,16 @@ __global__ __launch_bounds__(256) void k_pair_scan_prefix(ulonglong2* __restrict
 // otherwise it holds block b's own total and every block sums those of the blocks before it.
 template <bool PREFIX>
 __global__ __launch_bounds__(256) void k_pair_scan(const uint2* __restrict__ in, uint2* __restrict__ out, int P,
-                                                   const ulonglong2* __restrict__ tot) {
+                                                   const ulonglong2* __restrict__ tot, const uint32_t* n_dev) {
     constexpr int IPT = kPairScanItems / 256;  // 8 consecutive items per thread
+    const int n = scan_len(P, n_dev);  // items read; all P are written
     __shared__ unsigned long long s[8];
     __shared__ unsigned long long s_wx[4], s_wy[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const size_t i0 = (size_t)blockIdx.x * kPairScanItems + (size_t)t * IPT;
     // this thread's items: four 16-B loads (two items each) when the run is in range
     uint2 v[IPT];
-    if (i0 + IPT <= (size_t)P) {
+    if (i0 + IPT <= (size_t)n) {
         const uint4* p = reinterpret_cast<const uint4*>(in + i0);
 #pragma unroll
         for (int k = 0; k < IPT / 2; k++) {
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(256) void k_pair_scan(const uint2* __restrict__ in,
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < IPT; k++) v[k] = i0 + k < (size_t)P ? in[i0 + k] : make_uint2(0u, 0u);
+        for (int k = 0; k < IPT; k++) v[k] = i0 + k < (size_t)n ? in[i0 + k] : make_uint2(0u, 0u);
     }
     // sum of the totals of all earlier blocks
     unsigned long long bx = 0, by = 0;
@@ -344,16 +352,16 @@ int g_pair_scan_direct = kPairScanDirectBlocks;
 }
 void set_pair_scan_direct_blocks(int nb) { g_pair_scan_direct = nb >= 0 ? nb : kPairScanDirectBlocks; }
 
-void launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_t st) {
+void launch_pair_scan(const uint2* in, uint2* out, int P, const uint32_t* n_dev, void* temp, hipStream_t st) {
     if (P <= 0) return;
     const int nb = (P + kPairScanItems - 1) / kPairScanItems;
     ulonglong2* tot = static_cast<ulonglong2*>(temp);
-    k_pair_scan_totals<<<nb, 256, 0, st>>>(in, P, tot);
+    k_pair_scan_totals<<<nb, 256, 0, st>>>(in, P, tot, n_dev);
     if (nb <= g_pair_scan_direct) {
-        k_pair_scan<false><<<nb, 256, 0, st>>>(in, out, P, tot);
+        k_pair_scan<false><<<nb, 256, 0, st>>>(in, out, P, tot, n_dev);
     } else {
         k_pair_scan_prefix<<<1, 256, 0, st>>>(tot, nb);
-        k_pair_scan<true><<<nb, 256, 0, st>>>(in, out, P, tot);
+        k_pair_scan<true><<<nb, 256, 0, st>>>(in, out, P, tot, n_dev);
     }
 }
 

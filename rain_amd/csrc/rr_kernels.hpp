@@ -180,7 +180,7 @@ void launch_preprocess(const PreArgs& a, hipStream_t st);
 constexpr int kPairScanItems = 2048;                 // items per block (256 threads x 8)
 constexpr int kPairScanDirectBlocks = 512;
 size_t pair_scan_temp_bytes(int P);
-void launch_pair_scan(const uint2* in, uint2* out, int P, void* temp, hipStream_t st);
+void launch_pair_scan(const uint2* in, uint2* out, int P, const uint32_t* n_dev, void* temp, hipStream_t st);
 void set_pair_scan_direct_blocks(int nb);
 template <typename K>
 struct DupArgs {
@@ -250,12 +250,16 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
                             const uint32_t* n_dev = nullptr, const uint2* gather_src = nullptr,
-                            uint2* gather_dst = nullptr, const struct PublishJob* publish = nullptr);
+                            uint2* gather_dst = nullptr, const struct PublishJob* publish = nullptr,
+                            uint32_t* kept = nullptr);
 // publish (optional, needs !first_counts_ready): one extra workgroup of the first count launch
 // runs the pair-count publish (rr_api.hip pair_counts_publish) beside the counting instead of a
 // launch of its own between the preprocess and the sort.
 // gather_src / gather_dst (optional): the last pass also writes gather_dst[i] = gather_src[vals_out[i]]
 // (the depth sort hands the scan its {pairs, rect} in depth order, a contiguous array).
+// kept (optional, a device word; not with unit_len / n_dev): the first pass drops every item whose
+// key is all ones (the preprocess's culled Gaussians) and writes the number it kept to *kept; the
+// later passes sort only those, and the output past *kept is left unwritten.
 const char* radix_sort_last_error();
 void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
 void set_sort_min_units_tile(int units);  // the same for the bin sorts (<= 16-bit keys; default 1024)

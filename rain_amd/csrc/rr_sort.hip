@@ -60,7 +60,7 @@ template <typename K, int MAXR, int DB>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ keys, size_t n, int shift, int dbits,
                                                           int rounds, uint32_t* __restrict__ counts, int units,
                                                           const uint32_t* __restrict__ n_dev, PublishJob pub,
-                                                          int has_pub) {
+                                                          int has_pub, int drop_ones) {
     static_assert(64 * kWaves == 256, "publish_pair_counts_block runs on 256 threads");
     if (has_pub && (int)blockIdx.x == units) {  // the extra workgroup (block-uniform)
         publish_pair_counts_block(pub);
@@ -79,7 +79,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ 
 #pragma unroll
     for (int r = 0; r < MAXR; r++) {  // all loads in flight before the first LDS atomic
         const uint32_t li = (uint32_t)r * 64 * kWaves + t;
-        dr[r] = (r < rounds && li < len) ? (((uint32_t)keys[base + li] >> shift) & mask) : 0xffffffffu;
+        const K k = (r < rounds && li < len) ? keys[base + li] : (K)~(K)0;
+        dr[r] = (r < rounds && li < len && !(drop_ones && k == (K)~(K)0)) ? (((uint32_t)k >> shift) & mask)
+                                                                             : 0xffffffffu;
     }
     __syncthreads();
 #pragma unroll
@@ -168,7 +170,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
                                                             const uint32_t* __restrict__ unit_len,
                                                             const uint32_t* __restrict__ n_dev,
                                                             const uint2* __restrict__ gather_src,
-                                                            uint2* __restrict__ gather_dst) {
+                                                            uint2* __restrict__ gather_dst, int drop_ones,
+                                                            uint32_t* __restrict__ kept) {
     constexpr int ND = 1 << DB;  // digits the kernel is compiled for (>= 1 << dbits)
     constexpr int DPL = ND / 64;  // digits per lane in the digit scans
     __shared__ uint32_t dbase[ND];         // first output slot of each digit
@@ -177,6 +180,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     __shared__ uint32_t goff[ND];          // global slot of block-local position 0 of each digit's run
     __shared__ uint32_t s_val[64 * kWaves * MAXR];
     __shared__ K s_key[64 * kWaves * MAXR];
+    __shared__ uint32_t s_nu;  // items staged (len minus the dropped ones)
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int ndig = 1 << dbits;
     const uint32_t mask = (uint32_t)ndig - 1u;
@@ -210,6 +214,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
             dbase[DPL * lane + i] = run;
             run += tv[i];
         }
+        if (kept && unit == 0 && lane == 63) kept[0] = run;  // every digit's total: the items kept
     }
     // the wave's items go to registers once (all loads in flight together); counting, ranking
     // and staging then run from registers
@@ -219,13 +224,17 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     for (int r = 0; r < MAXR; r++) {
         const size_t i = wbase + (size_t)r * 64 + lane;
         const bool valid = r < rounds && wl + (uint32_t)r * 64 + lane < len;
-        kr[r] = valid ? keys_in[i] : (K)0;
+        kr[r] = valid ? keys_in[i] : (K)~(K)0;
         vr[r] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
     }
+    // an item takes part when it is in range and (drop_ones) its key is not all ones
+    auto live = [&](int r) {
+        return r < rounds && wl + (uint32_t)r * 64 + lane < len && !(drop_ones && kr[r] == (K)~(K)0);
+    };
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < MAXR; r++) {
-        if (r < rounds && wl + (uint32_t)r * 64 + lane < len) atomicAdd(&wcnt[w][((uint32_t)kr[r] >> shift) & mask], 1u);
+        if (live(r)) atomicAdd(&wcnt[w][((uint32_t)kr[r] >> shift) & mask], 1u);
     }
     __syncthreads();
     // block-local starts: digits in order, then waves in order inside each digit.  Wave 0 scans the
@@ -264,13 +273,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
             }
             run += tot[i];
         }
+        if (lane == 63) s_nu = run;
     }
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < MAXR; r++) {
         if (r >= rounds || wl + (uint32_t)r * 64 >= len) continue;  // wave-uniform; keeps the loop unrollable
-        const bool valid = wl + (uint32_t)r * 64 + lane < len;
+        const bool valid = live(r);
         const K k = kr[r];
         const uint32_t v = vr[r];
         const uint32_t d = ((uint32_t)k >> shift) & mask;
@@ -291,7 +301,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
         }
     }
     __syncthreads();
-    const int nu = (int)len;
+    const int nu = (int)s_nu;
     for (int j = t; j < nu; j += 64 * kWaves) {
         const K k = s_key[j];
         const uint32_t d = ((uint32_t)k >> shift) & mask;
@@ -389,13 +399,15 @@ template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev,
-                            const uint2* gather_src, uint2* gather_dst, const PublishJob* publish) {
+                            const uint2* gather_src, uint2* gather_dst, const PublishJob* publish, uint32_t* kept) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
     g_why = "";
     if (n > 0xffffffffull || bits <= 0 || bits > (int)(8 * sizeof(K))) return g_why = "bad size/bits", hipErrorInvalidValue;
     if (unit_len && !n_dev) return g_why = "sparse units without n_dev", hipErrorInvalidValue;
     if (publish && first_counts_ready) return g_why = "publish rides on the first count launch", hipErrorInvalidValue;
+    if (kept && (unit_len || n_dev || first_counts_ready))
+        return g_why = "dropping all-ones keys needs a dense first pass", hipErrorInvalidValue;
     const SortLayout s = sort_layout<K>(temp, n, bits);
     if (temp_bytes < s.total) return g_why = "temp too small", hipErrorInvalidValue;
     const int passes = sort_passes(bits);
@@ -424,8 +436,10 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                                       : rounds <= 8 ? k_rs_count<K, 8, 8>
                                                     : k_rs_count<K, kMaxRounds, 8>);
             const bool pub = p == 0 && publish;
-            count<<<units + (pub ? 1 : 0), 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev,
-                                                                 pub ? *publish : PublishJob{}, pub ? 1 : 0);
+            const uint32_t* nd = p > 0 && kept ? kept : n_dev;
+            count<<<units + (pub ? 1 : 0), 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, nd,
+                                                                 pub ? *publish : PublishJob{}, pub ? 1 : 0,
+                                                                 p == 0 && kept ? 1 : 0);
         }
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
         auto scatter = dbits > 8 ? (rounds <= 2   ? k_rs_scatter<K, 2, 9>
@@ -437,8 +451,9 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                                     : rounds <= 8 ? k_rs_scatter<K, 8, 8>
                                                   : k_rs_scatter<K, kMaxRounds, 8>);
         scatter<<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets, units,
-                                               s.totals, p == 0 ? unit_len : nullptr, n_dev,
-                                               last ? gather_src : nullptr, last ? gather_dst : nullptr);
+                                               s.totals, p == 0 ? unit_len : nullptr, p > 0 && kept ? kept : n_dev,
+                                               last ? gather_src : nullptr, last ? gather_dst : nullptr,
+                                               p == 0 && kept ? 1 : 0, p == 0 ? kept : nullptr);
         ksrc = kdst;
         vsrc = vdst;
         shift += dbits;
@@ -452,10 +467,10 @@ template size_t radix_sort_temp_bytes<uint16_t>(size_t, int);
 template size_t radix_sort_temp_bytes<uint32_t>(size_t, int);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, const uint2*, uint2*, const PublishJob*);
+                                               const uint32_t*, const uint2*, uint2*, const PublishJob*, uint32_t*);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, const uint2*, uint2*, const PublishJob*);
+                                               const uint32_t*, const uint2*, uint2*, const PublishJob*, uint32_t*);
 template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int);
 template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int);
 
