@@ -361,6 +361,10 @@ int rr_debug_set_fwd_trace(void* dev_buf);
 int rr_set_binning_config(int split_denominator, int min_pairs);
 int rr_profile_collect(double* ms, int64_t* counts);
 const char* rr_stage_name(int stage);
+/* Diagnostics: host time this thread spent waiting for forwards' pair counts (the one device->host
+ * read per frame) since the last reset, in ns, and the number of waits; reset != 0 clears both
+ * after reading.  Near zero per frame means the host, not the device, paces the loop. */
+int rr_host_wait_stats(int reset, int64_t* wait_ns, int64_t* waits);
 
 #ifdef __cplusplus
 }

@@ -90,7 +90,7 @@ RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr
                   "rr_forward_geometry", "rr_forward_render", "rr_forward_render_aux", "rr_forward", "rr_backward", "rr_mark_visible", "rr_last_error",
                   "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
                   "rr_set_binning_config", "rr_set_tuning", "rr_debug_set_fwd_trace", "rr_profile_enable",
-                  "rr_profile_select", "rr_profile_collect", "rr_stage_name", "rr_geometry_layout",
+                  "rr_profile_select", "rr_profile_collect", "rr_stage_name", "rr_host_wait_stats", "rr_geometry_layout",
                   "rr_preprocess_rows", "rr_forward_from_geometry", "rr_forward_render_geometry",
                   "rr_backward_records", "rr_gauss_backward_views"]
 
@@ -141,6 +141,8 @@ def raster():
         L.rr_debug_get_views.argtypes = [fp, vp, vp, vp, ci, ctypes.POINTER(RRDebugViews)]
         L.rr_set_blend_config.restype = ci
         L.rr_set_blend_config.argtypes = [ci, ci]
+        L.rr_host_wait_stats.restype = ci
+        L.rr_host_wait_stats.argtypes = [ci, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         L.rr_profile_enable.restype = ci
         L.rr_profile_enable.argtypes = [ci]
         L.rr_set_tuning.restype = ci

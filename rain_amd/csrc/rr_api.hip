@@ -4,6 +4,7 @@
 // Replaces CudaRasterizer::Rasterizer::{forward,backward,markVisible}
 // (rasterizer_impl.cu:130-142,187-430) and the pybind wrappers (rasterize_points.cu:24-212).
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -349,7 +350,17 @@ hipError_t pair_counts_copy(const unsigned long long* src, uint2* out, bool* wid
     return e;
 }
 
+thread_local int64_t g_wait_ns = 0, g_waits = 0;
+struct WaitClock {  // adds the scope's duration to the host-wait statistics
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~WaitClock() {
+        g_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        g_waits++;
+    }
+};
+
 hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, bool* wide, hipStream_t st) {
+    WaitClock clock;
     Mailbox& mb = g_mailbox;
     if (r.seq == 0) return pair_counts_copy(r.copy, out, wide, st);
     for (uint32_t spin = 1;; spin++) {
@@ -1013,6 +1024,13 @@ int rr_profile_enable(int enable) {
 
 int rr_profile_select(unsigned stage_mask) {
     g_prof_mask = stage_mask;
+    return RR_OK;
+}
+
+int rr_host_wait_stats(int reset, int64_t* wait_ns, int64_t* waits) {
+    if (wait_ns) *wait_ns = g_wait_ns;
+    if (waits) *waits = g_waits;
+    if (reset) g_wait_ns = g_waits = 0;
     return RR_OK;
 }
 

@@ -58,6 +58,9 @@ def main():
         tr.step(it)
         it += 1
     torch.cuda.synchronize()
+    import ctypes
+    wn, wc = ctypes.c_int64(0), ctypes.c_int64(0)
+    _native.raster().rr_host_wait_stats(1, ctypes.byref(wn), ctypes.byref(wc))
     pr = cProfile.Profile()
     t0 = time.perf_counter()
     if not a.no_cprofile:
@@ -68,7 +71,9 @@ def main():
     pr.disable()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    print(f"lib {a.raster_lib} split {a.binning_split} ms/step {1e3 * (t1 - t0) / a.steps:.3f}")
+    _native.raster().rr_host_wait_stats(1, ctypes.byref(wn), ctypes.byref(wc))
+    print(f"lib {a.raster_lib} split {a.binning_split} ms/step {1e3 * (t1 - t0) / a.steps:.3f}  "
+          f"host wait for the pair counts {wn.value / 1e3 / max(wc.value, 1):.1f} us per frame ({wc.value} waits)")
     if a.no_cprofile:
         return
     s = io.StringIO()
