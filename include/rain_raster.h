@@ -245,6 +245,12 @@ int rr_geometry_layout(int P, size_t* offsets);
  * padding.  Outputs are the caller's arrays of n_rows entries (block sums: n_rows/256). */
 int rr_preprocess_rows(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int n_rows, int* radii,
                        void* splats, void* tiles, void* depth_keys, void* block_sums, void* block_wide, void* stream);
+/* rr_preprocess_rows for num_views views of the same rows in one launch: view v's camera from
+ * views[v] (the frame's width / height / tan_fov / low_pass are replaced by the view's), its arrays
+ * at out + v * view_stride + field_offsets[k] for k = radii, splats, tiles, depth keys, block
+ * sums, wide flags (the owner's send chunks of the Gaussian-sharded step). */
+int rr_preprocess_rows_views(const rr_frame* f, const rr_view* views, int num_views, const rr_gaussians* g,
+                             int n_rows, void* out, size_t view_stride, const size_t field_offsets[6], void* stream);
 /* rr_forward over a geometry buffer whose preprocess arrays are already filled (frame.P rows, a
  * multiple of 256; radii [P]); same outputs, same RR_INCOMPLETE / binning_needed protocol, with
  * rr_forward_render_geometry as the second stage. */

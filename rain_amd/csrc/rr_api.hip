@@ -820,6 +820,61 @@ int rr_preprocess_rows(const rr_frame* f, const rr_camera* cam, const rr_gaussia
     return RR_OK;
 }
 
+int rr_preprocess_rows_views(const rr_frame* f, const rr_view* views, int num_views, const rr_gaussians* g,
+                             int n_rows, void* out, size_t view_stride, const size_t field_offsets[6], void* stream) {
+    if (!f || !views || !g || !field_offsets) return fail(RR_ERR_ARG, "null argument");
+    if (num_views < 1 || num_views > RR_MAX_VIEWS) return fail(RR_ERR_ARG, "1 <= num_views <= RR_MAX_VIEWS");
+    if (n_rows < f->P || (n_rows % 256) != 0) return fail(RR_ERR_ARG, "n_rows must be >= P and a multiple of 256");
+    if (f->flags & RR_FLAG_AUX_NORMAL) return fail(RR_ERR_ARG, "row blocks carry no aux normals");
+    for (int v = 0; v < num_views; v++) {
+        const rr_view& w = views[v];
+        if (!w.viewmatrix || !w.projmatrix || !w.campos || w.width <= 0 || w.height <= 0)
+            return fail(RR_ERR_ARG, "bad view");
+    }
+    // the frame's own validation, with view 0 standing in for the camera (the preprocess reads no
+    // background)
+    const rr_camera cam0{views[0].viewmatrix, views[0].viewmatrix, views[0].projmatrix, views[0].campos};
+    int rc = validate(f, &cam0, g, true);
+    if (rc) return rc;
+    if (n_rows == 0) return RR_OK;
+    if (!out) return fail(RR_ERR_ARG, "null output buffer");
+    PreArgs a = pre_args(f, &cam0, g);
+    char* base = static_cast<char*>(out);
+    a.radii = reinterpret_cast<int*>(base + field_offsets[0]);
+    a.splats = reinterpret_cast<Splat*>(base + field_offsets[1]);
+    a.tiles = reinterpret_cast<uint2*>(base + field_offsets[2]);
+    a.depth_keys = reinterpret_cast<uint32_t*>(base + field_offsets[3]);
+    a.block_sums = reinterpret_cast<uint2*>(base + field_offsets[4]);
+    a.block_wide = reinterpret_cast<uint32_t*>(base + field_offsets[5]);
+    a.n_out = n_rows;
+    PreViews vs{};
+    vs.V = num_views;
+    vs.stride = view_stride;
+    for (int v = 0; v < num_views; v++) {
+        const rr_view& w = views[v];
+        PreView& c = vs.v[v];
+        c.view = w.viewmatrix;
+        c.proj = w.projmatrix;
+        c.campos = w.campos;
+        c.tanfovx = w.tan_fovx;
+        c.tanfovy = w.tan_fovy;
+        c.focal_x = w.width / (2.0f * w.tan_fovx);
+        c.focal_y = w.height / (2.0f * w.tan_fovy);
+        c.low_pass = w.low_pass;
+        c.W = w.width;
+        c.H = w.height;
+        c.gx = grid_x(w.width);
+        c.gy = grid_y(w.height);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    {
+        StageTimer tm(RR_STAGE_PREPROCESS, st);
+        launch_preprocess_views(a, vs, st);
+    }
+    RR_STAGE_CHECK("preprocess (rows, views)");
+    return RR_OK;
+}
+
 int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
                              size_t geom_bytes, void* image_buffer, size_t image_bytes, void* binning_buffer,
                              size_t binning_bytes, int* num_rendered, int* num_pairs, size_t* binning_needed,

@@ -27,8 +27,11 @@
 
 namespace rr {
 
-// OCC: minimum waves per SIMD requested from the register allocator (4 caps k_blend_bwd<1> at
-// 128 VGPRs, a few spills in the per-round flush; 1 = compiler's choice, 132 VGPRs / 3 waves).
+// OCC: minimum waves per SIMD requested from the register allocator.  The default 3 leaves the
+// compiler its 132 VGPRs without spills; 4 caps it at 128 with 96 B/lane of scratch in the
+// per-round flush (0.2446 / 0.2424 vs 0.2411 / 0.2413 ms/step in an interleaved A/B; a variant
+// that also read the next pair's record from LDS one pair ahead was neutral at 3 waves and slower
+// at 4: profiles/r03_blend_bwd_occupancy_ab.txt).
 template <int NW, int OCC>
 __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
     constexpr int PPL = 4 / NW;
@@ -345,9 +348,9 @@ void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
     const int nw = g_bwd_waves ? g_bwd_waves : env_waves("RAIN_BLEND_BWD_WAVES", kBwdWavesDefault);
     switch (nw) {
         case 2: k_blend_bwd<2, 1><<<T, 128, 0, st>>>(a); break;
-        case 3: k_blend_bwd<1, 1><<<T, 64, 0, st>>>(a); break;  // A/B variant: 1 wave, no occupancy cap
+        case 3: k_blend_bwd<1, 4><<<T, 64, 0, st>>>(a); break;  // A/B variant: 1 wave capped at 128 VGPRs
         case 4: k_blend_bwd<4, 1><<<T, 256, 0, st>>>(a); break;
-        default: k_blend_bwd<1, 4><<<T, 64, 0, st>>>(a); break;
+        default: k_blend_bwd<1, 3><<<T, 64, 0, st>>>(a); break;
     }
 }
 

@@ -126,7 +126,7 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx, bool&
 // contended 64-bit atomic per block measured +37 us on 1M Gaussians): the frame's pair count is
 // then known right after this kernel (rr_api.hip pair_counts_publish reduces them).
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
+__device__ __forceinline__ void preprocess_block(const PreArgs& a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     bool wide = false;
     uint2 c = make_uint2(0u, 0u);
@@ -158,6 +158,38 @@ __global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
                                               s_sum[0].y + s_sum[1].y + s_sum[2].y + s_sum[3].y);
         a.block_wide[blockIdx.x] = s_wide[0] | s_wide[1] | s_wide[2] | s_wide[3];
     }
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
+    preprocess_block<DEG>(a);
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void k_preprocess_views(PreArgs a, PreViews vs) {
+    const PreView& c = vs.v[blockIdx.y];
+    PreArgs b = a;
+    b.view = c.view;
+    b.proj = c.proj;
+    b.campos = c.campos;
+    b.tanfovx = c.tanfovx;
+    b.tanfovy = c.tanfovy;
+    b.focal_x = c.focal_x;
+    b.focal_y = c.focal_y;
+    b.low_pass = c.low_pass;
+    b.W = c.W;
+    b.H = c.H;
+    b.gx = c.gx;
+    b.gy = c.gy;
+    const size_t off = (size_t)blockIdx.y * vs.stride;
+    auto at = [&](auto* p) { return reinterpret_cast<decltype(p)>(reinterpret_cast<char*>(p) + off); };
+    b.radii = at(a.radii);
+    b.splats = at(a.splats);
+    b.tiles = at(a.tiles);
+    b.depth_keys = at(a.depth_keys);
+    b.block_sums = at(a.block_sums);
+    b.block_wide = at(a.block_wide);
+    preprocess_block<DEG>(b);
 }
 
 // ---- scan of the pair counts in depth order (replaces a device-wide decoupled-look-back scan:
@@ -717,6 +749,18 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 // ---------------------------------------------------------------------------------------
 // host launchers
 static inline int blocks_for(long n, int b = 256) { return (int)((n + b - 1) / b); }
+
+void launch_preprocess_views(const PreArgs& a, const PreViews& vs, hipStream_t st) {
+    const int rows = a.n_out > a.P ? a.n_out : a.P;
+    if (rows == 0 || vs.V <= 0) return;
+    const dim3 grid(blocks_for(rows), vs.V);
+    switch (a.colors_precomp ? 0 : a.D) {
+        case 0: k_preprocess_views<0><<<grid, 256, 0, st>>>(a, vs); break;
+        case 1: k_preprocess_views<1><<<grid, 256, 0, st>>>(a, vs); break;
+        case 2: k_preprocess_views<2><<<grid, 256, 0, st>>>(a, vs); break;
+        default: k_preprocess_views<3><<<grid, 256, 0, st>>>(a, vs); break;
+    }
+}
 
 void launch_preprocess(const PreArgs& a, hipStream_t st) {
     const int rows = a.n_out > a.P ? a.n_out : a.P;

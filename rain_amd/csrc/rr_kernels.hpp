@@ -171,6 +171,23 @@ struct GaussBwdArgs {
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);
+// One launch preprocessing the same rows for up to kMaxPreViews views (the Gaussian-sharded step's
+// owner preprocess): view v = blockIdx.y takes its camera from vs.v[v] and writes every output
+// array of PreArgs displaced by v * vs.stride bytes.
+constexpr int kMaxPreViews = 16;
+struct PreView {
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float tanfovx, tanfovy, focal_x, focal_y, low_pass;
+    int W, H, gx, gy;
+};
+struct PreViews {
+    PreView v[kMaxPreViews];
+    size_t stride;
+    int V;
+};
+void launch_preprocess_views(const PreArgs& a, const PreViews& vs, hipStream_t st);
 // Inclusive scan of the per-Gaussian {pairs, rect tiles} in depth order, saturating at 2^32 - 1
 // per component (rasterizer_impl.cu:269).  Per-block totals, then each block scans its items on
 // top of the sum of the earlier totals: up to kPairScanDirectBlocks blocks (P <= 1,048,576) every

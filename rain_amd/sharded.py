@@ -112,35 +112,12 @@ class ShardedStep:
         dev = model._xyz.device
         P = model._xyz.shape[0]
         Nw = self.world
-        Q, P_pad, lo, nv = self.layout(P)
+        Q, P_pad, _lo, _nv = self.layout(P)
         stream = N.stream_of(model._xyz)
         u8 = torch.uint8
 
-        # 1. owner preprocess of every view over the owned rows -> send buffer: one chunk per view,
-        #    [splat records Q x 48 B | pair counts Q x 8 | depth keys Q x 4 | radii Q x 4 |
-        #     block sums Q/256 x 8 | wide flags Q/256 x 4]
-        gs, M = self._row_params(model, lo)
-        nb = Q // 256
-        fields = ((SPLAT_BYTES, Q), (8, Q), (4, Q), (4, Q), (8, nb), (4, nb))
-        starts, c = [], 0
-        for w, n in fields:
-            starts.append(c)
-            c += w * n
-        chunk = c
-        send = self._buf("g_send", Nw * chunk, u8, dev)
-        keep = []
-        for v, cam in enumerate(cams):
-            fr = self._frame(model, nv, cam, low_pass, flags | N.RR_FLAG_RAW_PARAMS)
-            k = (bg.contiguous(), cam.world_view_transform.contiguous(), cam.full_proj_transform.contiguous(),
-                 cam.camera_center.contiguous())
-            keep.append(k)
-            rc = N.RRCamera(*[_p(t) for t in k])
-            b = v * chunk
-            N.check(L.rr_preprocess_rows(ctypes.byref(fr), ctypes.byref(rc), ctypes.byref(gs), Q,
-                                         _p(send, b + starts[3]), _p(send, b + starts[0]), _p(send, b + starts[1]),
-                                         _p(send, b + starts[2]), _p(send, b + starts[4]), _p(send, b + starts[5]),
-                                         stream),
-                    "sharded preprocess")
+        # 1. owner preprocess of every view over the owned rows -> send buffer, one chunk per view
+        send, chunk, fields, starts, keep = self.preprocess_views(model, cams, bg, low_pass, flags)
 
         # 2. one all-to-all: chunk i of recv = rank i's rows for this rank's view; then each field
         #    into its array of the geometry buffer (rows in global order)
@@ -190,6 +167,40 @@ class ShardedStep:
 
         self.exchange_and_own(model, cams, keep, recs, low_pass, adam, stats)
         return color, loss
+
+    def preprocess_views(self, model, cams, bg, low_pass, flags):
+        """Step 1: the owner's rows preprocessed for each of the step's views into the send buffer,
+        one chunk per view: [splat records Q x 48 B | pair counts Q x 8 | depth keys Q x 4 |
+        radii Q x 4 | block sums Q/256 x 8 | wide flags Q/256 x 4].  Returns (send, chunk bytes,
+        fields, field starts, keep = per-view (bg, view, proj, campos) tensors)."""
+        L = N.raster()
+        dev = model._xyz.device
+        P = model._xyz.shape[0]
+        Nw = self.world
+        Q, _P_pad, lo, nv = self.layout(P)
+        stream = N.stream_of(model._xyz)
+        gs, _M = self._row_params(model, lo)
+        nb = Q // 256
+        fields = ((SPLAT_BYTES, Q), (8, Q), (4, Q), (4, Q), (8, nb), (4, nb))
+        starts, c = [], 0
+        for w, n in fields:
+            starts.append(c)
+            c += w * n
+        chunk = c
+        send = self._buf("g_send", Nw * chunk, torch.uint8, dev)
+        keep = [(bg.contiguous(), cam.world_view_transform.contiguous(), cam.full_proj_transform.contiguous(),
+                 cam.camera_center.contiguous()) for cam in cams]
+        # every view in one launch (rr_preprocess_rows_views): view v's chunk at v * chunk
+        views = (N.RRView * Nw)()
+        for v, (cam, k) in enumerate(zip(cams, keep)):
+            views[v] = N.RRView(_p(k[1]), _p(k[2]), _p(k[3]), math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5),
+                                float(low_pass), int(cam.image_width), int(cam.image_height))
+        fr = self._frame(model, nv, cams[0], low_pass, flags | N.RR_FLAG_RAW_PARAMS)
+        offs = (ctypes.c_size_t * 6)(starts[3], starts[0], starts[1], starts[2], starts[4], starts[5])
+        N.check(L.rr_preprocess_rows_views(ctypes.byref(fr), views, Nw, ctypes.byref(gs), Q, _p(send), chunk, offs,
+                                           stream),
+                "sharded preprocess")
+        return send, chunk, fields, starts, keep
 
     def exchange_and_own(self, model, cams, keep, recs, low_pass, adam, stats):
         """Steps 4-5 of step(): the record exchange and the owners' per-Gaussian backward + Adam.

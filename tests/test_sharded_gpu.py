@@ -97,3 +97,48 @@ def test_owner_chunking_is_bitwise_neutral():
     for other in results[1:]:
         for i, (a, b) in enumerate(zip(results[0], other)):
             assert torch.equal(a, b), f"state tensor {i} differs between chunkings"
+
+
+def test_multi_view_preprocess_equals_per_view():
+    """rr_preprocess_rows_views (every view of the owner's rows in one launch) writes the same
+    bytes as one rr_preprocess_rows call per view."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ctypes
+    import math
+
+    from rain_amd import _native as N
+    from rain_amd import cameras, synthetic
+    from rain_amd.diff_gaussian_rasterization import _C
+    from rain_amd.gaussian_model import GaussianModel
+    from rain_amd.sharded import ShardedStep, _p
+
+    dev = torch.device("cuda:0")
+    g = GaussianModel(3, divide_ratio=0.8, device=dev)
+    g.set_params(synthetic.random_gaussians(7000, sh_degree=3, seed=4, bench=True))
+    g.active_sh_degree = 3
+    world = 3
+    cams = [c.to(dev) for c in cameras.fibonacci_cameras(world, 200, 150)]
+    bg = torch.zeros(3, device=dev)
+    L = N.raster()
+    for rank in range(world):
+        sh = ShardedStep(None, rank, world)
+        send, chunk, fields, starts, keep = sh.preprocess_views(g, cams, bg, 0.3, _C.frame_flags())
+        send.fill_(0xAB)  # culled rows leave their splat records unwritten: same fill on both sides
+        send, chunk, fields, starts, keep = sh.preprocess_views(g, cams, bg, 0.3, _C.frame_flags())
+        got = send.clone()
+        Q, _P_pad, lo, nv = sh.layout(g._xyz.shape[0])
+        gs, _M = sh._row_params(g, lo)
+        ref = torch.full_like(send, 0xAB)
+        stream = N.stream_of(g._xyz)
+        for v, cam in enumerate(cams):
+            fr = sh._frame(g, nv, cam, 0.3, _C.frame_flags() | N.RR_FLAG_RAW_PARAMS)
+            rc = N.RRCamera(*[_p(t) for t in keep[v]])
+            b = v * chunk
+            N.check(L.rr_preprocess_rows(ctypes.byref(fr), ctypes.byref(rc), ctypes.byref(gs), Q,
+                                         _p(ref, b + starts[3]), _p(ref, b + starts[0]), _p(ref, b + starts[1]),
+                                         _p(ref, b + starts[2]), _p(ref, b + starts[4]), _p(ref, b + starts[5]),
+                                         stream), "per-view preprocess")
+        torch.cuda.synchronize()
+        assert math.isfinite(float(got.float().sum()))
+        assert torch.equal(got, ref), f"rank {rank}: multi-view preprocess differs"

@@ -60,7 +60,18 @@ def main():
                 sh.exchange_and_own(g, cams[:world], keep[:world], recs, 0.3, g.optimizer.fused_step(g), stats)
         br = _native.Profiler.collect()
         ms, cnt = br["gauss_bwd"]
-        out[f"N{world}"] = {"Q": Q, "owner_ms": round(ms / cnt, 4)}
+        # step 1 of the sharded step: the owner's rows preprocessed for each of the N views
+        from rain_amd.diff_gaussian_rasterization import _C
+        for _ in range(3):
+            sh.preprocess_views(g, cams[:world], bg, 0.3, _C.frame_flags())
+        torch.cuda.synchronize()
+        _native.Profiler.collect()
+        with _native.Profiler(["preprocess"]):
+            for _ in range(10):
+                sh.preprocess_views(g, cams[:world], bg, 0.3, _C.frame_flags())
+        pms, pcnt = _native.Profiler.collect()["preprocess"]
+        out[f"N{world}"] = {"Q": Q, "owner_ms": round(ms / cnt, 4), "preprocess_views_ms": round(pms / 10, 4),
+                            "preprocess_launches": int(pcnt // 10)}
     print(json.dumps(out), flush=True)
 
 
