@@ -160,13 +160,19 @@ __device__ __forceinline__ void preprocess_block(const PreArgs& a) {
     }
 }
 
+// 5 waves per SIMD: the SH-3 instance fits 88 VGPRs without spills (the compiler's own choice,
+// 98, gives 4; 6 waves spill 52 B/lane): preprocess 0.094 -> 0.090 ms/step in an interleaved A/B
+// (profiles/r03_preprocess_occupancy_ab.txt; 8 waves measured 0.129 vs 0.091 in round 2)
+#ifndef RR_PRE_OCC
+#define RR_PRE_OCC 5
+#endif
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess(PreArgs a) {
+__global__ __launch_bounds__(256, RR_PRE_OCC) void k_preprocess(PreArgs a) {
     preprocess_block<DEG>(a);
 }
 
 template <int DEG>
-__global__ __launch_bounds__(256) void k_preprocess_views(PreArgs a, PreViews vs) {
+__global__ __launch_bounds__(256, RR_PRE_OCC) void k_preprocess_views(PreArgs a, PreViews vs) {
     const PreView& c = vs.v[blockIdx.y];
     PreArgs b = a;
     b.view = c.view;
