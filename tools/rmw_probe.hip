@@ -131,6 +131,21 @@ __global__ __launch_bounds__(256) void k_rmw_mv(v4f* __restrict__ p, v4f* __rest
     q[0] = b;
     q[64] = d;
 }
+// ping-pong with p|m|v interleaved per 64-float4 chunk in both buffers: one read front, one write
+// front (the copy's pattern) instead of six
+__global__ __launch_bounds__(256) void k_pingpong_inter(const v4f* __restrict__ s, v4f* __restrict__ d, long n) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const long c = i >> 6, l = i & 63;
+    const v4f* q = s + c * 192 + l;
+    v4f* o = d + c * 192 + l;
+    v4f a = q[0], b = q[64], e = q[128];
+    b = b * 0.9f + a * 0.1f;
+    e = e * 0.999f + a * a * 0.001f;
+    o[0] = a - b * 1e-3f;
+    o[64] = b;
+    o[128] = e;
+}
 __global__ __launch_bounds__(256) void k_copy3(v4f* __restrict__ d, const v4f* __restrict__ s, long n) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
@@ -173,6 +188,14 @@ int main() {
     });
     run("rmw interleaved p|m|v", [&] { k_rmw_inter<<<(n + 255) / 256, 256>>>(p, n); });
     run("rmw p + interleaved m|v", [&] { k_rmw_mv<<<(n + 255) / 256, 256>>>(p, p + n, n); });
+    run("ping-pong interleaved", [&] { k_pingpong_inter<<<(n + 255) / 256, 256>>>(p, d, n); });
+    run("ping-pong interleaved alt", [&] {
+        static int k = 0;
+        v4f* a = (k & 1) ? d : p;
+        v4f* b = (k & 1) ? p : d;
+        k++;
+        k_pingpong_inter<<<(n + 255) / 256, 256>>>(a, b, n);
+    });
     run("copy nt (same bytes)", [&] { k_copy3<<<(3 * n + 255) / 256, 256>>>(d, p, 3 * n); });
     return 0;
 }

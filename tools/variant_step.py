@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--points", type=int, default=1_000_000)
     ap.add_argument("--api", action="store_true", help="also time the reference-API step (Trainer(fused=False))")
+    ap.add_argument("--pack", action="store_true", help="parameters and moments in three flat buffers (pack_flat_state)")
     a = ap.parse_args()
     import torch
 
@@ -47,6 +48,9 @@ def main():
     opt = OptimizationParams()
     g.training_setup(opt)
     tr = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(seed=0), scene_extent=4.4)
+    if a.pack:
+        g.optimizer.fused_step(g)  # creates the moment state the packing moves
+        g.pack_flat_state(1)
     it = 1001
     for _ in range(10):
         tr.step(it)
