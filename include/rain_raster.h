@@ -248,9 +248,19 @@ int rr_preprocess_rows(const rr_frame* f, const rr_camera* cam, const rr_gaussia
 /* rr_preprocess_rows for num_views views of the same rows in one launch: view v's camera from
  * views[v] (the frame's width / height / tan_fov / low_pass are replaced by the view's), its arrays
  * at out + v * view_stride + field_offsets[k] for k = radii, splats, tiles, depth keys, block
- * sums, wide flags (the owner's send chunks of the Gaussian-sharded step). */
+ * sums, wide flags (the owner's send chunks of the Gaussian-sharded step).  wire != 0: instead of
+ * the 48-B splat records and the depth keys, one 40-B wire record per row at field_offsets[1]
+ * (the 10 floats a splat record holds that cannot be recomputed; field_offsets[3] unused), which
+ * rr_unpack_rows turns back into the geometry arrays bitwise. */
 int rr_preprocess_rows_views(const rr_frame* f, const rr_view* views, int num_views, const rr_gaussians* g,
-                             int n_rows, void* out, size_t view_stride, const size_t field_offsets[6], void* stream);
+                             int n_rows, void* out, size_t view_stride, const size_t field_offsets[6], int wire,
+                             void* stream);
+/* The receiving side of the geometry all-to-all: world chunks of chunk_bytes at recv (chunk j =
+ * rank j's rows_per_rank rows in wire form, fields at field_offsets = wire records, tiles, radii,
+ * block sums, wide flags) into a geometry buffer of world * rows_per_rank rows (splat records,
+ * pair counts, depth keys, block sums at rr_geometry_layout's offsets) and radii[]. */
+int rr_unpack_rows(int world, int rows_per_rank, const void* recv, size_t chunk_bytes, const size_t field_offsets[5],
+                   void* geom_buffer, size_t geom_bytes, int* radii, void* stream);
 /* rr_forward over a geometry buffer whose preprocess arrays are already filled (frame.P rows, a
  * multiple of 256; radii [P]); same outputs, same RR_INCOMPLETE / binning_needed protocol, with
  * rr_forward_render_geometry as the second stage. */

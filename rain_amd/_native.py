@@ -91,7 +91,7 @@ RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr
                   "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
                   "rr_set_binning_config", "rr_set_tuning", "rr_debug_set_fwd_trace", "rr_profile_enable",
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name", "rr_host_wait_stats", "rr_geometry_layout",
-                  "rr_preprocess_rows", "rr_preprocess_rows_views", "rr_forward_from_geometry",
+                  "rr_preprocess_rows", "rr_preprocess_rows_views", "rr_unpack_rows", "rr_forward_from_geometry",
                   "rr_forward_render_geometry",
                   "rr_backward_records", "rr_gauss_backward_views"]
 
@@ -165,7 +165,9 @@ def raster():
         L.rr_preprocess_rows.argtypes = [fp, cp, gp, ci, vp, vp, vp, vp, vp, vp, vp]
         L.rr_preprocess_rows_views.restype = ci
         L.rr_preprocess_rows_views.argtypes = [fp, ctypes.POINTER(RRView), ci, gp, ci, vp, sz,
-                                               ctypes.POINTER(ctypes.c_size_t), vp]
+                                               ctypes.POINTER(ctypes.c_size_t), ci, vp]
+        L.rr_unpack_rows.restype = ci
+        L.rr_unpack_rows.argtypes = [ci, ci, vp, sz, ctypes.POINTER(ctypes.c_size_t), vp, sz, vp, vp]
         L.rr_forward_from_geometry.restype = ci
         L.rr_forward_from_geometry.argtypes = [fp, cp, vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(ci), ctypes.POINTER(ci),
                                                ctypes.POINTER(sz), vp, vp, vp]

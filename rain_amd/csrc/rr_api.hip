@@ -821,7 +821,8 @@ int rr_preprocess_rows(const rr_frame* f, const rr_camera* cam, const rr_gaussia
 }
 
 int rr_preprocess_rows_views(const rr_frame* f, const rr_view* views, int num_views, const rr_gaussians* g,
-                             int n_rows, void* out, size_t view_stride, const size_t field_offsets[6], void* stream) {
+                             int n_rows, void* out, size_t view_stride, const size_t field_offsets[6], int wire,
+                             void* stream) {
     if (!f || !views || !g || !field_offsets) return fail(RR_ERR_ARG, "null argument");
     if (num_views < 1 || num_views > RR_MAX_VIEWS) return fail(RR_ERR_ARG, "1 <= num_views <= RR_MAX_VIEWS");
     if (n_rows < f->P || (n_rows % 256) != 0) return fail(RR_ERR_ARG, "n_rows must be >= P and a multiple of 256");
@@ -841,9 +842,14 @@ int rr_preprocess_rows_views(const rr_frame* f, const rr_view* views, int num_vi
     PreArgs a = pre_args(f, &cam0, g);
     char* base = static_cast<char*>(out);
     a.radii = reinterpret_cast<int*>(base + field_offsets[0]);
-    a.splats = reinterpret_cast<Splat*>(base + field_offsets[1]);
+    if (wire) {  // 10-float wire records, no depth keys (rr_unpack_rows rebuilds both)
+        if ((field_offsets[1] | view_stride) & 7u) return fail(RR_ERR_ARG, "wire records need 8-B alignment");
+        a.wire = reinterpret_cast<float*>(base + field_offsets[1]);
+    } else {
+        a.splats = reinterpret_cast<Splat*>(base + field_offsets[1]);
+        a.depth_keys = reinterpret_cast<uint32_t*>(base + field_offsets[3]);
+    }
     a.tiles = reinterpret_cast<uint2*>(base + field_offsets[2]);
-    a.depth_keys = reinterpret_cast<uint32_t*>(base + field_offsets[3]);
     a.block_sums = reinterpret_cast<uint2*>(base + field_offsets[4]);
     a.block_wide = reinterpret_cast<uint32_t*>(base + field_offsets[5]);
     a.n_out = n_rows;
@@ -873,6 +879,24 @@ int rr_preprocess_rows_views(const rr_frame* f, const rr_view* views, int num_vi
     }
     RR_STAGE_CHECK("preprocess (rows, views)");
     return RR_OK;
+}
+
+int rr_unpack_rows(int world, int rows_per_rank, const void* recv, size_t chunk_bytes, const size_t field_offsets[5],
+                   void* geom_buffer, size_t geom_bytes, int* radii, void* stream) {
+    if (world < 1 || rows_per_rank < 0 || (rows_per_rank % 256) != 0)
+        return fail(RR_ERR_ARG, "world >= 1 and rows_per_rank a multiple of 256");
+    if (!field_offsets) return fail(RR_ERR_ARG, "null field offsets");
+    const int P = world * rows_per_rank;
+    if (P == 0) return RR_OK;
+    if (!recv || !geom_buffer || !radii) return fail(RR_ERR_ARG, "null buffer");
+    if ((chunk_bytes | field_offsets[0] | field_offsets[1]) & 7u)
+        return fail(RR_ERR_ARG, "chunks and wire / tile fields need 8-B alignment");
+    const Geom gm = carve_geom(geom_buffer, P);
+    if (geom_bytes < gm.total) return fail(RR_ERR_CAPACITY, "geometry buffer too small");
+    hipStream_t st = (hipStream_t)stream;
+    launch_unpack_rows(world, rows_per_rank, static_cast<const char*>(recv), chunk_bytes, field_offsets, gm.splats,
+                       gm.tiles, gm.depth_keys, radii, gm.block_sums, gm.block_wide, st);
+    return check(nullptr, st, "unpack rows");
 }
 
 int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,

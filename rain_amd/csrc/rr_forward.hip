@@ -24,7 +24,7 @@ template <int DEG>
 __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx, bool& wide) {
     a.radii[idx] = 0;
     a.tiles[idx] = make_uint2(0u, 0u);
-    a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
+    if (a.depth_keys) a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
 
     const v3 p = load3(a.means3D + 3 * (size_t)idx);
     // in_frustum (auxiliary.h:128-153)
@@ -94,11 +94,22 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx, bool&
         rgb = make_float4(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f), 0.f);
     }
     const float opacity = a.raw ? act_opacity(a.opacities[idx]) : a.opacities[idx];
+    float log2o, inv_o;
+    splat_derived(opacity, log2o, inv_o);
     Splat s;
     s.a = make_float4(px, py, kQHalf * cx, kQFull * cy);
-    s.b = make_float4(kQHalf * cz, __builtin_amdgcn_logf(opacity), p_view.z, opacity);
-    s.c = make_float4(rgb.x, rgb.y, rgb.z, opacity > 0.f ? 1.0f / opacity : 0.f);
-    a.splats[idx] = s;
+    s.b = make_float4(kQHalf * cz, log2o, p_view.z, opacity);
+    s.c = make_float4(rgb.x, rgb.y, rgb.z, inv_o);
+    if (a.wire) {
+        float2* w = reinterpret_cast<float2*>(a.wire + (size_t)kWireFloats * idx);
+        w[0] = make_float2(s.a.x, s.a.y);
+        w[1] = make_float2(s.a.z, s.a.w);
+        w[2] = make_float2(s.b.x, s.b.z);
+        w[3] = make_float2(s.b.w, s.c.x);
+        w[4] = make_float2(s.c.y, s.c.z);
+    } else {
+        a.splats[idx] = s;
+    }
     if (a.normals) a.normals[idx] = gaussian_normal(sc, q, a.view, p_view);
     a.radii[idx] = radius;
     // (bin, Gaussian) pairs: bins (2 x 2 tiles, rr_common.hpp) holding a tile the Gaussian reaches
@@ -117,7 +128,7 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx, bool&
     a.tiles[idx] = make_uint2(n, (uint32_t)area);
     // > 0.2, so the bit pattern orders like the value, and so does its offset from kDepthKeyBase
     const uint32_t key = __float_as_uint(p_view.z) - kDepthKeyBase;
-    a.depth_keys[idx] = key;
+    if (a.depth_keys) a.depth_keys[idx] = key;
     wide = key >= (1u << kDepthKeyBits);
     return make_uint2(n, (uint32_t)area);
 }
@@ -135,7 +146,7 @@ __device__ __forceinline__ void preprocess_block(const PreArgs& a) {
     } else if (idx < a.n_out) {  // padding row of a row block: culled
         a.radii[idx] = 0;
         a.tiles[idx] = make_uint2(0u, 0u);
-        a.depth_keys[idx] = 0xffffffffu;
+        if (a.depth_keys) a.depth_keys[idx] = 0xffffffffu;
     }
     if (!a.block_sums) return;
     __shared__ uint2 s_sum[4];
@@ -192,10 +203,53 @@ __global__ __launch_bounds__(256, RR_PRE_OCC) void k_preprocess_views(PreArgs a,
     b.radii = at(a.radii);
     b.splats = at(a.splats);
     b.tiles = at(a.tiles);
-    b.depth_keys = at(a.depth_keys);
+    b.depth_keys = a.depth_keys ? at(a.depth_keys) : nullptr;
     b.block_sums = at(a.block_sums);
     b.block_wide = at(a.block_wide);
+    b.wire = a.wire ? at(a.wire) : nullptr;
     preprocess_block<DEG>(b);
+}
+
+// The receiving side of the sharded step's geometry exchange: rows of `world` chunks (chunk j =
+// rank j's rows, wire format) into the geometry arrays in global row order, splats rebuilt with
+// splat_derived, depth keys from the depth (0xffffffff for a culled row, radius 0).
+__global__ __launch_bounds__(256) void k_unpack_rows(int world, int Q, const char* __restrict__ recv, size_t chunk,
+                                                     size_t o_wire, size_t o_tiles, size_t o_radii, size_t o_bsum,
+                                                     size_t o_bwide, Splat* __restrict__ splats,
+                                                     uint2* __restrict__ tiles, uint32_t* __restrict__ keys,
+                                                     int* __restrict__ radii, uint2* __restrict__ bsum,
+                                                     uint32_t* __restrict__ bwide) {
+    const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= (size_t)world * Q) return;
+    const int j = (int)(g / (size_t)Q), r = (int)(g - (size_t)j * Q);
+    const char* c = recv + (size_t)j * chunk;
+    const float2* w = reinterpret_cast<const float2*>(c + o_wire) + (size_t)(kWireFloats / 2) * r;
+    const int radius = reinterpret_cast<const int*>(c + o_radii)[r];
+    tiles[g] = reinterpret_cast<const uint2*>(c + o_tiles)[r];
+    radii[g] = radius;
+    const float2 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+    float log2o, inv_o;
+    splat_derived(w3.x, log2o, inv_o);
+    Splat s;
+    s.a = make_float4(w0.x, w0.y, w1.x, w1.y);
+    s.b = make_float4(w2.x, log2o, w2.y, w3.x);
+    s.c = make_float4(w3.y, w4.x, w4.y, inv_o);
+    splats[g] = s;
+    keys[g] = radius > 0 ? __float_as_uint(w2.y) - kDepthKeyBase : 0xffffffffu;
+    if ((r & 255) == 0) {  // Q is a multiple of 256: rank j's block b is global block g / 256
+        bsum[g / 256] = reinterpret_cast<const uint2*>(c + o_bsum)[r / 256];
+        bwide[g / 256] = reinterpret_cast<const uint32_t*>(c + o_bwide)[r / 256];
+    }
+}
+
+void launch_unpack_rows(int world, int rows_per_rank, const char* recv, size_t chunk_bytes,
+                        const size_t field_offsets[5], Splat* splats, uint2* tiles, uint32_t* depth_keys, int* radii,
+                        uint2* block_sums, uint32_t* block_wide, hipStream_t st) {
+    const size_t n = (size_t)world * rows_per_rank;
+    if (n == 0) return;
+    k_unpack_rows<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+        world, rows_per_rank, recv, chunk_bytes, field_offsets[0], field_offsets[1], field_offsets[2],
+        field_offsets[3], field_offsets[4], splats, tiles, depth_keys, radii, block_sums, block_wide);
 }
 
 // ---- scan of the pair counts in depth order (replaces a device-wide decoupled-look-back scan:

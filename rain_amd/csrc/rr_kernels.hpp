@@ -81,7 +81,22 @@ struct PreArgs {
     uint32_t* block_wide;        // with block_sums: per block, 1 if a visible depth key needs > kDepthKeyBits
     int n_out;                   // rows written (>= P): rows P..n_out-1 get the culled outputs (radius 0,
                                  // no pairs, the largest depth key) — the padding rows of a row block
+    float* wire;                 // optional (the sharded step's send chunks): per row the 10-float
+                                 // wire record (splat_to_wire) instead of splats[] and depth_keys[]
 };
+
+// The sharded step's wire record of a splat: the 10 floats Splat holds that cannot be recomputed
+// (x, y, qa, qb, qc, depth, o, r, g, b); log2 o, 1/o and the depth key are rebuilt by the
+// receiver with the preprocess's own expressions (splat_derived), so the unpacked geometry is
+// bitwise the preprocess's.
+__device__ __forceinline__ void splat_derived(float o, float& log2o, float& inv_o) {
+    log2o = __builtin_amdgcn_logf(o);
+    inv_o = o > 0.f ? 1.0f / o : 0.f;
+}
+constexpr int kWireFloats = 10;
+void launch_unpack_rows(int world, int rows_per_rank, const char* recv, size_t chunk_bytes,
+                        const size_t field_offsets[5], Splat* splats, uint2* tiles, uint32_t* depth_keys, int* radii,
+                        uint2* block_sums, uint32_t* block_wide, hipStream_t st);
 
 // Depth keys: the float bits of the view depth minus those of the smallest float above the near
 // plane (0.2f = 0x3E4CCCCD), so the keys of depths up to ~13107 fit 27 bits and the depth sort runs

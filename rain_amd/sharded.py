@@ -8,11 +8,13 @@ design (every rank holds every parameter, reduce-scatter the 236 MB of gradients
 cross the links are per-(Gaussian, view) records instead:
 
   rank r owns the Gaussian rows [r*Q, (r+1)*Q) (Q: ceil(P/N) rounded up to 256):
-  1. owner preprocess: for each of the step's N views, its rows' splat records (48 B), pair
-     counts, depth keys, radii and per-256-row block sums (rr_preprocess_rows), ~64 B per row;
+  1. owner preprocess: for each of the step's N views (one launch, rr_preprocess_rows_views), its
+     rows' 40-B wire records (the splat's 10 non-derived floats), pair counts, radii and
+     per-256-row block sums, 52 B per row;
   2. all-to-all (RCCL over xGMI, every pair of GPUs on its own link): rank v receives view v's
-     arrays of every block in one collective (one packed chunk per view) and copies each field
-     into its geometry buffer (rr_geometry_layout);
+     arrays of every block in one collective (one packed chunk per view), and one kernel
+     (rr_unpack_rows) rebuilds its geometry buffer (48-B splat records with log2 o and 1/o, depth
+     keys: bitwise the preprocess's);
   3. rank v renders view v from that geometry (rr_forward_from_geometry: depth sort, binning,
      blend), computes the L1+SSIM loss and its gradient, and runs the blend backward into one
      40-B record per Gaussian (rr_backward_records);
@@ -21,7 +23,7 @@ cross the links are per-(Gaussian, view) records instead:
      exchange then overlaps the owner kernel on chunk c-1);
   5. owner: the per-Gaussian backward of every view in view order, summed, x 1/N, Adam on its rows,
      densification statistics (rr_gauss_backward_views).
-So ~2 x (N-1)/N x 104 B per Gaussian per step cross xGMI (all-to-all: each GPU's share leaves on
+So ~(N-1)/N x (52 + 40) B per Gaussian per step cross xGMI (all-to-all: each GPU's share leaves on
 its seven direct links at once), the per-Gaussian backward and Adam of a rank cover 1/N of the
 rows, and no collective carries parameters or gradients.  The sum over views is formed per element
 in view order, like one process accumulating the same N views: the step's arithmetic is that of
@@ -42,7 +44,7 @@ import torch.distributed as dist
 from . import _native as N
 
 REC_FLOATS = 10
-SPLAT_BYTES = 48
+WIRE_BYTES = 40  # rr_preprocess_rows_views' wire record (the splat's 10 non-derived floats)
 
 
 def _p(t, byte_offset=0):
@@ -119,20 +121,15 @@ class ShardedStep:
         # 1. owner preprocess of every view over the owned rows -> send buffer, one chunk per view
         send, chunk, fields, starts, keep = self.preprocess_views(model, cams, bg, low_pass, flags)
 
-        # 2. one all-to-all: chunk i of recv = rank i's rows for this rank's view; then each field
-        #    into its array of the geometry buffer (rows in global order)
+        # 2. one all-to-all: chunk i of recv = rank i's rows for this rank's view, then one kernel
+        #    rebuilds the geometry arrays (rows in global order) from the wire records
         recv = self._buf("g_recv", Nw * chunk, u8, dev)
         self.ex.all_to_all(recv, send)
         geom = self._buf("geom", int(L.rr_geometry_bytes(P_pad)), u8, dev)
-        offs = (ctypes.c_size_t * 5)()
-        N.check(L.rr_geometry_layout(P_pad, offs), "geometry layout")
         radii = self._buf("radii", P_pad, torch.int32, dev)
-        rv = recv.view(Nw, chunk)
-        dsts = (geom[offs[0]:offs[0] + P_pad * SPLAT_BYTES], geom[offs[1]:offs[1] + P_pad * 8],
-                geom[offs[2]:offs[2] + P_pad * 4], radii.view(u8), geom[offs[3]:offs[3] + (P_pad // 256) * 8],
-                geom[offs[4]:offs[4] + (P_pad // 256) * 4])
-        for (w, n), st0, dst in zip(fields, starts, dsts):
-            dst.view(Nw, w * n).copy_(rv[:, st0:st0 + w * n])
+        offs = (ctypes.c_size_t * 5)(starts[0], starts[1], starts[2], starts[3], starts[4])
+        N.check(L.rr_unpack_rows(Nw, Q, _p(recv), chunk, offs, _p(geom), geom.numel(), _p(radii), stream),
+                "unpack rows")
 
         # 3. render this rank's view from the geometry, loss, blend backward -> records
         cam = cams[self.rank]
@@ -170,9 +167,10 @@ class ShardedStep:
 
     def preprocess_views(self, model, cams, bg, low_pass, flags):
         """Step 1: the owner's rows preprocessed for each of the step's views into the send buffer,
-        one chunk per view: [splat records Q x 48 B | pair counts Q x 8 | depth keys Q x 4 |
-        radii Q x 4 | block sums Q/256 x 8 | wide flags Q/256 x 4].  Returns (send, chunk bytes,
-        fields, field starts, keep = per-view (bg, view, proj, campos) tensors)."""
+        one chunk per view (256-B aligned): [wire records Q x 40 B | pair counts Q x 8 | radii Q x 4 |
+        block sums Q/256 x 8 | wide flags Q/256 x 4] — 52 B per row; the receiver rebuilds the 48-B
+        splat records and the depth keys (rr_unpack_rows).  Returns (send, chunk bytes, fields,
+        field starts, keep = per-view (bg, view, proj, campos) tensors)."""
         L = N.raster()
         dev = model._xyz.device
         P = model._xyz.shape[0]
@@ -181,12 +179,12 @@ class ShardedStep:
         stream = N.stream_of(model._xyz)
         gs, _M = self._row_params(model, lo)
         nb = Q // 256
-        fields = ((SPLAT_BYTES, Q), (8, Q), (4, Q), (4, Q), (8, nb), (4, nb))
+        fields = ((WIRE_BYTES, Q), (8, Q), (4, Q), (8, nb), (4, nb))
         starts, c = [], 0
         for w, n in fields:
             starts.append(c)
             c += w * n
-        chunk = c
+        chunk = (c + 255) // 256 * 256
         send = self._buf("g_send", Nw * chunk, torch.uint8, dev)
         keep = [(bg.contiguous(), cam.world_view_transform.contiguous(), cam.full_proj_transform.contiguous(),
                  cam.camera_center.contiguous()) for cam in cams]
@@ -196,9 +194,10 @@ class ShardedStep:
             views[v] = N.RRView(_p(k[1]), _p(k[2]), _p(k[3]), math.tan(cam.FoVx * 0.5), math.tan(cam.FoVy * 0.5),
                                 float(low_pass), int(cam.image_width), int(cam.image_height))
         fr = self._frame(model, nv, cams[0], low_pass, flags | N.RR_FLAG_RAW_PARAMS)
-        offs = (ctypes.c_size_t * 6)(starts[3], starts[0], starts[1], starts[2], starts[4], starts[5])
+        # [radii, wire records, pair counts, (no depth keys), block sums, wide flags]
+        offs = (ctypes.c_size_t * 6)(starts[2], starts[0], starts[1], 0, starts[3], starts[4])
         N.check(L.rr_preprocess_rows_views(ctypes.byref(fr), views, Nw, ctypes.byref(gs), Q, _p(send), chunk, offs,
-                                           stream),
+                                           1, stream),
                 "sharded preprocess")
         return send, chunk, fields, starts, keep
 

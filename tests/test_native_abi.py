@@ -65,12 +65,17 @@ def test_geometry_layout_and_sharded_step_validation():
     assert rc == 1 and b"multiple of 256" in L.rr_last_error()
     views = (N.RRView * 17)()
     offs6 = (ctypes.c_size_t * 6)()
-    rc = L.rr_preprocess_rows_views(ctypes.byref(f), views, 17, ctypes.byref(g), 512, None, 0, offs6, None)
+    rc = L.rr_preprocess_rows_views(ctypes.byref(f), views, 17, ctypes.byref(g), 512, None, 0, offs6, 1, None)
     assert rc == 1 and b"num_views" in L.rr_last_error()
-    rc = L.rr_preprocess_rows_views(ctypes.byref(f), views, 2, ctypes.byref(g), 300, None, 0, offs6, None)
+    rc = L.rr_preprocess_rows_views(ctypes.byref(f), views, 2, ctypes.byref(g), 300, None, 0, offs6, 1, None)
     assert rc == 1 and b"multiple of 256" in L.rr_last_error()
-    rc = L.rr_preprocess_rows_views(ctypes.byref(f), views, 2, ctypes.byref(g), 512, None, 0, offs6, None)
+    rc = L.rr_preprocess_rows_views(ctypes.byref(f), views, 2, ctypes.byref(g), 512, None, 0, offs6, 1, None)
     assert rc == 1 and b"bad view" in L.rr_last_error()  # null matrices
+    offs5 = (ctypes.c_size_t * 5)()
+    rc = L.rr_unpack_rows(2, 300, None, 0, offs5, None, 0, None, None)
+    assert rc == 1 and b"multiple of 256" in L.rr_last_error()
+    rc = L.rr_unpack_rows(2, 256, 1, 12, offs5, 1, 1 << 30, 1, None)
+    assert rc == 1 and b"alignment" in L.rr_last_error()
     out = N.RRGrads()
     rc = L.rr_gauss_backward_views(ctypes.byref(f), views, 17, ctypes.byref(g), None, 300, 1.0, ctypes.byref(out), None)
     assert rc == 1 and b"num_views" in L.rr_last_error()

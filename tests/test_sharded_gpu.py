@@ -99,13 +99,13 @@ def test_owner_chunking_is_bitwise_neutral():
             assert torch.equal(a, b), f"state tensor {i} differs between chunkings"
 
 
-def test_multi_view_preprocess_equals_per_view():
-    """rr_preprocess_rows_views (every view of the owner's rows in one launch) writes the same
-    bytes as one rr_preprocess_rows call per view."""
+def test_multi_view_wire_preprocess_unpacks_to_the_per_view_geometry():
+    """rr_preprocess_rows_views (every view of the owner's rows in one launch, 52-B wire rows) then
+    rr_unpack_rows gives bitwise the geometry of one rr_preprocess_rows call per view: splat records
+    of the visible rows (log2 o, 1/o rebuilt), pair counts, depth keys, radii, block sums."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import ctypes
-    import math
 
     from rain_amd import _native as N
     from rain_amd import cameras, synthetic
@@ -121,24 +121,38 @@ def test_multi_view_preprocess_equals_per_view():
     cams = [c.to(dev) for c in cameras.fibonacci_cameras(world, 200, 150)]
     bg = torch.zeros(3, device=dev)
     L = N.raster()
+    stream = N.stream_of(g._xyz)
     for rank in range(world):
         sh = ShardedStep(None, rank, world)
         send, chunk, fields, starts, keep = sh.preprocess_views(g, cams, bg, 0.3, _C.frame_flags())
-        send.fill_(0xAB)  # culled rows leave their splat records unwritten: same fill on both sides
-        send, chunk, fields, starts, keep = sh.preprocess_views(g, cams, bg, 0.3, _C.frame_flags())
-        got = send.clone()
         Q, _P_pad, lo, nv = sh.layout(g._xyz.shape[0])
         gs, _M = sh._row_params(g, lo)
-        ref = torch.full_like(send, 0xAB)
-        stream = N.stream_of(g._xyz)
+        gbytes = int(L.rr_geometry_bytes(Q))
+        lay = (ctypes.c_size_t * 5)()
+        N.check(L.rr_geometry_layout(Q, lay), "layout")
+        o_spl, o_til, o_key, o_bs, o_bw = list(lay)
+        offs = (ctypes.c_size_t * 5)(*starts)
         for v, cam in enumerate(cams):
+            got = torch.zeros(gbytes, dtype=torch.uint8, device=dev)
+            got_r = torch.zeros(Q, dtype=torch.int32, device=dev)
+            N.check(L.rr_unpack_rows(1, Q, _p(send, v * chunk), chunk, offs, _p(got), gbytes, _p(got_r), stream),
+                    "unpack")
+            ref = torch.zeros(gbytes, dtype=torch.uint8, device=dev)
+            ref_r = torch.zeros(Q, dtype=torch.int32, device=dev)
             fr = sh._frame(g, nv, cam, 0.3, _C.frame_flags() | N.RR_FLAG_RAW_PARAMS)
             rc = N.RRCamera(*[_p(t) for t in keep[v]])
-            b = v * chunk
-            N.check(L.rr_preprocess_rows(ctypes.byref(fr), ctypes.byref(rc), ctypes.byref(gs), Q,
-                                         _p(ref, b + starts[3]), _p(ref, b + starts[0]), _p(ref, b + starts[1]),
-                                         _p(ref, b + starts[2]), _p(ref, b + starts[4]), _p(ref, b + starts[5]),
-                                         stream), "per-view preprocess")
-        torch.cuda.synchronize()
-        assert math.isfinite(float(got.float().sum()))
-        assert torch.equal(got, ref), f"rank {rank}: multi-view preprocess differs"
+            N.check(L.rr_preprocess_rows(ctypes.byref(fr), ctypes.byref(rc), ctypes.byref(gs), Q, _p(ref_r),
+                                         _p(ref, o_spl), _p(ref, o_til), _p(ref, o_key), _p(ref, o_bs),
+                                         _p(ref, o_bw), stream), "per-view preprocess")
+            torch.cuda.synchronize()
+            assert torch.equal(got_r, ref_r), (rank, v)
+            vis = ref_r > 0
+            assert int(vis.sum()) > 100
+            for off, width in ((o_til, 8), (o_key, 4)):
+                assert torch.equal(got[off:off + Q * width], ref[off:off + Q * width]), (rank, v, off)
+            nb = Q // 256
+            assert torch.equal(got[o_bs:o_bs + 8 * nb], ref[o_bs:o_bs + 8 * nb])
+            assert torch.equal(got[o_bw:o_bw + 4 * nb], ref[o_bw:o_bw + 4 * nb])
+            gs_rows = got[o_spl:o_spl + 48 * Q].view(Q, 48)[vis]
+            rs_rows = ref[o_spl:o_spl + 48 * Q].view(Q, 48)[vis]
+            assert torch.equal(gs_rows, rs_rows), (rank, v, "splat records")
