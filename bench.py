@@ -73,7 +73,7 @@ MODELED = ("preprocess", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd"
 VALU_BOUND = ("blend_fwd", "blend_bwd")
 
 
-def algorithmic_bytes(stage, st, P, W, H, K, world=1):
+def algorithmic_bytes(stage, st, P, W, H, K, world=1, sharded=None):
     """SURVEY §8(d) algorithmic bytes per frame (one training step renders one frame).  Binning
     stages are priced on the (bin, Gaussian) pairs this implementation actually sorts (num_binned:
     bins of 2 x 2 tiles, after exact culling and early-stop binning), not on the reference's larger
@@ -91,7 +91,8 @@ def algorithmic_bytes(stage, st, P, W, H, K, world=1):
         "ranges": (kw + 4) * Lb + 8 * T,
         "blend_fwd": 8 * T + 44 * Le + 24 * N,
         "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
-        "gauss_bwd": gauss_bwd_bytes(P, V, K, M) if world == 1 else gauss_bwd_views_bytes(P, K, M, world),
+        "gauss_bwd": (gauss_bwd_views_bytes(P, K, M, world) if (world > 1 if sharded is None else sharded)
+                      else gauss_bwd_bytes(P, V, K, M)),
     }.get(stage)
 
 
@@ -292,8 +293,12 @@ def main():
         if cnt:
             # per step (= per frame): early-stop binning runs the binning stages in two phases
             kernels[name] = {"ms_per_step": ms / PW, "launches_per_step": cnt / PW, "total_ms": ms}
+    sharded = getattr(trainer, "_owner", None) is not None
     if dom_timed and dom_timed[1]:
-        byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2, world)
+        # per frame; the sharded step's owner kernel may run as several row-chunk launches
+        byts = algorithmic_bytes(dom, mean_stats, Pn, W, H, (D + 1) ** 2, world, sharded)
+        launches_per_step = max(1, round(dom_timed[1] / K))
+        byts = byts / launches_per_step
         dom_ms = dom_timed[0] / dom_timed[1]  # HIP events around every launch inside the timed loop
         gbs = byts / (dom_ms * 1e-3) / 1e9
         rmw_gbs = _rmw_peak(dev)
@@ -308,6 +313,7 @@ def main():
                     # PMC passes are committed for the headline workload only (tools/pmc_workload.py)
                     "traffic": _pmc_traffic(dom) if (P, W, H) == (1_000_000, 1920, 1080) else None,
                     "algorithmic_bytes_per_launch": int(byts),
+                    "launches_per_step": launches_per_step,
                     # the blend kernels are VALU-issue bound, not HBM bound: fraction of SIMD
                     # cycles issuing a VALU op, from the committed SQ counter pass
                     "valu_busy": _pmc_field(dom, "valu_busy") if (P, W, H) == (1_000_000, 1920, 1080) else None,
@@ -316,7 +322,7 @@ def main():
                     "valu_issue_frac": (_pmc_field(dom, "valu_issue_frac")
                                         if (P, W, H) == (1_000_000, 1920, 1080) else None)}
         for k in kernels:
-            b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2, world)
+            b = algorithmic_bytes(k, mean_stats, Pn, W, H, (D + 1) ** 2, world, sharded)
             if b is not None:
                 kernels[k]["algorithmic_GBps"] = round(b / (kernels[k]["ms_per_step"] * 1e-3) / 1e9, 1)
         # north_star states its roofline target on the per-tile blend: both blends' HBM fractions

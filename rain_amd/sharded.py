@@ -76,6 +76,8 @@ class ShardedStep:
         N = 8); rec_chunk_rows overrides (tests)."""
         if self.rec_chunk_rows:
             return max(256, int(self.rec_chunk_rows) // 256 * 256)
+        if self.world == 1:  # nothing crosses a link: one launch
+            return Q
         units = Q // 256
         C = max(1, min(4, Q // self.FILL_ROWS))
         return 256 * -(-units // C)
