@@ -556,7 +556,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         RR_STAGE_CHECK("bin sort");
         {
             StageTimer tm(RR_STAGE_RANGES, st);
-            launch_expand<K>(LA, nullptr, keys_sorted, bn.vals_sorted, gx, gy, 0u, bn.point_list, im.ranges, st);
+            launch_expand<K>(LA, nullptr, keys_sorted, bn.vals_sorted, gx, gy, 0u, bn.point_list, im.ranges, nullptr,
+                             st);
         }
         RR_STAGE_CHECK("expand");
     }
@@ -591,7 +592,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_expand<K>(LB, im.counters, keys_sorted + LA, bn.vals_sorted + LA, gx, gy, 4u * LA, bn.point_list,
-                         im.ranges_b, st);
+                         im.ranges_b, im.open_bits, st);
     }
     RR_STAGE_CHECK("expand (phase B)");
     {

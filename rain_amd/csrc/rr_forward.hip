@@ -723,11 +723,24 @@ template <typename K>
 __global__ __launch_bounds__(256) void k_expand(uint32_t n_host, const uint32_t* __restrict__ n_dev,
                                                 const K* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                 int gx, int gy, uint32_t out_base, uint32_t* __restrict__ point_list,
-                                                uint2* __restrict__ ranges) {
+                                                uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits) {
     __shared__ uint32_t wsum[4][4];
     const int bgx = bins_x(gx);
     const int bin = blockIdx.x;
     const int X = bin % bgx, Y = bin / bgx;
+    if (open_bits) {  // phase B: a bin whose tiles all closed in phase A holds no pair, and its
+                      // tiles' ranges were cleared with the frame's: nothing to search or write
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int tx = 2 * X + (b & 1), ty = 2 * Y + (b >> 1);
+            if (tx < gx && ty < gy) {
+                const uint32_t tile = (uint32_t)(ty * gx + tx);
+                any = any || ((open_bits[tile >> 5] >> (tile & 31)) & 1u);
+            }
+        }
+        if (!any) return;  // block-uniform
+    }
     const uint32_t n = n_dev ? *n_dev : n_host;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // 256-ary searches for the bin's first pair and the next bin's: each round probes 256 evenly
@@ -864,14 +877,14 @@ void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_
 
 template <typename K>
 void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,
-                   uint32_t out_base, uint32_t* point_list, uint2* ranges, hipStream_t st) {
+                   uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
-    if (nb > 0) k_expand<K><<<nb, 256, 0, st>>>(L, n_dev, keys, vals, gx, gy, out_base, point_list, ranges);
+    if (nb > 0) k_expand<K><<<nb, 256, 0, st>>>(L, n_dev, keys, vals, gx, gy, out_base, point_list, ranges, open_bits);
 }
 template void launch_expand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, int, int, uint32_t,
-                                      uint32_t*, uint2*, hipStream_t);
+                                      uint32_t*, uint2*, const uint32_t*, hipStream_t);
 template void launch_expand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, int, int, uint32_t,
-                                      uint32_t*, uint2*, hipStream_t);
+                                      uint32_t*, uint2*, const uint32_t*, hipStream_t);
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;

@@ -255,7 +255,7 @@ bool launch_duplicate(const DupArgs<K>& d, hipStream_t st);
 void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_t* open_bits, hipStream_t st);
 template <typename K>
 void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,
-                   uint32_t out_base, uint32_t* point_list, uint2* ranges, hipStream_t st);
+                   uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
