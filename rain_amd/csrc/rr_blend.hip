@@ -120,20 +120,34 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             const P2X px2 = blend_p2_x(A.z, A.w, Bv.y, dx);  // identical to the forward's values
             float sv = 0.f, svdy = 0.f, svdy2 = 0.f;
             const float4 Cc = s_c[j];  // once per pair (not per active row)
+            // every pixel's alpha first, in one basic block, so that the PPL exp chains interleave
+            // instead of each waiting behind the previous pixel's branched body (LLVM sinks each
+            // back into its pixel's block without the opaque uses): blend bwd 0.2453 -> 0.2435 ms
+            // per step in an interleaved A/B; the reciprocals hoisted too (paid for inactive pixels
+            // as well) measured 0.2491 (profiles/r03_blend_bwd_hoist_ab.jsonl)
+            float ev[PPL], av[PPL];
+            bool acv[PPL];
 #pragma unroll
             for (int q = 0; q < PPL; q++) {
                 const float dy = A.y - (float)(py0 + 4 * q);
                 const float e2 = blend_e2(px2, Bv.x, dy);
-                const float e = __builtin_amdgcn_exp2f(e2);  // o G
-                const float alpha = fminf(0.99f, e);
-                const bool act = contributor < last[q] && e2 <= Bv.y && alpha >= 1.0f / 255.0f;
+                ev[q] = __builtin_amdgcn_exp2f(e2);  // o G
+                av[q] = fminf(0.99f, ev[q]);
+                acv[q] = contributor < last[q] && e2 <= Bv.y && av[q] >= 1.0f / 255.0f;
+            }
+#pragma unroll
+            for (int q = 0; q < PPL; q++) asm volatile("" : "+v"(ev[q]), "+v"(av[q]));
+#pragma unroll
+            for (int q = 0; q < PPL; q++) {
+                const float dy = A.y - (float)(py0 + 4 * q);
+                const float e = ev[q], alpha = av[q];
+                const bool act = acv[q];
                 if (act) {
                     any = true;
-                    const float one_m = 1.f - alpha;
                     // both divisions by (1 - alpha) share one reciprocal; the Newton step keeps T's
                     // recovery within an ulp per pair over lists of thousands of pairs (the bare
                     // v_rcp_f32 measured 2 % faster on this kernel, 0.238 vs 0.243 ms)
-                    const float inv = rcp_nr(one_m);
+                    const float inv = rcp_nr(1.f - alpha);
                     T[q] = T[q] * inv;                // T_i, the transmittance in front of this Gaussian
                     const float dchannel_dcolor = alpha * T[q];
                     const float cdp = Cc.x * dp0[q] + Cc.y * dp1[q] + Cc.z * dp2[q];

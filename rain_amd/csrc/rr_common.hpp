@@ -320,8 +320,8 @@ __device__ __forceinline__ void ewa_cov2d(const Proj2D& p, const float cov[6], f
 // Coefficient 0 is dc[0..3), coefficient k >= 1 is rest[3(k-1)..): one contiguous [M,3] block
 // (dc = sh, rest = sh + 3) or the model's separate f_dc / f_rest tensors (raw-parameter mode).
 template <int DEG>
-__device__ __forceinline__ v3 sh_eval(v3 dir, const float* dc, const float* rest) {
-    v3 r = RR_SH_C0 * load3(dc);
+__device__ __forceinline__ v3 sh_eval(v3 dir, v3 dc, const float* rest) {
+    v3 r = RR_SH_C0 * dc;
     if (DEG > 0) {
         const float x = dir.x, y = dir.y, z = dir.z;
         r = r - (RR_SH_C1 * y) * load3(rest + 0) + (RR_SH_C1 * z) * load3(rest + 3) - (RR_SH_C1 * x) * load3(rest + 6);
@@ -344,6 +344,10 @@ __device__ __forceinline__ v3 sh_eval(v3 dir, const float* dc, const float* rest
         }
     }
     return mk(r.x + 0.5f, r.y + 0.5f, r.z + 0.5f);
+}
+template <int DEG>
+__device__ __forceinline__ v3 sh_eval(v3 dir, const float* dc, const float* rest) {
+    return sh_eval<DEG>(dir, load3(dc), rest);
 }
 
 // N consecutive floats at a dword-aligned address, as 16-B loads (the target runs in unaligned

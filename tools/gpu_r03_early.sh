@@ -1,0 +1,17 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for i in 1 2; do
+  for v in base e1o3 e2; do
+    RAIN_RASTER_LIB=gpurun_variants/$v.so timeout -k 10 240 python -u tools/variant_step.py --tag $v --steps 40 >> gpurun_out/r03_early.jsonl 2>> gpurun_out/r03_early.err || { tail -20 gpurun_out/r03_early.err; exit 1; }
+  done
+done
+python3 - <<'P'
+import json
+for l in open("gpurun_out/r03_early.jsonl"):
+    d = json.loads(l); print(d["tag"], d["ms_per_step"], d["stages_ms"]["preprocess"])
+P
+for v in e1o3 e2; do
+RAIN_RASTER_LIB=gpurun_variants/$v.so timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py tests/test_fused_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r03_${v}_parity.log 2>&1 || { tail -5 gpurun_out/r03_${v}_parity.log; exit 1; }
+tail -1 gpurun_out/r03_${v}_parity.log
+done
