@@ -182,7 +182,7 @@ def raster():
     return _raster
 
 
-LOSS_LIB = os.path.join(LIB_DIR, "librain_loss.so")
+LOSS_LIB = os.environ.get("RAIN_LOSS_LIB") or os.path.join(LIB_DIR, "librain_loss.so")
 LOSS_SYMBOLS = ["rl_workspace_bytes", "rl_l1_ssim_forward", "rl_l1_ssim_backward", "rl_last_error"]
 _loss = None
 

@@ -26,7 +26,9 @@ namespace {
 // output rows.  The block streams the TH + 10 input rows of its band through an NR-row LDS ring,
 // and global loads run LA rows ahead of the ring in a small register queue, so memory latency
 // hides behind LA rows of arithmetic while a wave needs only NR x 74 floats of LDS per plane
-// (LA 2..6 and TH 16..64 measured: TH 32 best, LA within 5%).
+// (LA 2..6 and TH 16..64 measured: TH 32 best, LA within 5%; per kernel in round 3, standalone
+// 3x1080x1920: backward TH 8/16/32/48/64 = 62/54/45/51/57 us, forward TH 16/32/48 = 55/52/65 us,
+// profiles/r03_ssim_band_ab.jsonl).
 // The row loop is fully unrolled (build flag -pragma-unroll-threshold, rain_amd/_build.py): every
 // ring / queue slot is a compile-time register.
 constexpr int R = 5;             // window radius (11 taps)
@@ -34,15 +36,18 @@ constexpr int TW = 64;           // output columns per block
 #ifndef RL_TH
 #define RL_TH 32
 #endif
+#ifndef RL_TH_BWD
+#define RL_TH_BWD RL_TH
+#endif
 #ifndef RL_LA_FWD
 #define RL_LA_FWD 2
 #endif
 #ifndef RL_LA_BWD
 #define RL_LA_BWD 4
 #endif
-constexpr int TH = RL_TH;        // output rows per block
+constexpr int TH_FWD = RL_TH;     // output rows per block, forward
+constexpr int TH_BWD = RL_TH_BWD; // and backward
 constexpr int PW = TW + 2 * R;   // 74: patch row width (halo of 5 each side, zero padded)
-constexpr int PH = TH + 2 * R;   // 42: input rows per band
 constexpr int NR = 2;            // LDS row ring (double buffer)
 constexpr int LA_FWD = RL_LA_FWD; // rows of global-load lookahead (register queue), forward
 constexpr int LA_BWD = RL_LA_BWD; // and backward (fewer live values: deeper queue fits)
@@ -131,7 +136,7 @@ struct Band {
 };
 
 // Rows 0..NR-1 into the LDS ring, rows NR..NR+LA-1 into the register queue.
-template <int NP, int LA>
+template <int NP, int LA, int PH>
 __device__ __forceinline__ void prime(const Rsrc (&rs)[NP], const Band& bd, float (*dst)[NR][PW],
                                       PatchRow<NP> (&q)[LA + 1], int lane) {
     PatchRow<NP> rows[NR];
@@ -147,12 +152,12 @@ __device__ __forceinline__ void prime(const Rsrc (&rs)[NP], const Band& bd, floa
 
 // Per band row r (compile time): issue the load of row r + NR + LA, and after the row has been
 // read from the ring move row r + NR from the queue into its slot.
-template <int NP, int LA>
+template <int NP, int LA, int PH>
 __device__ __forceinline__ void queue_issue(const Rsrc (&rs)[NP], const Band& bd, PatchRow<NP> (&q)[LA + 1], int r) {
     __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (bounded register lifetimes)
     if (r + NR + LA < PH) q[(r + NR + LA) % (LA + 1)].load(rs, bd.voff, bd.soff(r + NR + LA));
 }
-template <int NP, int LA>
+template <int NP, int LA, int PH>
 __device__ __forceinline__ void queue_retire(float (*dst)[NR][PW], const PatchRow<NP> (&q)[LA + 1], int r, int lane) {
     __syncthreads();  // every lane's reads of slot r % NR are done before it is refilled
     if (r + NR < PH) q[(r + NR) % (LA + 1)].store(dst, r % NR, lane);
@@ -162,6 +167,7 @@ __device__ __forceinline__ void queue_retire(float (*dst)[NR][PW], const PatchRo
 // pass over the LDS ring gives the five row moments (x, y, x^2, y^2, xy), kept in an 11-row
 // register ring; once it is full each new row completes one output row through the 11-tap
 // vertical pass, followed by the SSIM term and the three gradient maps.
+template <int TH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_ssim_fwd(const float* __restrict__ img, const float* __restrict__ gt, int H,
                                                  int W, float lambda, float inv_n, Win win, float* __restrict__ g1,
                                                  float* __restrict__ g11, float* __restrict__ g12,
@@ -171,13 +177,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     const int x0 = blockIdx.x * TW - R, y0 = blockIdx.y * TH - R;
     const size_t plane = (size_t)H * W;
     const int lane = threadIdx.x;
+    constexpr int PH = TH + 2 * R;  // input rows per band
     const Rsrc rs[2] = {plane_rsrc(img + c * plane, 4 * (int)plane), plane_rsrc(gt + c * plane, 4 * (int)plane)};
     const Rsrc ws[3] = {plane_rsrc(g1 + c * plane, 4 * (int)plane), plane_rsrc(g11 + c * plane, 4 * (int)plane),
                         plane_rsrc(g12 + c * plane, 4 * (int)plane)};
     const Band bd(x0, y0, H, W, lane);
     constexpr int LA = LA_FWD;
     PatchRow<2> q[LA + 1];
-    prime<2, LA>(rs, bd, sp, q, lane);
+    prime<2, LA, PH>(rs, bd, sp, q, lane);
     const int gx = blockIdx.x * TW + lane;
     const bool col_in = gx < W;
     const int vo = col_in ? 4 * gx : kOOB;
@@ -187,7 +194,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     float s_val = 0.f, l1 = 0.f;
 #pragma unroll
     for (int r = 0; r < PH; r++) {
-        queue_issue<2, LA>(rs, bd, q, r);
+        queue_issue<2, LA, PH>(rs, bd, q, r);
         const int slot = r % NR;
         const lds_ptr px = row_base(&sp[0][slot][lane]);
         const lds_ptr py = px + NR * PW;  // plane 1, same slot
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         // compiler cannot sink the row's arithmetic into conditional blocks (the LDS reads would
         // then stay live across rows and spill)
         if (r >= R && r < TH + R) l1 += (col_in && y0 + r < H) ? fabsf(px[R] - py[R]) : 0.f;
-        queue_retire<2, LA>(sp, q, r, lane);
+        queue_retire<2, LA, PH>(sp, q, r, lane);
         r0[r % 11] = a;
         r1[r % 11] = b;
         r2[r % 11] = aa;
@@ -316,6 +323,7 @@ __global__ __launch_bounds__(kFinT) void k_loss_finalize(const float2* __restric
 // Backward: the same streamed walk over the three forward maps (G1, G11, G12): horizontal pass
 // from the LDS ring into an 11-row register ring, vertical pass from registers, then the
 // pointwise chain rule.
+template <int TH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_ssim_bwd(const float* __restrict__ img, const float* __restrict__ gt, int H,
                                                  int W, float lambda, float inv_n, Win win,
                                                  const float* __restrict__ g1, const float* __restrict__ g11,
@@ -326,6 +334,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int x0 = blockIdx.x * TW - R, y0 = blockIdx.y * TH - R;
     const size_t plane = (size_t)H * W;
     const int lane = threadIdx.x;
+    constexpr int PH = TH + 2 * R;  // input rows per band
     const Rsrc rs[3] = {plane_rsrc(g1 + c * plane, 4 * (int)plane), plane_rsrc(g11 + c * plane, 4 * (int)plane),
                         plane_rsrc(g12 + c * plane, 4 * (int)plane)};
     const Rsrc ps[3] = {plane_rsrc(img + c * plane, 4 * (int)plane), plane_rsrc(gt + c * plane, 4 * (int)plane),
@@ -333,7 +342,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const Band bd(x0, y0, H, W, lane);
     constexpr int LA = LA_BWD;
     PatchRow<3> q[LA + 1];
-    prime<3, LA>(rs, bd, sg, q, lane);
+    prime<3, LA, PH>(rs, bd, sg, q, lane);
     const int gx = blockIdx.x * TW + lane;
     const int vo = gx < W ? 4 * gx : kOOB;
     const float gl = grad_loss[0];
@@ -341,7 +350,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     float r0[11], r1[11], r2[11];
 #pragma unroll
     for (int r = 0; r < PH; r++) {
-        queue_issue<3, LA>(rs, bd, q, r);
+        queue_issue<3, LA, PH>(rs, bd, q, r);
         const int slot = r % NR;
         const lds_ptr pa = row_base(&sg[0][slot][lane]);
         float a = 0.f, b = 0.f, d = 0.f;
@@ -355,7 +364,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         pin(a);
         pin(b);
         pin(d);
-        queue_retire<3, LA>(sg, q, r, lane);
+        queue_retire<3, LA, PH>(sg, q, r, lane);
         r0[r % 11] = a;
         r1[r % 11] = b;
         r2[r % 11] = d;
@@ -383,7 +392,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
 }
 
-int nblocks(int C, int H, int W) { return ((W + TW - 1) / TW) * ((H + TH - 1) / TH) * C; }
+int nblocks(int C, int H, int W) { return ((W + TW - 1) / TW) * ((H + TH_FWD - 1) / TH_FWD) * C; }
 
 }  // namespace
 
@@ -418,8 +427,8 @@ int rl_l1_ssim_forward(const float* img, const float* gt, int C, int H, int W, f
     float2* partial = reinterpret_cast<float2*>(g12 + n);
     const float inv_n = (float)(1.0 / (double)n);
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid((W + TW - 1) / TW, (H + TH - 1) / TH, C);
-    k_ssim_fwd<<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g11, g12, partial);
+    dim3 grid((W + TW - 1) / TW, (H + TH_FWD - 1) / TH_FWD, C);
+    k_ssim_fwd<TH_FWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g11, g12, partial);
     k_loss_finalize<<<1, kFinT, 0, st>>>(partial, nblocks(C, H, W), lambda, inv_n, loss, parts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -445,8 +454,8 @@ int rl_l1_ssim_backward(const float* img, const float* gt, int C, int H, int W, 
     const float* g1 = static_cast<const float*>(workspace);
     const float inv_n = (float)(1.0 / (double)n);
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid((W + TW - 1) / TW, (H + TH - 1) / TH, C);
-    k_ssim_bwd<<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg);
+    dim3 grid((W + TW - 1) / TW, (H + TH_BWD - 1) / TH_BWD, C);
+    k_ssim_bwd<TH_BWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("rl_l1_ssim_backward: ") + hipGetErrorString(e);
