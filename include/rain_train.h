@@ -61,11 +61,18 @@ int rt_adam_step_scaled(const rt_adam_group* groups, int n_groups, double beta1,
  * draws them, scaling = log(s_i * (1 / split_scale_div)) (torch divides by a scalar through its
  * reciprocal), and the parameters of i otherwise; clones and children get zero Adam moments.
  *
- * rt_densify_plan: flags + offsets into the workspace and the four counts (host, after a sync):
+ * With abe_split (RAIN-GS warm-up, train.py:138-140, gaussian_model.py:342-364) the split
+ * Gaussians first get n_split - 1 copies each, appended after the clones (copy-major, like
+ * repeat(BACK_N, 1)): xyz = (xyz * abe_xyz_scale0) * abe_xyz_scale1, scaling = log(exp(s)), the
+ * other parameters as they are, zero moments, pruned like any row; the caller draws (and drops)
+ * the (n_split - 1) * counts[3] rows of normals the reference draws for them before the split's.
+ *
+ * rt_densify_plan: flags + offsets into the workspace and the five counts (host, after a sync):
  *   counts[0] = originals kept, [1] = clones kept, [2] = split Gaussians whose children are kept,
- *   [3] = split Gaussians (rows of standard normals per child block).
+ *   [3] = split Gaussians (rows of standard normals per child block), [4] = split Gaussians whose
+ *   abe copies are kept (0 without abe_split).
  * rt_densify_apply: writes every group's parameter / exp_avg / exp_avg_sq rows for the new set of
- *   counts[0] + counts[1] + n_split * counts[2] Gaussians.
+ *   counts[0] + counts[1] + (n_split - 1) * counts[4] + n_split * counts[2] Gaussians.
  */
 typedef struct rt_densify_params {
     int P;                    /* Gaussians before densification */
@@ -76,6 +83,9 @@ typedef struct rt_densify_params {
     float big_world_scale;    /* 0.1 * extent */
     int prune_big_world;      /* max_screen_size given */
     float split_scale_div;    /* divide_ratio * N */
+    int abe_split;            /* RAIN-GS warm-up split (gaussian_model.py:342-364): n_split - 1 extra copies */
+    float abe_xyz_scale0;     /* 0.3: an abe copy's xyz = (xyz * abe_xyz_scale0) * abe_xyz_scale1 */
+    float abe_xyz_scale1;     /* scene_extent */
 } rt_densify_params;
 
 typedef struct rt_densify_group {
@@ -96,9 +106,9 @@ typedef struct rt_densify_group {
 size_t rt_densify_workspace_bytes(int P);
 int rt_densify_plan(const rt_densify_params* p, const float* xyz_gradient_accum, const float* denom,
                     const float* scaling, const float* opacity, void* workspace, size_t workspace_bytes,
-                    int64_t counts[4], void* stream);
+                    int64_t counts[5], void* stream);
 int rt_densify_apply(const rt_densify_params* p, const float* scaling, const float* rotation, const float* normals,
-                     const void* workspace, const rt_densify_group* groups, int n_groups, const int64_t counts[4],
+                     const void* workspace, const rt_densify_group* groups, int n_groups, const int64_t counts[5],
                      void* stream);
 
 /* Streaming device-to-device copy of n_bytes (multiple of 16; both pointers 16-B aligned): 16-B

@@ -214,7 +214,8 @@ class RTDensifyParams(ctypes.Structure):
     _fields_ = [("P", ctypes.c_int), ("n_split", ctypes.c_int), ("grad_threshold", ctypes.c_float),
                 ("clone_split_scale", ctypes.c_float), ("min_opacity", ctypes.c_float),
                 ("big_world_scale", ctypes.c_float), ("prune_big_world", ctypes.c_int),
-                ("split_scale_div", ctypes.c_float)]
+                ("split_scale_div", ctypes.c_float), ("abe_split", ctypes.c_int), ("abe_xyz_scale0", ctypes.c_float),
+                ("abe_xyz_scale1", ctypes.c_float)]
 
 
 class RTDensifyGroup(ctypes.Structure):

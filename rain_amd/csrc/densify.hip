@@ -5,11 +5,11 @@
 // their 12 Adam moment tensors (clone: cat; split: gather, bmm, cat, then a prune; final prune:
 // gather), i.e. several full passes over ~0.7 KB per Gaussian plus a host sync per masked index.
 // Here:
-//   k_densify_classify  one thread per Gaussian: clone / split / prune decisions -> 4 flag bits
-//   rocPRIM scan        exclusive scan of the 4 flags (as uint4) -> every survivor's output row
+//   k_densify_classify  one thread per Gaussian: clone / split / abe / prune decisions -> 5 flag bits
+//   rocPRIM scan        exclusive scan of the 5 flags -> every survivor's output row
 //   k_densify_apply     one pass over every group's (param, exp_avg, exp_avg_sq) elements, each
 //                       element written straight to its rows in the new set (original / clone /
-//                       n_split children); coalesced reads, contiguous runs of writes.
+//                       abe copies / n_split children); coalesced reads, contiguous runs of writes.
 // One host sync (the counts, to size the outputs and draw the split samples).
 //
 // Arithmetic is written as torch evaluates the reference's expressions (one rounding per op: fp
@@ -44,24 +44,28 @@ constexpr size_t kAlign = 256;
 inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 
 // flag bits per Gaussian
-constexpr unsigned kKeepOrig = 1u, kKeepClone = 2u, kKeepChildren = 4u, kSplit = 8u;
+constexpr unsigned kKeepOrig = 1u, kKeepClone = 2u, kKeepChildren = 4u, kSplit = 8u, kKeepAbe = 16u;
 
-struct Flags4 {
-    __host__ __device__ uint4 operator()(uint8_t f) const {
-        return make_uint4(f & 1u, (f >> 1) & 1u, (f >> 2) & 1u, (f >> 3) & 1u);
+// the five ranks of a Gaussian: {orig, clone, children, split, abe copies}
+struct Rank5 {
+    uint32_t o, c, ch, s, ab;
+};
+struct Flags5 {
+    __host__ __device__ Rank5 operator()(uint8_t f) const {
+        return Rank5{f & 1u, (f >> 1) & 1u, (f >> 2) & 1u, (f >> 3) & 1u, (f >> 4) & 1u};
     }
 };
-struct Add4 {
-    __host__ __device__ uint4 operator()(const uint4& a, const uint4& b) const {
-        return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+struct Add5 {
+    __host__ __device__ Rank5 operator()(const Rank5& a, const Rank5& b) const {
+        return Rank5{a.o + b.o, a.c + b.c, a.ch + b.ch, a.s + b.s, a.ab + b.ab};
     }
 };
-using FlagIt = rocprim::transform_iterator<const uint8_t*, Flags4, uint4>;
+using FlagIt = rocprim::transform_iterator<const uint8_t*, Flags5, Rank5>;
 
 struct Workspace {
     uint8_t* flags;
-    uint4* offsets;  // exclusive scan of the flag bits: {orig, clone, children, split} rank
-    uint4* totals;   // [1]
+    Rank5* offsets;  // exclusive scan of the flag bits
+    Rank5* totals;   // [1]
     void* temp;
     size_t temp_bytes;
     size_t total;
@@ -69,8 +73,8 @@ struct Workspace {
 size_t scan_temp_bytes(int P) {
     size_t b = 0;
     if (P > 0)
-        (void)rocprim::exclusive_scan(nullptr, b, FlagIt((const uint8_t*)nullptr, Flags4()), (uint4*)nullptr,
-                                      make_uint4(0u, 0u, 0u, 0u), (size_t)P, Add4(), (hipStream_t)0);
+        (void)rocprim::exclusive_scan(nullptr, b, FlagIt((const uint8_t*)nullptr, Flags5()), (Rank5*)nullptr,
+                                      Rank5{0u, 0u, 0u, 0u, 0u}, (size_t)P, Add5(), (hipStream_t)0);
     return b;
 }
 Workspace carve(void* base, int P) {
@@ -85,8 +89,8 @@ Workspace carve(void* base, int P) {
         return p;
     };
     w.flags = reinterpret_cast<uint8_t*>(take(n));
-    w.offsets = reinterpret_cast<uint4*>(take(n * sizeof(uint4)));
-    w.totals = reinterpret_cast<uint4*>(take(sizeof(uint4)));
+    w.offsets = reinterpret_cast<Rank5*>(take(n * sizeof(Rank5)));
+    w.totals = reinterpret_cast<Rank5*>(take(sizeof(Rank5)));
     w.temp_bytes = scan_temp_bytes(P);
     w.temp = take(w.temp_bytes > 0 ? w.temp_bytes : 1);
     w.total = align_up(off);
@@ -124,14 +128,16 @@ __global__ __launch_bounds__(256) void k_densify_classify(rt_densify_params p, f
     if (clone && !prune) f |= kKeepClone;
     if (split && !prune_child) f |= kKeepChildren;
     if (split) f |= kSplit;
+    if (split && p.abe_split && p.n_split > 1) {  // abe copies: scaling log(exp(s)), pruned on its exp
+        const float a0 = logf(expf(s0)), a1 = logf(expf(s1)), a2 = logf(expf(s2));
+        if (!(low || (p.prune_big_world && max_exp3(a0, a1, a2) > p.big_world_scale))) f |= kKeepAbe;
+    }
     flags[i] = (uint8_t)f;
 }
 
-__global__ void k_totals(int P, const uint8_t* __restrict__ flags, const uint4* __restrict__ offsets,
-                         uint4* __restrict__ totals) {
-    const uint8_t f = flags[P - 1];
-    const uint4 o = offsets[P - 1];
-    *totals = make_uint4(o.x + (f & 1u), o.y + ((f >> 1) & 1u), o.z + ((f >> 2) & 1u), o.w + ((f >> 3) & 1u));
+__global__ void k_totals(int P, const uint8_t* __restrict__ flags, const Rank5* __restrict__ offsets,
+                         Rank5* __restrict__ totals) {
+    *totals = Add5()(offsets[P - 1], Flags5()(flags[P - 1]));
 }
 
 constexpr int kMaxGroups = 8;
@@ -151,10 +157,11 @@ struct ApplyArgs {
     ApplyGroup grp[kMaxGroups];
     int n_groups;
     int n_split;
-    uint32_t A, B, C, S;  // counts
-    float inv_div;        // 1 / (divide_ratio * N) in fp32
+    uint32_t A, B, C, S, E;  // counts
+    float inv_div;           // 1 / (divide_ratio * N) in fp32
+    float abe0, abe1;        // an abe copy's xyz = (xyz * abe0) * abe1
     const uint8_t* flags;
-    const uint4* offsets;
+    const Rank5* offsets;
     const float* scaling;
     const float* rotation;
     const float* normals;  // [n_split * S, 3]
@@ -197,11 +204,11 @@ __global__ __launch_bounds__(kApplyThreads) void k_densify_apply(ApplyArgs a) {
     const int64_t i = e / w;
     const int col = (int)(e - i * w);
     const unsigned f = a.flags[i];
-    if (!(f & (kKeepOrig | kKeepClone | kKeepChildren))) return;
-    const uint4 off = a.offsets[i];
+    if (!(f & (kKeepOrig | kKeepClone | kKeepChildren | kKeepAbe))) return;
+    const Rank5 off = a.offsets[i];
     const float pv = G.p[e];
     if (f & kKeepOrig) {
-        const int64_t d = (int64_t)off.x * w + col;
+        const int64_t d = (int64_t)off.o * w + col;
         G.op[d] = pv;
         if (G.om) {
             G.om[d] = G.m[e];
@@ -209,11 +216,24 @@ __global__ __launch_bounds__(kApplyThreads) void k_densify_apply(ApplyArgs a) {
         }
     }
     if (f & kKeepClone) {  // densify_and_clone: same values, zero moments
-        const int64_t d = ((int64_t)a.A + off.y) * w + col;
+        const int64_t d = ((int64_t)a.A + off.c) * w + col;
         G.op[d] = pv;
         if (G.om) {
             G.om[d] = 0.f;
             G.ov[d] = 0.f;
+        }
+    }
+    if (f & kKeepAbe) {  // the abe copies (copy-major after the clones), zero moments
+        float val = pv;
+        if (G.kind == RT_GROUP_SCALING) val = logf(expf(pv));  // scaling_inverse_activation(get_scaling)
+        if (G.kind == RT_GROUP_XYZ) val = (pv * a.abe0) * a.abe1;
+        for (int n = 0; n + 1 < a.n_split; n++) {
+            const int64_t d = ((int64_t)a.A + a.B + (int64_t)n * a.E + off.ab) * w + col;
+            G.op[d] = val;
+            if (G.om) {
+                G.om[d] = 0.f;
+                G.ov[d] = 0.f;
+            }
         }
     }
     if (f & kKeepChildren) {  // densify_and_split children
@@ -229,11 +249,12 @@ __global__ __launch_bounds__(kApplyThreads) void k_densify_apply(ApplyArgs a) {
         for (int n = 0; n < a.n_split; n++) {
             if (G.kind == RT_GROUP_XYZ) {
                 // samples = normal(0, 1) * std + 0 (torch.normal); new_xyz = bmm(R, samples) + xyz
-                const float* z = a.normals + 3 * ((int64_t)n * a.S + off.w);
+                const float* z = a.normals + 3 * ((int64_t)n * a.S + off.s);
                 const float q0 = z[0] * sd0 + 0.f, q1 = z[1] * sd1 + 0.f, q2 = z[2] * sd2 + 0.f;
                 val = fmaf(r2, q2, fmaf(r1, q1, r0 * q0)) + pv;
             }
-            const int64_t d = ((int64_t)a.A + a.B + (int64_t)n * a.C + off.z) * w + col;
+            const int64_t d = ((int64_t)a.A + a.B + (int64_t)(a.n_split - 1) * a.E + (int64_t)n * a.C + off.ch) * w +
+                              col;
             G.op[d] = val;
             if (G.om) {
                 G.om[d] = 0.f;
@@ -251,9 +272,9 @@ size_t rt_densify_workspace_bytes(int P) { return carve(nullptr, P).total; }
 
 int rt_densify_plan(const rt_densify_params* p, const float* xyz_gradient_accum, const float* denom,
                     const float* scaling, const float* opacity, void* workspace, size_t workspace_bytes,
-                    int64_t counts[4], void* stream) {
+                    int64_t counts[5], void* stream) {
     if (!p || !counts) return fail("rt_densify_plan: null params / counts");
-    for (int k = 0; k < 4; k++) counts[k] = 0;
+    for (int k = 0; k < 5; k++) counts[k] = 0;
     if (p->P < 0 || p->n_split < 1) return fail("rt_densify_plan: bad P / n_split");
     if (p->P == 0) return 0;
     if (!xyz_gradient_accum || !denom || !scaling || !opacity || !workspace)
@@ -265,31 +286,33 @@ int rt_densify_plan(const rt_densify_params* p, const float* xyz_gradient_accum,
     k_densify_classify<<<(p->P + 255) / 256, 256, 0, st>>>(*p, inv_div, xyz_gradient_accum, denom, scaling, opacity,
                                                             w.flags);
     size_t tb = w.temp_bytes;
-    hipError_t e = rocprim::exclusive_scan(w.temp, tb, FlagIt(w.flags, Flags4()), w.offsets,
-                                           make_uint4(0u, 0u, 0u, 0u), (size_t)p->P, Add4(), st);
+    hipError_t e = rocprim::exclusive_scan(w.temp, tb, FlagIt(w.flags, Flags5()), w.offsets,
+                                           Rank5{0u, 0u, 0u, 0u, 0u}, (size_t)p->P, Add5(), st);
     if (e != hipSuccess) return fail(std::string("densify scan: ") + hipGetErrorString(e));
     k_totals<<<1, 1, 0, st>>>(p->P, w.flags, w.offsets, w.totals);
-    uint4 t;
-    e = hipMemcpyAsync(&t, w.totals, sizeof(uint4), hipMemcpyDeviceToHost, st);
+    Rank5 t;
+    e = hipMemcpyAsync(&t, w.totals, sizeof(Rank5), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return fail(std::string("densify plan: ") + hipGetErrorString(e));
-    counts[0] = t.x;
-    counts[1] = t.y;
-    counts[2] = t.z;
-    counts[3] = t.w;
+    counts[0] = t.o;
+    counts[1] = t.c;
+    counts[2] = t.ch;
+    counts[3] = t.s;
+    counts[4] = t.ab;
     return 0;
 }
 
 int rt_densify_apply(const rt_densify_params* p, const float* scaling, const float* rotation, const float* normals,
-                     const void* workspace, const rt_densify_group* groups, int n_groups, const int64_t counts[4],
+                     const void* workspace, const rt_densify_group* groups, int n_groups, const int64_t counts[5],
                      void* stream) {
     if (!p || !counts || (n_groups > 0 && !groups)) return fail("rt_densify_apply: null argument");
     if (n_groups < 0 || n_groups > kMaxGroups) return fail("rt_densify_apply: n_groups must be 0..8");
     if (p->P == 0) return 0;
     if (!workspace || !scaling || !rotation) return fail("rt_densify_apply: null array");
     if (counts[3] > 0 && !normals) return fail("rt_densify_apply: split samples missing");
-    for (int k = 0; k < 4; k++)
+    for (int k = 0; k < 5; k++)
         if (counts[k] < 0 || counts[k] > p->P) return fail("rt_densify_apply: counts out of range");
+    if (counts[4] > 0 && !p->abe_split) return fail("rt_densify_apply: abe copies without abe_split");
     Workspace w = carve(const_cast<void*>(workspace), p->P);
     ApplyArgs a{};
     a.n_groups = n_groups;
@@ -298,7 +321,10 @@ int rt_densify_apply(const rt_densify_params* p, const float* scaling, const flo
     a.B = (uint32_t)counts[1];
     a.C = (uint32_t)counts[2];
     a.S = (uint32_t)counts[3];
+    a.E = (uint32_t)counts[4];
     a.inv_div = 1.0f / p->split_scale_div;
+    a.abe0 = p->abe_xyz_scale0;
+    a.abe1 = p->abe_xyz_scale1;
     a.flags = w.flags;
     a.offsets = w.offsets;
     a.scaling = scaling;

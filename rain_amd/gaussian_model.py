@@ -443,6 +443,10 @@ class GaussianModel:
             new_features_dc = self._features_dc[selected_pts_mask].repeat(BACK_N, 1, 1)
             new_features_rest = self._features_rest[selected_pts_mask].repeat(BACK_N, 1, 1)
             new_opacity = self._opacity[selected_pts_mask].repeat(BACK_N, 1)
+            # the reference draws (and never uses) BACK_N rows of normals per selected Gaussian here
+            # (gaussian_model.py:349-351): drawn too, so the split below sees the same random stream
+            stds = self.get_scaling[selected_pts_mask].repeat(BACK_N, 1)
+            torch.normal(mean=torch.zeros((stds.size(0), 3), device=dev), std=stds, generator=generator)
             new_xyz = new_xyz * 0.3 * scene_extent
             self.densification_postfix(new_xyz, new_features_dc, new_features_rest, new_opacity, new_scaling,
                                        new_rotation)
@@ -484,8 +488,11 @@ class GaussianModel:
 
     def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, N=2, abe_split=False,
                           generator=None):
-        if self.native_densify and self.device.type == "cuda" and not abe_split and self._xyz.shape[0] > 0:
-            return self._densify_and_prune_native(max_grad, min_opacity, extent, max_screen_size, N, generator)
+        # (abe_split with max_grad <= 0 would also select the abe copies for the split: torch path)
+        if (self.native_densify and self.device.type == "cuda" and self._xyz.shape[0] > 0
+                and not (abe_split and max_grad <= 0)):
+            return self._densify_and_prune_native(max_grad, min_opacity, extent, max_screen_size, N, generator,
+                                                  abe_split)
         grads = self.xyz_gradient_accum / self.denom
         grads[grads.isnan()] = 0.0
         self.densify_and_clone(grads, max_grad, extent)
@@ -497,11 +504,13 @@ class GaussianModel:
             prune_mask = torch.logical_or(torch.logical_or(prune_mask, big_points_vs), big_points_ws)
         self.prune_points(prune_mask)
 
-    def _densify_and_prune_native(self, max_grad, min_opacity, extent, max_screen_size, N, generator):
-        """densify_and_clone + densify_and_split + prune (gaussian_model.py:366-415) as one stream
-        compaction on the device: the same decisions, the survivors in the same order, the same values
-        (the split children's xyz up to the rounding of the reference's bmm) and the same
-        optimizer-state surgery (new Parameters, zero moments for the new Gaussians)."""
+    def _densify_and_prune_native(self, max_grad, min_opacity, extent, max_screen_size, N, generator,
+                                  abe_split=False):
+        """densify_and_clone + densify_and_split (with the RAIN-GS abe copies when abe_split) + prune
+        (gaussian_model.py:339-415) as one stream compaction on the device: the same decisions, the
+        survivors in the same order, the same values (the split children's xyz up to the rounding of
+        the reference's bmm) and the same optimizer-state surgery (new Parameters, zero moments for
+        the new Gaussians)."""
         import ctypes
 
         from . import _native as NV
@@ -518,18 +527,22 @@ class GaussianModel:
                 raise RuntimeError(f"{what}: {L.rt_last_error().decode(errors='replace')}")
 
         prm = NV.RTDensifyParams(P, int(N), float(max_grad), float(self.percent_dense * extent), float(min_opacity),
-                                 float(0.1 * extent), int(bool(max_screen_size)), float(self.divide_ratio * N))
+                                 float(0.1 * extent), int(bool(max_screen_size)), float(self.divide_ratio * N),
+                                 int(bool(abe_split)), 0.3, float(extent))
         ws = torch.empty((L.rt_densify_workspace_bytes(P),), dtype=torch.uint8, device=dev)
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         acc, den = self.xyz_gradient_accum.contiguous(), self.denom.contiguous()
         sc, op, rot = (t.detach().contiguous() for t in (self._scaling, self._opacity, self._rotation))
-        counts = (ctypes.c_int64 * 4)()
+        counts = (ctypes.c_int64 * 5)()
         check(L.rt_densify_plan(ctypes.byref(prm), ptr(acc), ptr(den), ptr(sc), ptr(op), ptr(ws), ws.numel(), counts,
                                 stream), "rt_densify_plan")
-        A, B, C, S = (int(c) for c in counts)
-        # torch.normal(mean=0, std) draws normal_(0, 1) into its output first: same draws, same generator
+        A, B, C, S, E = (int(c) for c in counts)
+        # torch.normal(mean=0, std) draws normal_(0, 1) into its output first: same draws, same
+        # generator; with abe_split the reference's unused (N - 1) * S rows come first
+        if abe_split and S and N > 1:
+            torch.empty(((N - 1) * S, 3), device=dev).normal_(0.0, 1.0, generator=generator)
         z = torch.empty((N * S, 3), device=dev).normal_(0.0, 1.0, generator=generator) if S else None
-        Pn = A + B + N * C
+        Pn = A + B + (N - 1) * E + N * C
         kinds = {"xyz": NV.RT_GROUP_XYZ, "scaling": NV.RT_GROUP_SCALING}
         plans, structs = [], []
         for group in self.optimizer.param_groups:

@@ -41,6 +41,9 @@ class TrainConfig:
     c2f_max_lowpass: float = 300.0
     warmup_iter: int = 0             # abe_split warm-up (train.py:38-39,138)
     ours: bool = False               # SH ramp from 5000 (train.py:79-85)
+    ours_new: bool = False           # --ours_new: SH ramp from 5000, learning-rate schedule shifted by
+                                     # warmup_iter (train.py:73-77; the reference's flag also sets
+                                     # warmup_iter = 10000, train.py:279-280)
     white_background: bool = False
     seed: int = 0
     densify: bool = True
@@ -222,8 +225,12 @@ class Trainer:
 
     def _low_pass_and_view(self, iteration):
         g, opt, cfg = self.g, self.opt, self.cfg
-        g.update_learning_rate(iteration)
-        if cfg.ours:
+        if cfg.ours_new:  # train.py:73-75: the schedule starts after the warm-up
+            if iteration >= cfg.warmup_iter:
+                g.update_learning_rate(iteration - cfg.warmup_iter)
+        else:
+            g.update_learning_rate(iteration)
+        if cfg.ours or cfg.ours_new:
             if iteration >= 5000 and iteration % 1000 == 0:
                 g.oneupSHdegree()
         elif iteration % 1000 == 0:

@@ -47,16 +47,19 @@ def _prime(g, seed):
     g.max_radii2D = torch.rand((P,), device="cuda", generator=gen) * 40
 
 
-@pytest.mark.parametrize("max_screen_size", [None, 20])
-def test_native_densify_matches_torch(max_screen_size):
+@pytest.mark.parametrize("max_screen_size,abe_split", [(None, False), (20, False), (None, True), (20, True)])
+def test_native_densify_matches_torch(max_screen_size, abe_split):
+    """abe_split: the RAIN-GS warm-up split (train.py:138-140, gaussian_model.py:342-364) — the
+    split Gaussians' copies at xyz * 0.3 * extent after the clones, and the reference's unused
+    normals drawn before the split's (the children match only if both sides draw them)."""
     P = 40_000
     a, b = _model(P, 3), _model(P, 3)
     _prime(a, 5)
     _prime(b, 5)
     a.native_densify = False
-    a.densify_and_prune(0.0002, 0.005, EXTENT, max_screen_size,
+    a.densify_and_prune(0.0002, 0.005, EXTENT, max_screen_size, abe_split=abe_split,
                         generator=torch.Generator(device="cuda").manual_seed(11))
-    b.densify_and_prune(0.0002, 0.005, EXTENT, max_screen_size,
+    b.densify_and_prune(0.0002, 0.005, EXTENT, max_screen_size, abe_split=abe_split,
                         generator=torch.Generator(device="cuda").manual_seed(11))
     Pn = a.get_xyz.shape[0]
     assert b.get_xyz.shape[0] == Pn and Pn != P
@@ -76,6 +79,37 @@ def test_native_densify_matches_torch(max_screen_size):
         assert any(pb is grp["params"][0] for grp in b.optimizer.param_groups)
     for t in (b.xyz_gradient_accum, b.denom, b.max_radii2D):
         assert t.shape[0] == Pn and float(t.abs().sum()) == 0.0
+
+
+def test_abe_split_rows_follow_the_reference_layout():
+    """Native abe_split: the rows after the clones are the split Gaussians' copies (xyz scaled by
+    0.3 * extent, the other raw parameters unchanged, zero moments), then the split children."""
+    P = 20_000
+    g = _model(P, 4)
+    _prime(g, 6)
+    raw = {n: p.detach().clone() for n, p in zip(PARAM_NAMES, g.params())}
+    grads = g.xyz_gradient_accum / g.denom
+    grads[grads.isnan()] = 0.0
+    smax = torch.exp(raw["scaling"]).max(dim=1).values
+    split = (grads.squeeze(1) >= 0.0002) & (smax > g.percent_dense * EXTENT)
+    clone = (torch.norm(grads, dim=-1) >= 0.0002) & (smax <= g.percent_dense * EXTENT)
+    op = torch.sigmoid(raw["opacity"]).squeeze(1)
+    keep_orig = ~split & (op >= 0.005)
+    keep_clone = clone & (op >= 0.005)
+    keep_abe = split & (op >= 0.005)  # max_screen_size None: opacity is the only prune
+    g.densify_and_prune(0.0002, 0.005, EXTENT, None, abe_split=True,
+                        generator=torch.Generator(device="cuda").manual_seed(2))
+    A, B, E = int(keep_orig.sum()), int(keep_clone.sum()), int(keep_abe.sum())
+    assert E > 0
+    new = {n: p.detach() for n, p in zip(PARAM_NAMES, g.params())}
+    abe = slice(A + B, A + B + E)
+    torch.testing.assert_close(new["xyz"][abe], raw["xyz"][keep_abe] * 0.3 * EXTENT, rtol=0, atol=0)
+    for n in ("f_dc", "f_rest", "opacity", "rotation"):
+        assert torch.equal(new[n][abe], raw[n][keep_abe]), n
+    torch.testing.assert_close(new["scaling"][abe], raw["scaling"][keep_abe], rtol=1e-6, atol=1e-7)
+    st = g.optimizer.state[g.params()[0]]
+    assert float(st["exp_avg"][abe].abs().sum()) == 0.0
+    assert new["xyz"].shape[0] == A + B + E + 2 * E  # children: the same opacity prune
 
 
 def test_native_densify_without_optimizer_state():

@@ -105,6 +105,36 @@ def test_densify_and_prune_bookkeeping(cpu_rasterizer):
     assert g.xyz_gradient_accum.shape == (P, 1) and g.max_radii2D.shape == (P,)
 
 
+def test_ours_new_warmup_abe_split_and_lr_shift(cpu_rasterizer):
+    """--ours_new (train.py:73-77, 138-140): during the warm-up the densify adds the abe copies of
+    the split Gaussians and the learning-rate schedule has not started; after it, the schedule runs
+    on iteration - warmup_iter."""
+    cams = cameras.fibonacci_cameras(8, 64, 48)
+    gts = [torch.rand(3, 48, 64, generator=torch.Generator().manual_seed(i)) for i in range(8)]
+    sizes = {}
+    for mode in ("plain", "ours_new"):
+        g = _model(2000, 1)
+        opt = OptimizationParams()
+        g.training_setup(opt)
+        lr0 = next(grp["lr"] for grp in g.optimizer.param_groups if grp["name"] == "xyz")
+        cfg = TrainConfig(c2f=False, ours_new=True, warmup_iter=700) if mode == "ours_new" else TrainConfig(c2f=False)
+        tr = Trainer(g, cams, gts, opt, PipelineParams(), cfg, scene_extent=4.4, loss_fn=_ref_loss)
+        opt.densify_grad_threshold = 1e-6  # force clones/splits on a tiny run
+        for it in range(595, 601):
+            info = tr.step(it)
+        assert info.densified
+        sizes[mode] = g.get_xyz.shape[0]
+        lr = next(grp["lr"] for grp in g.optimizer.param_groups if grp["name"] == "xyz")
+        if mode == "ours_new":
+            assert lr == lr0  # warm-up: update_learning_rate not called yet
+            tr.step(702)
+            lr = next(grp["lr"] for grp in g.optimizer.param_groups if grp["name"] == "xyz")
+            assert lr == g.xyz_scheduler_args(2)
+        else:
+            assert lr == g.xyz_scheduler_args(600)
+    assert sizes["ours_new"] > sizes["plain"]  # the abe copies (N - 1 = 1 per kept split Gaussian)
+
+
 # ---- view-sharded data parallel over gloo ------------------------------------------------
 
 def _scene():
