@@ -244,6 +244,10 @@ def main():
     # the reference's own timing bracket (train.py:71-117: iter_start before render, iter_end after
     # loss.backward()): render forward + L1/SSIM + backward, no optimizer step, no densification
     bracket_ms = _bracket(trainer, cams, gts, K if K < 50 else 50, world, dev)
+    # the RAIN-GS coarse-to-fine stress regime (train.py:95-107): the same bracket with the 2-D
+    # dilation the schedule applies early in training (up to c2f_max_lowpass = 300 px^2; radii of
+    # 52+ px and several times the pairs per frame)
+    c2f_ms = {str(lp): round(_bracket(trainer, cams, gts, 5, world, dev, low_pass=lp), 3) for lp in (30.0, 300.0)}
 
     # the same iteration through the reference's own API (what an unchanged train.py:109-147 runs):
     # render() -> GaussianRasterizer autograd -> getters' autograd -> torch.optim.Adam
@@ -286,6 +290,17 @@ def main():
                                          0.3)
             stats.append(_C.frame_stats(out[4], out[6], Pn, W, H))
     mean_stats = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
+    # the same frame statistics at the c2f stress dilation (first timed view)
+    c2f_stats = {}
+    with torch.no_grad():
+        s = _settings(cams[views_used[0]], gauss, bg)
+        act = (gauss.get_xyz, gauss.get_opacity, gauss.get_scaling, gauss.get_rotation, gauss.get_features)
+        e = torch.Tensor([])
+        for lp in (30.0, 300.0):
+            out = _C.rasterize_gaussians(s.bg, act[0], e, act[1], act[2], act[3], 1.0, e, s.viewmatrix,
+                                         s.projmatrix, s.tanfovx, s.tanfovy, H, W, act[4], D, s.campos, False, False,
+                                         lp)
+            c2f_stats[str(lp)] = {k: int(v) for k, v in _C.frame_stats(out[4], out[6], Pn, W, H).items()}
 
     roofline = None
     kernels = {}
@@ -369,6 +384,10 @@ def main():
         "views_per_s": round(iters_per_s, 3),  # one view per rank per step: = value
         "bracket_iters_per_s": round(world * 1000.0 / bracket_ms, 3),
         "bracket_ms": round(bracket_ms, 4),
+        "c2f_low_pass_bracket_ms": c2f_ms,
+        # num_rendered: the reference's bounding-square pair count; num_pairs: pairs after exact
+        # culling; num_binned: pairs the early-stop binning actually sorted and blended
+        "c2f_low_pass_frame_stats": c2f_stats,
         "api_iters_per_s": round(world * 1000.0 / api_ms, 3),
         "api_ms_per_step": round(api_ms, 4),
         "api_path": "unchanged train.py loop over this package's modules: render() -> GaussianRasterizer (autograd) "
@@ -391,9 +410,10 @@ def main():
         dist.destroy_process_group()
 
 
-def _bracket(trainer, cams, gts, n, world, dev):
+def _bracket(trainer, cams, gts, n, world, dev, low_pass=None):
     """ms per render-forward + loss + backward (the reference's iter_start..iter_end bracket,
-    train.py:71-117), max over ranks.  Gradients go to the parameters' .grad buffers; no Adam."""
+    train.py:71-117), max over ranks.  Gradients go to the parameters' .grad buffers; no Adam.
+    low_pass: the 2-D dilation to render with (default: the trainer's current one)."""
     import torch
     import torch.distributed as dist
 
@@ -408,7 +428,8 @@ def _bracket(trainer, cams, gts, n, world, dev):
     def one(i):
         nonlocal grads
         cam = cams[i % len(cams)]
-        image, _r, _d, st = fused.forward(g, cam, trainer.background, trainer.low_pass, cache=cache)
+        lp = trainer.low_pass if low_pass is None else low_pass
+        image, _r, _d, st = fused.forward(g, cam, trainer.background, lp, cache=cache)
         loss, _p, lws = l1_ssim_forward(image, gts[i % len(cams)], lam)
         dimg = l1_ssim_backward(image, gts[i % len(cams)], lam, lws)
         grads = dict(xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad,
