@@ -29,7 +29,13 @@ namespace rr {
 
 namespace {
 
-constexpr int kWaves = 4;       // waves per workgroup (unit)
+constexpr int kWaves = 4;       // waves per workgroup (unit) of the count kernel
+#ifndef RR_SORT_SW
+#define RR_SORT_SW 8
+#endif
+// waves per workgroup of the scatter (4 or 8): 8 halves each wave's serial rank rounds for the
+// same unit (depth sort 0.0913 -> 0.0877 ms/step, profiles/r03_sort_scatter8_ab.jsonl)
+constexpr int kScatterWaves = RR_SORT_SW;
 constexpr int kMaxRounds = 16;  // rounds of 64 items per wave
 constexpr int kMaxUnitItems = 64 * kWaves * kMaxRounds;  // 4096
 static_assert(kMaxUnitItems == kSortMaxUnit, "rr_kernels.hpp kSortMaxUnit");
@@ -160,8 +166,8 @@ __global__ __launch_bounds__(256) void k_rs_scan_rows(const uint32_t* __restrict
 // MAXR: rounds the kernel is compiled for (>= the call's rounds).  Small units get a small
 // instance: the LDS staging is sized by it, so e.g. the 512-item units of a 1M-key sort fit ~4x
 // more workgroups per CU than a 4096-item staging area allows.
-template <typename K, int MAXR, int DB>
-__global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict__ keys_in,
+template <typename K, int MAXR, int DB, int SW>
+__global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ keys_in,
                                                             const uint32_t* __restrict__ vals_in,
                                                             K* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
                                                             size_t n, int shift, int dbits, int rounds,
@@ -175,17 +181,17 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     constexpr int ND = 1 << DB;  // digits the kernel is compiled for (>= 1 << dbits)
     constexpr int DPL = ND / 64;  // digits per lane in the digit scans
     __shared__ uint32_t dbase[ND];         // first output slot of each digit
-    __shared__ uint32_t wcnt[kWaves][ND];  // per-wave digit counts, then per-wave cursors
+    __shared__ uint32_t wcnt[SW][ND];  // per-wave digit counts, then per-wave cursors
     __shared__ uint32_t dstart[ND];        // block-local start of each digit's run
     __shared__ uint32_t goff[ND];          // global slot of block-local position 0 of each digit's run
-    __shared__ uint32_t s_val[64 * kWaves * MAXR];
-    __shared__ K s_key[64 * kWaves * MAXR];
+    __shared__ uint32_t s_val[64 * SW * MAXR];
+    __shared__ K s_key[64 * SW * MAXR];
     __shared__ uint32_t s_nu;  // items staged (len minus the dropped ones)
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int ndig = 1 << dbits;
     const uint32_t mask = (uint32_t)ndig - 1u;
     const int unit = blockIdx.x;
-    const uint32_t unit_items = (uint32_t)rounds * 64 * kWaves;
+    const uint32_t unit_items = (uint32_t)rounds * 64 * SW;
     const size_t ubase = (size_t)unit * unit_items;
     const uint32_t len = unit_length(unit_len, n_dev, n, unit, unit_items);
     if (len == 0) return;  // empty unit (sparse producer / past the device-side count): no output
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     const uint32_t wl = (uint32_t)w * 64 * rounds;
     const size_t wbase = ubase + wl;
     for (int d = lane; d < ndig; d += 64) wcnt[w][d] = 0;
-    for (int d = t; d < ndig; d += 64 * kWaves) goff[d] = offsets[(size_t)d * units + unit];
+    for (int d = t; d < ndig; d += 64 * SW) goff[d] = offsets[(size_t)d * units + unit];
     if (w == 1) {  // digit bases: exclusive scan of the digit totals (DPL per lane, then shuffles)
         uint32_t tv[DPL], sum = 0;
 #pragma unroll
@@ -247,7 +253,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
             tot[i] = 0;
             if (d < ndig)
 #pragma unroll
-                for (int v = 0; v < kWaves; v++) tot[i] += wcnt[v][d];
+                for (int v = 0; v < SW; v++) tot[i] += wcnt[v][d];
             sum += tot[i];
         }
         uint32_t incl = sum;
@@ -265,7 +271,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
                 goff[d] += dbase[d] - run;
                 uint32_t r2 = run;
 #pragma unroll
-                for (int v = 0; v < kWaves; v++) {
+                for (int v = 0; v < SW; v++) {
                     const uint32_t x = wcnt[v][d];
                     wcnt[v][d] = r2;
                     r2 += x;
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_scatter(const K* __restrict_
     }
     __syncthreads();
     const int nu = (int)s_nu;
-    for (int j = t; j < nu; j += 64 * kWaves) {
+    for (int j = t; j < nu; j += 64 * SW) {
         const K k = s_key[j];
         const uint32_t d = ((uint32_t)k >> shift) & mask;
         const uint32_t pos = goff[d] + (uint32_t)j;
@@ -326,7 +332,10 @@ struct SortLayout {
 // units (rr_set_tuning "sort_min_units"; interleaved A/B on the bench step: with 8-bit digits 512
 // beat 1024 by 1.7%; the 3-pass 9-bit depth sort of 1M keys: 0.100 ms/step with 256 (2048-item
 // units), 0.109 with 128 or 512, 0.132 with 1024)
-constexpr int kMinUnitsDefault = 256;
+// With the 8-wave scatter (round 3) the depth sort prefers its largest units: 128 (4096-item
+// units, 245 for 1M keys) 0.086 vs 0.088 ms/step with 256 and 0.102 with 512; the bin sorts keep
+// 1024 (512: 0.090 / 2048: 0.093 duplicate vs 0.086), profiles/r03_sort_units_ab.jsonl
+constexpr int kMinUnitsDefault = 128;
 // Sorts of <= 16-bit keys (the bin sorts) target more, smaller units: their first pass's units are
 // the duplicate's windows, whose workgroups are latency-bound (interleaved A/B on the bench step:
 // duplicate 0.098 -> 0.092, bin sort 0.087 -> 0.077 ms/step with 1024; the depth sort keeps
@@ -442,15 +451,24 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                                                                  p == 0 && kept ? 1 : 0);
         }
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
-        auto scatter = dbits > 8 ? (rounds <= 2   ? k_rs_scatter<K, 2, 9>
-                                    : rounds <= 4 ? k_rs_scatter<K, 4, 9>
-                                    : rounds <= 8 ? k_rs_scatter<K, 8, 9>
-                                                  : k_rs_scatter<K, kMaxRounds, 9>)
-                                 : (rounds <= 2   ? k_rs_scatter<K, 2, 8>
-                                    : rounds <= 4 ? k_rs_scatter<K, 4, 8>
-                                    : rounds <= 8 ? k_rs_scatter<K, 8, 8>
-                                                  : k_rs_scatter<K, kMaxRounds, 8>);
-        scatter<<<units, 64 * kWaves, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rounds, s.offsets, units,
+        // the scatter ranks a unit with kScatterWaves waves (the same unit_items: rounds_s rounds
+        // per wave) where the unit has at least 2 count rounds
+        const int sw = (rounds >= 2 && kScatterWaves == 8) ? 8 : 4;
+        const int rs = rounds * kWaves / sw;
+        auto scatter =
+            sw == 8 ? (dbits > 8 ? (rs <= 2 ? k_rs_scatter<K, 2, 9, 8> : rs <= 4 ? k_rs_scatter<K, 4, 9, 8>
+                                                                        : k_rs_scatter<K, 8, 9, 8>)
+                                 : (rs <= 2 ? k_rs_scatter<K, 2, 8, 8> : rs <= 4 ? k_rs_scatter<K, 4, 8, 8>
+                                                                        : k_rs_scatter<K, 8, 8, 8>))
+                    : (dbits > 8 ? (rs <= 2   ? k_rs_scatter<K, 2, 9, 4>
+                                    : rs <= 4 ? k_rs_scatter<K, 4, 9, 4>
+                                    : rs <= 8 ? k_rs_scatter<K, 8, 9, 4>
+                                              : k_rs_scatter<K, kMaxRounds, 9, 4>)
+                                 : (rs <= 2   ? k_rs_scatter<K, 2, 8, 4>
+                                    : rs <= 4 ? k_rs_scatter<K, 4, 8, 4>
+                                    : rs <= 8 ? k_rs_scatter<K, 8, 8, 4>
+                                              : k_rs_scatter<K, kMaxRounds, 8, 4>));
+        scatter<<<units, 64 * sw, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rs, s.offsets, units,
                                                s.totals, p == 0 ? unit_len : nullptr, p > 0 && kept ? kept : n_dev,
                                                last ? gather_src : nullptr, last ? gather_dst : nullptr,
                                                p == 0 && kept ? 1 : 0, p == 0 ? kept : nullptr);

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--points", type=int, default=1_000_000)
     ap.add_argument("--api", action="store_true", help="also time the reference-API step (Trainer(fused=False))")
     ap.add_argument("--pack", action="store_true", help="parameters and moments in three flat buffers (pack_flat_state)")
+    ap.add_argument("--tune", action="append", default=[], help="rr_set_tuning key=value (repeatable)")
     a = ap.parse_args()
     import torch
 
@@ -31,6 +32,9 @@ def main():
     from rain_amd.renderer import PipelineParams, render
     from rain_amd.train import TrainConfig, Trainer
 
+    for kv in a.tune:
+        k, v = kv.split("=")
+        _native.check(_native.raster().rr_set_tuning(k.encode(), int(v)), "rr_set_tuning " + kv)
     dev = torch.device("cuda:0")
     cams = [c.to(dev) for c in fibonacci_cameras(200, 1920, 1080)]
     gm = GaussianModel(3, device=dev)
