@@ -355,7 +355,7 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *                         env RAIN_FWD_TILE_ORDER),
  *   "fwd_waves" / "bwd_waves" as rr_set_blend_config,
  *   "fwd_b_waves"    0/1  phase-B forward blend on 4 waves per tile (default 1),
- *   "sort_min_units" n    radix sorts pick the largest unit with >= n units (default 256; 0 resets),
+ *   "sort_min_units" n    radix sorts pick the largest unit with >= n units (default 128; 0 resets),
  *   "sort_min_units_tile" n  the same for the bin sorts (<= 16-bit keys; default 1024),
  *   "sort_max_rounds" r   cap on 64-item rounds per wave in a sort unit, 1..16 (default 16),
  *   "pair_scan_direct_blocks" n  pair-count scans of up to n blocks of 2048 Gaussians let every

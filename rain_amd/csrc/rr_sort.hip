@@ -339,7 +339,7 @@ constexpr int kMinUnitsDefault = 128;
 // Sorts of <= 16-bit keys (the bin sorts) target more, smaller units: their first pass's units are
 // the duplicate's windows, whose workgroups are latency-bound (interleaved A/B on the bench step:
 // duplicate 0.098 -> 0.092, bin sort 0.087 -> 0.077 ms/step with 1024; the depth sort keeps
-// kMinUnitsDefault = 256: 0.109 vs 0.129 ms with 1024)
+// kMinUnitsDefault (128 since the 8-wave scatter; 0.109 vs 0.129 ms with 1024 back at 256))
 constexpr int kMinUnitsTileDefault = 1024;
 int g_min_units = kMinUnitsDefault;
 int g_min_units_tile = kMinUnitsTileDefault;

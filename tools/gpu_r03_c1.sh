@@ -1,0 +1,18 @@
+# round-3 continuation: HEAD's full -m gpu suite, smoke and default bench
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > gpurun_out/r03_c1_suite.log 2>&1
+rc=$?; tail -3 gpurun_out/r03_c1_suite.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_c1_smoke.log 2>&1 || { tail -20 gpurun_out/r03_c1_smoke.log; exit 1; }
+tail -1 gpurun_out/r03_c1_smoke.log
+timeout -k 10 400 python -u bench.py > gpurun_out/r03_c1_bench.json 2> gpurun_out/r03_c1_bench.err || { tail -20 gpurun_out/r03_c1_bench.err; exit 1; }
+python3 - <<'P'
+import json
+d = json.loads(open("gpurun_out/r03_c1_bench.json").read().strip().splitlines()[-1])
+r = d["roofline"]
+print(d["value"], d["ms_per_step"], "densify", d.get("densify_iter_ms"), "api", d["api_iters_per_s"])
+print({k: r[k] for k in ("kernel", "achieved", "frac", "measured_copy_GBps", "measured_rmw_GBps")})
+print({k: round(v["ms_per_step"], 4) for k, v in d["kernels"].items()})
+print("blend_bwd", r["blend_bwd"], "blend_fwd", r["blend_fwd"])
+P
