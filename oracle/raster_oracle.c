@@ -189,13 +189,16 @@ static void cov2d_setup(f3 mean, float fx, float fy, float tanfovx, float tanfov
     c->V[2][0] = cov3D[2]; c->V[2][1] = cov3D[4]; c->V[2][2] = cov3D[5];
 }
 
-/* cov = A V A^T (upper 2x2), before the low-pass dilation */
+/* cov = A V A^T (upper 2x2), before the low-pass dilation, in glm's association of
+ * transpose(T) * transpose(Vrk) * T (forward.cu:95, backward.cu:184): (T^T Vrk^T)[k][r] = B[r][k] and
+ * cov[c][r] = sum_k B[r][k] * A[c][k] (k = 0, 1, 2 left to right), so the off-diagonal the reference
+ * returns, cov[0][1], is B[1] . A[0]. */
 static void cov2d_eval(const cov2d_ctx* c, float* a, float* b, float* cc) {
     float B[2][3];
     for (int i = 0; i < 2; i++)
         for (int j = 0; j < 3; j++) B[i][j] = c->A[i][0] * c->V[0][j] + c->A[i][1] * c->V[1][j] + c->A[i][2] * c->V[2][j];
     *a = B[0][0] * c->A[0][0] + B[0][1] * c->A[0][1] + B[0][2] * c->A[0][2];
-    *b = B[0][0] * c->A[1][0] + B[0][1] * c->A[1][1] + B[0][2] * c->A[1][2];
+    *b = B[1][0] * c->A[0][0] + B[1][1] * c->A[0][1] + B[1][2] * c->A[0][2];
     *cc = B[1][0] * c->A[1][0] + B[1][1] * c->A[1][1] + B[1][2] * c->A[1][2];
 }
 

@@ -303,7 +303,9 @@ __device__ __forceinline__ Proj2D ewa_setup(v3 mean, float fx, float fy, float t
     }
     return p;
 }
-// (a, b, c) of A V A^T before dilation.
+// (a, b, c) of A V A^T before dilation, associated as glm evaluates transpose(T) * transpose(Vrk) * T
+// (forward.cu:95): B = A V is (T^T Vrk^T)[k][r] = B[r][k], and cov[c][r] = sum_k B[r][k] A[c][k], so
+// the returned cov[0][1] is B[1] . A[0] (not B[0] . A[1], equal only in exact arithmetic).
 __device__ __forceinline__ void ewa_cov2d(const Proj2D& p, const float cov[6], float& a, float& b, float& c) {
     const float V[3][3] = {{cov[0], cov[1], cov[2]}, {cov[1], cov[3], cov[4]}, {cov[2], cov[4], cov[5]}};
     float B[2][3];
@@ -312,7 +314,7 @@ __device__ __forceinline__ void ewa_cov2d(const Proj2D& p, const float cov[6], f
 #pragma unroll
         for (int j = 0; j < 3; j++) B[i][j] = p.A[i][0] * V[0][j] + p.A[i][1] * V[1][j] + p.A[i][2] * V[2][j];
     a = B[0][0] * p.A[0][0] + B[0][1] * p.A[0][1] + B[0][2] * p.A[0][2];
-    b = B[0][0] * p.A[1][0] + B[0][1] * p.A[1][1] + B[0][2] * p.A[1][2];
+    b = B[1][0] * p.A[0][0] + B[1][1] * p.A[0][1] + B[1][2] * p.A[0][2];
     c = B[1][0] * p.A[1][0] + B[1][1] * p.A[1][1] + B[1][2] * p.A[1][2];
 }
 

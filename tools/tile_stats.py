@@ -22,7 +22,7 @@ def main():
     params = synthetic.random_gaussians(1_000_000, sh_degree=3, seed=0, bench=True, device=dev)
     act = synthetic.activated(params)
     cams = [c.to(dev) for c in fibonacci_cameras(200, 1920, 1080)]
-    out = {}
+    out, arrays = {}, {}
     for v in (0, 17, 101):
         s = synthetic.settings_for(cams[v], 3, torch.zeros(3, device=dev))
         e = torch.Tensor([])
@@ -37,7 +37,10 @@ def main():
         out[v] = dict(pairs=dict(sum=int(n.sum()), mean=float(n.mean()), pct=q(n)),
                       tile_max=dict(sum=int(tm.sum()), mean=float(tm.mean()), pct=q(tm),
                                     top16=sorted(tm.tolist())[-16:]))
+        arrays[f"tile_max_{v}"] = tm
     print(json.dumps(out, indent=1))
+    if len(sys.argv) > 1:  # per-tile arrays for offline schedule models
+        np.savez_compressed(sys.argv[1], **arrays)
 
 
 if __name__ == "__main__":
