@@ -128,11 +128,10 @@ struct Img {
     uint2* ranges;      // phase-A (or single-phase) lists; ranges_b and counters follow it
     uint2* ranges_b;    // phase-B lists of early-stop binning (all {0,0} otherwise)
     uint32_t* counters; // [0] = phase-B pair count (device-side)
-    size_t zero_bytes;  // ranges .. counters: cleared before every render
+    size_t zero_bytes;  // ranges .. open_bits: cleared before every render
     uint32_t* tile_max;
     uint8_t* open;      // [T] tile still open after phase A
-    uint32_t* sat;      // [(gy+1)*(gx+1)] 2-D prefix sum of open
-    uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask
+    uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask (in the zeroed block; the phase-A blend sets it)
     uint32_t* order;      // [T] backward blend dispatch order (heaviest tiles first)
     size_t total;
 };
@@ -143,14 +142,15 @@ Img carve_img(void* buf, int W, int H) {
     const size_t T = (size_t)std::max(grid_x(W) * grid_y(H), 1);
     m.final_T = c.take<float>(N);
     m.n_contrib = c.take<uint32_t>(N);
-    m.ranges = c.take<uint2>(2 * T + 2);  // one block: ranges [T], ranges_b [T], counters [4]
+    // one block: ranges [T], ranges_b [T], counters [4], open_bits [ceil(T/32)]
+    const size_t nbits = ((size_t)T + 31) / 32;
+    m.ranges = c.take<uint2>(2 * (size_t)T + 2 + (nbits + 1) / 2);
     m.ranges_b = m.ranges ? m.ranges + T : nullptr;
     m.counters = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T) : nullptr;
-    m.zero_bytes = (2 * T + 2) * sizeof(uint2);
+    m.open_bits = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T + 2) : nullptr;
+    m.zero_bytes = (2 * (size_t)T + 2 + (nbits + 1) / 2) * sizeof(uint2);
     m.tile_max = c.take<uint32_t>(T);
     m.open = c.take<uint8_t>(T);
-    m.sat = c.take<uint32_t>((size_t)(grid_x(W) + 1) * (grid_y(H) + 1));
-    m.open_bits = c.take<uint32_t>((T + 31) / 32);
     m.order = c.take<uint32_t>(T);
     m.total = align_up(c.off);
     return m;
@@ -351,6 +351,9 @@ hipError_t pair_counts_copy(const unsigned long long* src, uint2* out, bool* wid
 }
 
 thread_local int64_t g_wait_ns = 0, g_waits = 0;
+#ifndef RR_WAIT_QUERY_MS
+#define RR_WAIT_QUERY_MS 20
+#endif
 struct WaitClock {  // adds the scope's duration to the host-wait statistics
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     ~WaitClock() {
@@ -370,7 +373,10 @@ hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, bool* wide, hipS
             *wide = __atomic_load_n(mb.host + 3, __ATOMIC_RELAXED) != 0;
             return hipSuccess;
         }
-        if ((spin & 4095u) == 0) {
+        // the stream is queried only once the wait has outlasted any frame (RR_WAIT_QUERY_MS): a query
+        // while the device is still busy with this frame is not free on the device side
+        if ((spin & 4095u) == 0 &&
+            std::chrono::steady_clock::now() - clock.t0 > std::chrono::milliseconds(RR_WAIT_QUERY_MS)) {
             const hipError_t q = hipStreamQuery(st);
             if (q == hipSuccess) {
                 if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) continue;
@@ -573,10 +579,9 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     // phase B: pairs [LA, L), only for tiles phase A left open; positions LA.. of the arrays
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
-        launch_open_sat(gx, gy, im.open, im.sat, im.open_bits, st);
         d.first = bn.first + pa.units; d.pair0 = LA; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units; d.L = L;
         d.keys = keys + LA; d.vals = bn.vals + LA; d.dbits = pb.dbits0; d.counts = pb.counts;
-        d.sat = im.sat; d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
+        d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
         d.zero = nullptr; d.nzero = 0;
         d.starts_done = starts_b;
         launch_duplicate<K>(d, st);
@@ -691,7 +696,7 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
     }
     BlendFwdArgs b{};
     b.W = W; b.H = H; b.gx = gx; b.gy = gy;
-    b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.open = im.open;
+    b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.open = im.open; b.open_bits = im.open_bits;
     b.point_list = bn.point_list; b.splats = gm.splats; b.bg = cam->background;
     b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
     b.out_color = out_color; b.out_depth = out_depth;

@@ -242,7 +242,12 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
         for (int k = 0; k < PIX; k++) any_open |= T[k] > 0.f;
         const bool tile_open = NW == 1 ? __builtin_amdgcn_ballot_w64(any_open) != 0
                                        : __syncthreads_or(any_open) != 0;
-        if (threadIdx.x == 0) a.open[tile] = tile_open ? 1 : 0;
+        if (threadIdx.x == 0) {
+            a.open[tile] = tile_open ? 1 : 0;
+            // phase B's open-tile bitmask (zeroed with the frame's ranges): replaces a one-workgroup
+            // pass over the flags between the two phases
+            if (tile_open) atomicOr(&a.open_bits[tile >> 5], 1u << (tile & 31));
+        }
         if (tile_open) {
 #pragma unroll
             for (int k = 0; k < PIX; k++) {

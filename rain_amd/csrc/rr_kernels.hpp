@@ -129,6 +129,7 @@ struct BlendFwdArgs {
     float* out_depth;
     const uint2* ranges_b;  // phase B lists
     uint8_t* open;          // [T] tile still open after phase A
+    uint32_t* open_bits;    // [ceil(T/32)] the same as a bitmask (cleared with the ranges; phase A ORs)
     int phase;              // BlendPhase
     const float4* normals;  // aux normal output (RR_FLAG_AUX_NORMAL): per-Gaussian normals and
     float* out_normal;      // the blended normal map [3,H,W]; both null otherwise
@@ -232,7 +233,6 @@ struct DupArgs {
     int dbits;           // first-pass digit width of the tile sort
     uint32_t* counts;    // its per-window digit counts
     // phase B (early-stop binning); all null for an unfiltered pass
-    const uint32_t* sat;
     const uint32_t* open_bits;
     uint32_t* unit_len;
     uint32_t* n_total;
@@ -252,7 +252,6 @@ struct DupArgs {
 // returns whether the window starts (both sets) were computed
 template <typename K>
 bool launch_duplicate(const DupArgs<K>& d, hipStream_t st);
-void launch_open_sat(int gx, int gy, const uint8_t* open, uint32_t* sat, uint32_t* open_bits, hipStream_t st);
 template <typename K>
 void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,
                    uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, hipStream_t st);
