@@ -30,6 +30,14 @@ int rl_l1_ssim_forward(const float* img, const float* gt, int C, int H, int W, f
 int rl_l1_ssim_backward(const float* img, const float* gt, int C, int H, int W, float lambda, const float* window,
                         const void* workspace, const float* grad_loss, float* dimg, void* stream);
 
+/* Forward and backward in one call, for a caller that needs both at once (a training step):
+ * loss / parts exactly as rl_l1_ssim_forward, dimg exactly as rl_l1_ssim_backward; the finalize of
+ * the loss rides on the backward launch (one launch less).  Not in the reference: its loss is
+ * autograd over utils/loss_utils.py:22-53; this entry is the fused step's shortcut. */
+int rl_l1_ssim_forward_backward(const float* img, const float* gt, int C, int H, int W, float lambda,
+                                const float* window, void* workspace, size_t workspace_bytes, float* loss,
+                                float* parts, const float* grad_loss, float* dimg, void* stream);
+
 const char* rl_last_error(void);
 
 #ifdef __cplusplus

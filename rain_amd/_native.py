@@ -183,7 +183,8 @@ def raster():
 
 
 LOSS_LIB = os.environ.get("RAIN_LOSS_LIB") or os.path.join(LIB_DIR, "librain_loss.so")
-LOSS_SYMBOLS = ["rl_workspace_bytes", "rl_l1_ssim_forward", "rl_l1_ssim_backward", "rl_last_error"]
+LOSS_SYMBOLS = ["rl_workspace_bytes", "rl_l1_ssim_forward", "rl_l1_ssim_backward", "rl_l1_ssim_forward_backward",
+                "rl_last_error"]
 _loss = None
 
 
@@ -198,6 +199,9 @@ def loss_lib():
         L.rl_l1_ssim_forward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, ctypes.c_size_t, vp, vp, vp]
         L.rl_l1_ssim_backward.restype = ci
         L.rl_l1_ssim_backward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, vp, vp, vp]
+        L.rl_l1_ssim_forward_backward.restype = ci
+        L.rl_l1_ssim_forward_backward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, ctypes.c_size_t, vp,
+                                                  vp, vp, vp, vp]
         L.rl_last_error.restype = ctypes.c_char_p
         _loss = L
     return _loss

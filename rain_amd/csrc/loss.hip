@@ -271,12 +271,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
 // its loads are all in flight (a single chain of dependent adds made this a 25 us latency-bound
 // kernel).  Fixed summation order: the result is deterministic.
 constexpr int kFinT = 1024;
-__global__ __launch_bounds__(kFinT) void k_loss_finalize(const float2* __restrict__ partial, int nb, float lambda,
-                                                         float inv_n, float* __restrict__ loss,
-                                                         float* __restrict__ parts) {
-    __shared__ double rs[kFinT / 64], rl[kFinT / 64];
+// Thread i's two sums of the fixed-order reduction, then its wave's butterfly (shared by the
+// 1024-thread kernel and the one-wave form that rides on the backward launch: same order, same bits).
+__device__ __forceinline__ void finalize_wave_sums(const float2* __restrict__ partial, int nb, int i, double& ss,
+                                                   double& ll) {
     double s[4] = {0.0, 0.0, 0.0, 0.0}, l[4] = {0.0, 0.0, 0.0, 0.0};
-    int i = threadIdx.x;
     for (; i + 3 * kFinT < nb; i += 4 * kFinT) {
         float2 v[4];
 #pragma unroll
@@ -291,12 +290,33 @@ __global__ __launch_bounds__(kFinT) void k_loss_finalize(const float2* __restric
         s[k] += partial[i].x;
         l[k] += partial[i].y;
     }
-    double ss = (s[0] + s[1]) + (s[2] + s[3]), ll = (l[0] + l[1]) + (l[2] + l[3]);
+    ss = (s[0] + s[1]) + (s[2] + s[3]);
+    ll = (l[0] + l[1]) + (l[2] + l[3]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         ss += __shfl_xor(ss, o);
         ll += __shfl_xor(ll, o);
     }
+}
+// S, Lv: the 16 wave totals added in wave order
+__device__ __forceinline__ void finalize_store(double S, double Lv, float lambda, float inv_n, float* __restrict__ loss,
+                                               float* __restrict__ parts) {
+    const float ssim = (float)(S * inv_n);
+    const float l1 = (float)(Lv * inv_n);
+    const float total = (1.0f - lambda) * l1 + lambda * (1.0f - ssim);
+    loss[0] = total;
+    if (parts) {
+        parts[0] = total;
+        parts[1] = l1;
+        parts[2] = ssim;
+    }
+}
+__global__ __launch_bounds__(kFinT) void k_loss_finalize(const float2* __restrict__ partial, int nb, float lambda,
+                                                         float inv_n, float* __restrict__ loss,
+                                                         float* __restrict__ parts) {
+    __shared__ double rs[kFinT / 64], rl[kFinT / 64];
+    double ss, ll;
+    finalize_wave_sums(partial, nb, threadIdx.x, ss, ll);
     if ((threadIdx.x & 63) == 0) {
         rs[threadIdx.x >> 6] = ss;
         rl[threadIdx.x >> 6] = ll;
@@ -308,16 +328,21 @@ __global__ __launch_bounds__(kFinT) void k_loss_finalize(const float2* __restric
             S += rs[w];
             Lv += rl[w];
         }
-        const float ssim = (float)(S * inv_n);
-        const float l1 = (float)(Lv * inv_n);
-        const float total = (1.0f - lambda) * l1 + lambda * (1.0f - ssim);
-        loss[0] = total;
-        if (parts) {
-            parts[0] = total;
-            parts[1] = l1;
-            parts[2] = ssim;
-        }
+        finalize_store(S, Lv, lambda, inv_n, loss, parts);
     }
+}
+// The same reduction by ONE wave standing in for the 16 waves in turn (an extra workgroup of the
+// backward launch in rl_l1_ssim_forward_backward: one launch less per training step).
+__device__ void loss_finalize_one_wave(const float2* __restrict__ partial, int nb, float lambda, float inv_n,
+                                       float* __restrict__ loss, float* __restrict__ parts) {
+    double S = 0.0, Lv = 0.0;
+    for (int w = 0; w < kFinT / 64; w++) {
+        double ss, ll;
+        finalize_wave_sums(partial, nb, w * 64 + (int)threadIdx.x, ss, ll);
+        S += ss;  // the butterfly left every lane with the wave total: the same additions in order
+        Lv += ll;
+    }
+    if (threadIdx.x == 0) finalize_store(S, Lv, lambda, inv_n, loss, parts);
 }
 
 // Backward: the same streamed walk over the three forward maps (G1, G11, G12): horizontal pass
@@ -328,7 +353,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                                  int W, float lambda, float inv_n, Win win,
                                                  const float* __restrict__ g1, const float* __restrict__ g11,
                                                  const float* __restrict__ g12, const float* __restrict__ grad_loss,
-                                                 float* __restrict__ dimg) {
+                                                 float* __restrict__ dimg, const float2* __restrict__ partial,
+                                                 int nb, float* __restrict__ loss, float* __restrict__ parts) {
+    if (loss && blockIdx.x == gridDim.x - 1) {  // the extra column (block-uniform): the forward's finalize
+        if (blockIdx.y == 0 && blockIdx.z == 0) loss_finalize_one_wave(partial, nb, lambda, inv_n, loss, parts);
+        return;
+    }
     __shared__ float sg[3][NR][PW];
     const int c = blockIdx.z;
     const int x0 = blockIdx.x * TW - R, y0 = blockIdx.y * TH - R;
@@ -455,10 +485,47 @@ int rl_l1_ssim_backward(const float* img, const float* gt, int C, int H, int W, 
     const float inv_n = (float)(1.0 / (double)n);
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((W + TW - 1) / TW, (H + TH_BWD - 1) / TH_BWD, C);
-    k_ssim_bwd<TH_BWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg);
+    k_ssim_bwd<TH_BWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg,
+                                            nullptr, 0, nullptr, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("rl_l1_ssim_backward: ") + hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+int rl_l1_ssim_forward_backward(const float* img, const float* gt, int C, int H, int W, float lambda,
+                                const float* window, void* workspace, size_t workspace_bytes, float* loss,
+                                float* parts, const float* grad_loss, float* dimg, void* stream) {
+    if (!img || !gt || !window || !workspace || !loss || !grad_loss || !dimg || C <= 0 || H <= 0 || W <= 0) {
+        g_err = "rl_l1_ssim_forward_backward: bad argument";
+        return 1;
+    }
+    if ((size_t)H * W * 4 >= (size_t)kOOB) {
+        g_err = "rl_l1_ssim_forward_backward: image plane larger than 2^30 bytes";
+        return 1;
+    }
+    if (workspace_bytes < rl_workspace_bytes(C, H, W) || nblocks(C, H, W) > NB_MAX) {
+        g_err = "rl_l1_ssim_forward_backward: workspace too small";
+        return 3;
+    }
+    Win win;
+    for (int i = 0; i < 11; i++) win.w[i] = window[i];
+    const size_t n = (size_t)C * H * W;
+    float* g1 = static_cast<float*>(workspace);
+    float2* partial = reinterpret_cast<float2*>(g1 + 3 * n);
+    const float inv_n = (float)(1.0 / (double)n);
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 gf((W + TW - 1) / TW, (H + TH_FWD - 1) / TH_FWD, C);
+    k_ssim_fwd<TH_FWD><<<gf, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, partial);
+    // one extra column of the backward grid finalizes the loss (bitwise rl_l1_ssim_forward's)
+    const dim3 gb((W + TW - 1) / TW + 1, (H + TH_BWD - 1) / TH_BWD, C);
+    k_ssim_bwd<TH_BWD><<<gb, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg,
+                                          partial, nblocks(C, H, W), loss, parts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = std::string("rl_l1_ssim_forward_backward: ") + hipGetErrorString(e);
         return 2;
     }
     return 0;

@@ -89,6 +89,30 @@ def l1_ssim_backward(img, gt, lambda_dssim, ws, grad_loss=None):
     return dimg
 
 
+def l1_ssim_forward_backward(img, gt, lambda_dssim, grad_loss=None):
+    """Forward and backward at once (the training step's form): (loss, parts, dimg), bitwise
+    l1_ssim_forward's loss / parts and l1_ssim_backward's dimg, in two launches instead of three."""
+    from . import _native as N
+
+    L = N.loss_lib()
+    img = img.contiguous()
+    gt = gt.contiguous()
+    C, H, W = img.shape[-3:]
+    ws = torch.empty((L.rl_workspace_bytes(C, H, W),), dtype=torch.uint8, device=img.device)
+    loss = torch.empty((), dtype=torch.float32, device=img.device)
+    parts = torch.empty((3,), dtype=torch.float32, device=img.device)
+    dimg = torch.empty_like(img)
+    if grad_loss is None:
+        grad_loss = _ones(img.device)
+    g = grad_loss.reshape(1).contiguous().float()
+    rc = L.rl_l1_ssim_forward_backward(img.data_ptr(), gt.data_ptr(), C, H, W, float(lambda_dssim), _window_host(),
+                                       ws.data_ptr(), ws.numel(), loss.data_ptr(), parts.data_ptr(), g.data_ptr(),
+                                       dimg.data_ptr(), N.stream_of(img))
+    if rc:
+        raise RuntimeError(L.rl_last_error().decode())
+    return loss, parts, dimg
+
+
 class _FusedL1SSIM(torch.autograd.Function):
     """(1-λ)·L1 + λ·(1-SSIM) in two HIP kernels (rain_amd/csrc/loss.hip, include/rain_loss.h)."""
 

@@ -289,7 +289,7 @@ class Trainer:
         densify iteration the reference's optimizer.step() finds only replaced parameters (no step),
         on a reset-only iteration it steps every group but the replaced opacity."""
         from .diff_gaussian_rasterization import _C
-        from .loss import l1_ssim_backward, l1_ssim_forward
+        from .loss import l1_ssim_forward_backward
 
         g, opt = self.g, self.opt
         vidx, _cam = self._low_pass_and_view(iteration)
@@ -304,8 +304,8 @@ class Trainer:
         lam = opt.lambda_dssim
 
         def loss_fn(image):
-            loss, _parts, lws = l1_ssim_forward(image, gt, lam)
-            return l1_ssim_backward(image, gt, lam, lws), loss
+            loss, _parts, dimg = l1_ssim_forward_backward(image, gt, lam)
+            return dimg, loss
 
         with torch.no_grad():
             _image, loss = self._owner.step(g, cams, self.background, self.low_pass, _C.frame_flags(), loss_fn, adam,
@@ -330,7 +330,7 @@ class Trainer:
 
     def _step_fused(self, iteration: int, sync_loss: bool) -> StepInfo:
         from . import fused
-        from .loss import l1_ssim_backward, l1_ssim_forward
+        from .loss import l1_ssim_forward_backward
 
         if self._owner is not None:
             return self._step_owner(iteration, sync_loss)
@@ -353,8 +353,8 @@ class Trainer:
             image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass,
                                                      cache=self._bin_cache if self.reuse_binning else None)
             gt = self.gt[vidx]
-            loss, _parts, lws = l1_ssim_forward(image, gt, opt.lambda_dssim)
-            dimg = l1_ssim_backward(image, gt, opt.lambda_dssim, lws)
+            # loss and dL/dimage in one call (bitwise the separate forward / backward)
+            loss, _parts, dimg = l1_ssim_forward_backward(image, gt, opt.lambda_dssim)
             grads = None if fuse_adam else dict(
                 xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad, opacity=g._opacity.grad,
                 scaling=g._scaling.grad, rotation=g._rotation.grad)

@@ -39,3 +39,22 @@ def test_fused_loss_grad_scale(gpu):
     l2, _ = fused_l1_ssim_loss(x2, gt)
     l2.backward()
     torch.testing.assert_close(x1.grad, 3.0 * x2.grad, rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("H,W", [(75, 100), (9, 200), (1080, 1920)])
+def test_forward_backward_in_one_call_is_bitwise_the_two_calls(gpu, H, W):
+    """rl_l1_ssim_forward_backward (the training step's form: the loss finalize rides on the
+    backward launch) gives bitwise the loss / parts of rl_l1_ssim_forward and the dimg of
+    rl_l1_ssim_backward, also with a grad_loss scale."""
+    from rain_amd.loss import l1_ssim_backward, l1_ssim_forward, l1_ssim_forward_backward
+
+    g = torch.Generator().manual_seed(7 * H + W)
+    img = torch.rand((3, H, W), generator=g).to(gpu)
+    gt = (img.cpu() * 0.6 + 0.4 * torch.rand((3, H, W), generator=g)).to(gpu)
+    for scale in (None, 2.5):
+        gl = None if scale is None else torch.tensor([scale], device=gpu)
+        loss, parts, ws = l1_ssim_forward(img, gt, 0.2)
+        dimg = l1_ssim_backward(img, gt, 0.2, ws, gl)
+        loss2, parts2, dimg2 = l1_ssim_forward_backward(img, gt, 0.2, gl)
+        assert torch.equal(loss, loss2) and torch.equal(parts, parts2)
+        assert torch.equal(dimg, dimg2)

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--api", action="store_true", help="also time the reference-API step (Trainer(fused=False))")
     ap.add_argument("--pack", action="store_true", help="parameters and moments in three flat buffers (pack_flat_state)")
     ap.add_argument("--tune", action="append", default=[], help="rr_set_tuning key=value (repeatable)")
+    ap.add_argument("--loss-split", action="store_true",
+                    help="the trainer's loss as two calls (forward, backward) instead of rl_l1_ssim_forward_backward")
     a = ap.parse_args()
     import torch
 
@@ -32,6 +34,14 @@ def main():
     from rain_amd.renderer import PipelineParams, render
     from rain_amd.train import TrainConfig, Trainer
 
+    if a.loss_split:
+        import rain_amd.loss as RL
+
+        def split(img, gt, lam, grad_loss=None):
+            loss, parts, ws = RL.l1_ssim_forward(img, gt, lam)
+            return loss, parts, RL.l1_ssim_backward(img, gt, lam, ws, grad_loss)
+
+        RL.l1_ssim_forward_backward = split
     for kv in a.tune:
         k, v = kv.split("=")
         _native.check(_native.raster().rr_set_tuning(k.encode(), int(v)), "rr_set_tuning " + kv)
