@@ -582,6 +582,11 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         d.first = bn.first + pa.units; d.pair0 = LA; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units; d.L = L;
         d.keys = keys + LA; d.vals = bn.vals + LA; d.dbits = pb.dbits0; d.counts = pb.counts;
         d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
+        // the backward's tile order on phase A's tile_max (counters[1] = T marks it done; the forward
+        // blends' own order, when enabled, shares im.order and keeps the prologue's sort instead)
+        if (bwd_tile_order() && !fwd_tile_order()) {
+            d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
+        }
         d.zero = nullptr; d.nzero = 0;
         d.starts_done = starts_b;
         launch_duplicate<K>(d, st);
@@ -629,7 +634,7 @@ int blend_backward(const rr_frame* f, const rr_camera* cam, const void* geom_buf
     uint32_t* order = blend && bwd_tile_order() ? im.order : nullptr;
     {
         StageTimer tm(RR_STAGE_MEMSET, st);
-        launch_bwd_prologue(gacc, (size_t)P * GACC_STRIDE, gx * gy, im.tile_max, order, st);
+        launch_bwd_prologue(gacc, (size_t)P * GACC_STRIDE, gx * gy, im.tile_max, order, im.counters + 1, st);
         RR_CHECK(hipGetLastError(), "clear accumulators");
     }
     if (blend) {

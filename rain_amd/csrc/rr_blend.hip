@@ -269,9 +269,12 @@ __global__ __launch_bounds__(1024) void k_tile_order(int T, const uint32_t* __re
 // alone on the GPU for ~11 us between the clear and the blend).
 __global__ __launch_bounds__(1024) void k_bwd_prologue(float4* __restrict__ gacc, size_t n4, int T,
                                                        const uint32_t* __restrict__ tile_max,
-                                                       uint32_t* __restrict__ order) {
+                                                       uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ order_flag) {
     if (order) {
         if (blockIdx.x == 0) {
+            // the phase-B duplicate launch already sorted this frame's tiles (DupArgs::order_out)
+            if (order_flag && *order_flag == (uint32_t)T) return;
             tile_order_body(T, tile_max, nullptr, order);
             return;
         }
@@ -282,12 +285,12 @@ __global__ __launch_bounds__(1024) void k_bwd_prologue(float4* __restrict__ gacc
 }
 
 void launch_bwd_prologue(float* gacc, size_t nfloats, int T, const uint32_t* tile_max, uint32_t* order,
-                         hipStream_t st) {
+                         const uint32_t* order_flag, hipStream_t st) {
     const size_t n4 = nfloats / 4;  // P * GACC_STRIDE, a multiple of 4
     const size_t zb = std::max<size_t>(1, std::min<size_t>((n4 + 1023) / 1024, 2048));
     const bool ord = order && T > 0;
     k_bwd_prologue<<<(unsigned)(zb + (ord ? 1 : 0)), 1024, 0, st>>>(reinterpret_cast<float4*>(gacc), n4, T, tile_max,
-                                                                    ord ? order : nullptr);
+                                                                    ord ? order : nullptr, order_flag);
 }
 
 namespace {

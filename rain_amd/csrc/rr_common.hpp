@@ -493,4 +493,49 @@ __device__ __forceinline__ void red9_store(float* dst, int lane, float t0, float
     }
 }
 
+// The backward blend's tile order (heaviest first, rr_blend.hip tile_order_body: counting sort by
+// 1023 - min(cost / 4, 1023), order inside a bucket free) by ONE 256-thread workgroup: the extra
+// workgroup of the phase-B duplicate launch, where it runs beside the duplicate instead of on the
+// backward prologue's critical path.  There the costs are phase A's: a tile phase A left open
+// (open_bits) goes on walking in phase B and counts as heaviest (bucket 0).
+__device__ __forceinline__ void tile_order_body256(int T, const uint32_t* __restrict__ cost,
+                                                   const uint32_t* __restrict__ open_bits,
+                                                   uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[1024];
+    __shared__ uint32_t wsum[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    auto bucket = [&](int i) {
+        if (open_bits && ((open_bits[i >> 5] >> (i & 31)) & 1u)) return 0u;
+        return 1023u - min(cost[i] >> 2, 1023u);
+    };
+#pragma unroll
+    for (int k = 0; k < 4; k++) hist[4 * t + k] = 0;
+    __syncthreads();
+    for (int i = t; i < T; i += 256) atomicAdd(&hist[bucket(i)], 1u);
+    __syncthreads();
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        v[k] = hist[4 * t + k];
+        sum += v[k];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int i = 0; i < w; i++) run += wsum[i];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        hist[4 * t + k] = run;
+        run += v[k];
+    }
+    __syncthreads();
+    for (int i = t; i < T; i += 256) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
+}
+
 }  // namespace rr

@@ -510,7 +510,17 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
                                                    uint32_t* __restrict__ vals, int dbits,
                                                    uint32_t* __restrict__ counts, int units,
                                                    const uint32_t* __restrict__ open_bits,
-                                                   uint32_t* __restrict__ unit_len, uint32_t* __restrict__ n_total) {
+                                                   uint32_t* __restrict__ unit_len, uint32_t* __restrict__ n_total,
+                                                   const uint32_t* __restrict__ order_cost, uint32_t* __restrict__ order_out,
+                                                   uint32_t* __restrict__ order_flag, int order_T) {
+    // the extra workgroup (block-uniform) is block 0, so that it is dispatched first and runs
+    // under the duplicate instead of after it; the windows are blocks 1..units
+    if (FILTER && order_out && blockIdx.x == 0) {
+        tile_order_body256(order_T, order_cost, open_bits, order_out);
+        if (threadIdx.x == 0) *order_flag = (uint32_t)order_T;
+        return;
+    }
+    const int wb = (FILTER && order_out) ? (int)blockIdx.x - 1 : (int)blockIdx.x;  // window
     // open-tile bitmask in LDS for grids of <= 65536 tiles; larger grids read open_bits directly
     // (FILTER: phase B; the unfiltered kernel does without the mask's 8 KiB of LDS)
     const bool kMaskLds = FILTER && gx * gy <= 65536;
@@ -523,7 +533,7 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     const int ndig = 1 << dbits;
     constexpr bool filter = FILTER;
     for (int d = t; d < ndig; d += 256) hist[d] = 0;
-    const uint32_t w0 = pair0 + blockIdx.x * win, w1 = min(w0 + win, L);
+    const uint32_t w0 = pair0 + wb * win, w1 = min(w0 + win, L);
     const uint32_t wn = w1 - w0;
     if (filter) {
         for (uint32_t j = t; j < wn; j += 256) s_val[j] = 0xffffffffu;  // not emitted
@@ -560,7 +570,7 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
         return false;
     };
     const int bgx = bins_x(gx);
-    const int s0 = (int)first[blockIdx.x];
+    const int s0 = (int)first[wb];
     for (int base = s0;; base += 256) {
         const int s = base + t;
         if (s < P) {
@@ -616,8 +626,8 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     }
     __syncthreads();
     const uint32_t mask = (uint32_t)ndig - 1u;
-    K* const kout = keys + (size_t)blockIdx.x * win;
-    uint32_t* const vout = vals + (size_t)blockIdx.x * win;
+    K* const kout = keys + (size_t)wb * win;
+    uint32_t* const vout = vals + (size_t)wb * win;
     if (!filter) {
         for (uint32_t j = t; j < wn; j += 256) {
             const K k = s_key[j];
@@ -655,12 +665,12 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
             __syncthreads();
         }
         if (t == 0) {
-            unit_len[blockIdx.x] = carry;
+            unit_len[wb] = carry;
             if (carry) atomicAdd(n_total, carry);
         }
     }
     __syncthreads();
-    for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + blockIdx.x] = hist[d];
+    for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + wb] = hist[d];
 }
 
 // One workgroup per bin.  The bin's run [lo, hi) of the bin-sorted list (two binary searches over
@@ -810,9 +820,11 @@ bool launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
                                                          second ? d.win_b : 1u, second ? d.nwin_b : 0,
                                                          d.first_b, d.zero, d.zero ? d.nzero : 0);
     auto kern = d.open_bits ? k_duplicate<K, true> : k_duplicate<K, false>;
-    kern<<<d.nwin, 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
-                                            d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts, d.nwin,
-                                            d.open_bits, d.unit_len, d.n_total);
+    const bool ord = d.open_bits && d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
+    kern<<<d.nwin + (ord ? 1 : 0), 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
+                                                  d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts,
+                                                  d.nwin, d.open_bits, d.unit_len, d.n_total, ord ? d.order_cost : nullptr,
+                                                  ord ? d.order_out : nullptr, d.order_flag, d.order_T);
     return !d.starts_done && second;
 }
 template bool launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);

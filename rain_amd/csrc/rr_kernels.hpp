@@ -236,6 +236,13 @@ struct DupArgs {
     const uint32_t* open_bits;
     uint32_t* unit_len;
     uint32_t* n_total;
+    // optional (phase B): one extra workgroup computes the backward blend's tile order from the
+    // phase-A tile_max (order_cost) into order_out and sets *order_flag = order_T, so that the
+    // backward prologue skips its own one-workgroup sort (its critical path)
+    const uint32_t* order_cost;
+    uint32_t* order_out;
+    uint32_t* order_flag;
+    int order_T;
     // optional: words cleared by the window-starts kernel before the duplicate runs (the frame's
     // tile ranges and counters; saves a memset launch on the path right after the pair-count
     // readback)
@@ -260,7 +267,9 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 
 void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st);  // a.order: from launch_bwd_prologue
 // clears the nfloats gradient accumulators and, with order, writes the backward's tile order
+// order_flag (may be null): *order_flag == T means the order was already computed this frame
 void launch_bwd_prologue(float* gacc, size_t nfloats, int T, const uint32_t* tile_max, uint32_t* order,
+                         const uint32_t* order_flag,
                          hipStream_t st);
 
 // Largest sort unit (items per workgroup) of rr_sort.hip; the duplicate kernel's LDS windows are
