@@ -211,6 +211,13 @@ def main():
     timer = _native.Profiler([dom]) if dom else None
     if timer:  # the timed loop records only the reported kernel: two events per launch
         timer.__enter__()
+    # trace markers around the timed loop, outside its clock: a rocprofv3 kernel trace of this run
+    # is cut to exactly these K steps by tools/step_breakdown.py --window (profiles/*_timed_*)
+    mark = _native.train_lib().rt_trace_marker
+    _native.check_rt(mark(0, K, _native.stream_of(trainer.background)), "trace marker")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     views_used = []
     for _ in range(K):
@@ -221,6 +228,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    _native.check_rt(mark(1, K, _native.stream_of(trainer.background)), "trace marker")
     dom_timed = None
     if timer:
         timer.__exit__()
@@ -351,13 +359,24 @@ def main():
                                "traffic": _pmc_traffic(k) if headline else None,
                                "valu_issue_frac": _pmc_field(k, "valu_issue_frac") if headline else None}
 
+    # the CPU baseline on every line (north_star: iters/s at 1, 2, 4, 8 GPUs "alongside the CPU
+    # baseline"): rank 0 times the oracle on the same frame; the other ranks wait at the barrier
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = _cpu_baseline(gauss, cams[views_used[0]], bg, D, args.cpu_threads)
+        if world > 1:
+            cpu["note"] = (f"rank 0 of {world}, timed after the GPU legs while the other ranks idle; the "
+                           f"oracle renders one view per iteration, so it is the same figure at every N")
+    if world > 1:
+        dist.barrier()
 
     line = {
         "metric": "train iters/sec + forward Mpix/sec, 1M Gaussians @ 1080p, 1/2/4/8 MI355X",
         "value": round(iters_per_s, 3),
+        # the reference loop's densify/prune share (1 iteration in 100) priced in: the measured window
+        # when it holds one, else the ordinary steps plus 1/100 of the measured extra cost of a
+        # densify iteration (densify_iter_ms - ordinary_iter_ms_alone)
+        "iters_per_s_1in100": round(world * 1000.0 / ms_1in100, 3),
         "unit": "train iters/s",
         "n_gpus": world,
         "steps": K,
@@ -378,7 +397,6 @@ def main():
         "densify_iter_ms": round(one_ms[D1], 3),
         "ordinary_iter_ms_alone": round(one_ms[D1 - 1], 3),
         "densify_extra_ms": round(densify_extra_ms, 3),
-        "iters_per_s_1in100": round(world * 1000.0 / ms_1in100, 3),
         "forward_mpix_per_s": round(fwd_mpix, 2),
         "forward_outputs": "color+depth+normal" if args.aux_normal else "color+depth",
         "views_per_s": round(iters_per_s, 3),  # one view per rank per step: = value

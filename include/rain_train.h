@@ -124,6 +124,11 @@ int rt_stream_copy(void* dst, const void* src, size_t n_bytes, void* stream);
  * bench.py prices the fused-Adam backward kernel against. */
 int rt_stream_rmw(float* p, float* m, float* v, size_t n_floats, void* stream);
 
+/* Trace markers (not on the training path): launches an empty one-wave kernel named
+ * k_trace_mark_begin (which == 0) or k_trace_mark_end (which != 0) on `stream`, so that a
+ * rocprofv3 kernel trace can be cut to the launches between them (bench.py's timed loop). */
+int rt_trace_marker(int which, int tag, void* stream);
+
 const char* rt_last_error(void);
 
 #ifdef __cplusplus

@@ -209,7 +209,7 @@ def loss_lib():
 
 TRAIN_LIB = os.path.join(LIB_DIR, "librain_train.so")
 TRAIN_SYMBOLS = ["rt_adam_step", "rt_adam_step_scaled", "rt_densify_workspace_bytes", "rt_densify_plan",
-                 "rt_densify_apply", "rt_stream_copy", "rt_stream_rmw", "rt_last_error"]
+                 "rt_densify_apply", "rt_stream_copy", "rt_stream_rmw", "rt_trace_marker", "rt_last_error"]
 RT_MAX_GROUPS = 8
 _train = None
 
@@ -260,6 +260,8 @@ def train_lib():
         L.rt_stream_copy.argtypes = [vp, vp, ctypes.c_size_t, vp]
         L.rt_stream_rmw.restype = ctypes.c_int
         L.rt_stream_rmw.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
+        L.rt_trace_marker.restype = ctypes.c_int
+        L.rt_trace_marker.argtypes = [ctypes.c_int, ctypes.c_int, vp]
         L.rt_last_error.restype = ctypes.c_char_p
         _train = L
     return _train
@@ -282,6 +284,13 @@ def knn():
 def check(rc: int, what: str):
     if rc != 0:
         msg = raster().rr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg}")
+
+
+def check_rt(rc: int, what: str):
+    """check() for librain_train.so calls (its own last-error slot)."""
+    if rc != 0:
+        msg = train_lib().rt_last_error().decode(errors="replace")
         raise RuntimeError(f"{what}: {msg}")
 
 

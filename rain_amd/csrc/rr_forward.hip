@@ -235,15 +235,21 @@ __global__ __launch_bounds__(256) void k_unpack_rows(int world, int Q, const cha
     const int radius = reinterpret_cast<const int*>(c + o_radii)[r];
     tiles[g] = reinterpret_cast<const uint2*>(c + o_tiles)[r];
     radii[g] = radius;
-    const float2 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-    float log2o, inv_o;
-    splat_derived(w3.x, log2o, inv_o);
     Splat s;
-    s.a = make_float4(w0.x, w0.y, w1.x, w1.y);
-    s.b = make_float4(w2.x, log2o, w2.y, w3.x);
-    s.c = make_float4(w3.y, w4.x, w4.y, inv_o);
+    if (radius > 0) {
+        const float2 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+        float log2o, inv_o;
+        splat_derived(w3.x, log2o, inv_o);
+        s.a = make_float4(w0.x, w0.y, w1.x, w1.y);
+        s.b = make_float4(w2.x, log2o, w2.y, w3.x);
+        s.c = make_float4(w3.y, w4.x, w4.y, inv_o);
+    } else {
+        // a culled row's wire record was never written by its owner (the preprocess returns before
+        // the record): a zero record keeps the geometry buffer deterministic
+        s.a = s.b = s.c = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     splats[g] = s;
-    keys[g] = radius > 0 ? __float_as_uint(w2.y) - kDepthKeyBase : 0xffffffffu;
+    keys[g] = radius > 0 ? __float_as_uint(s.b.z) - kDepthKeyBase : 0xffffffffu;
     if ((r & 255) == 0) {  // Q is a multiple of 256: rank j's block b is global block g / 256
         bsum[g / 256] = reinterpret_cast<const uint2*>(c + o_bsum)[r / 256];
         bwide[g / 256] = reinterpret_cast<const uint32_t*>(c + o_bwide)[r / 256];

@@ -171,6 +171,20 @@ int rt_stream_copy(void* dst, const void* src, size_t n_bytes, void* stream) {
     return 0;
 }
 
+// Trace markers: empty one-wave kernels whose names delimit a region of a rocprofv3 kernel trace
+// (bench.py brackets its timed loop with them, outside the timed clock; tools/step_breakdown.py
+// --window keeps the launches between the two).
+__global__ void k_trace_mark_begin(int tag) {}
+__global__ void k_trace_mark_end(int tag) {}
+
+int rt_trace_marker(int which, int tag, void* stream) {
+    if (which == 0) k_trace_mark_begin<<<1, 64, 0, (hipStream_t)stream>>>(tag);
+    else k_trace_mark_end<<<1, 64, 0, (hipStream_t)stream>>>(tag);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(std::string("trace marker launch: ") + hipGetErrorString(e));
+    return 0;
+}
+
 int rt_stream_rmw(float* p, float* m, float* v, size_t n_floats, void* stream) {
     if ((n_floats & 3u) || !aligned16(p) || !aligned16(m) || !aligned16(v))
         return fail("stream rmw: 4-float multiples, 16-B aligned arrays only");

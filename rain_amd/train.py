@@ -241,7 +241,11 @@ class Trainer:
         cam = self.cams[vidx]
         if cfg.c2f:
             if iteration == 1 or (iteration % cfg.c2f_every_step == 0 and iteration < opt.densify_until_iter):
-                self.low_pass = low_pass_schedule(cam.image_height, cam.image_width, g.get_xyz.shape[0],
+                # one value per step on every rank: the schedule reads the image size of the step's
+                # FIRST view (views[0], the one a single process would render first), so ranks whose
+                # own views differ in size still blur every Gaussian alike
+                c0 = self.cams[views[0]]
+                self.low_pass = low_pass_schedule(c0.image_height, c0.image_width, g.get_xyz.shape[0],
                                                   cfg.c2f_max_lowpass)
         else:
             self.low_pass = 0.3
@@ -292,6 +296,10 @@ class Trainer:
         from .loss import l1_ssim_forward_backward
 
         g, opt = self.g, self.opt
+        if not hasattr(g.optimizer, "fused_step"):  # before any collective of the step starts
+            raise ValueError("the Gaussian-sharded fused step applies Adam inside its owner kernel: the model's "
+                             "optimizer must be rain_amd.optim.FusedAdam (GaussianModel.training_setup builds one); "
+                             "use Trainer(fused=False) for another optimizer")
         vidx, _cam = self._low_pass_and_view(iteration)
         cams = [self.cams[v] for v in self._views]
         densify_phase = iteration < opt.densify_until_iter
@@ -349,19 +357,25 @@ class Trainer:
         if self.sharded:
             g.pack_flat_state(self.world)
         flat = None if fuse_adam else g.bind_flat_grad(zero=False, pad_to=self.world)  # backward overwrites all
+        # Everything the backward needs from Python is prepared BEFORE the forward: the forward's one
+        # host wait (the pair-count read-back, rasterizer_impl.cu:273) returns when the device is at
+        # this frame's depth sort, and from there the host must enqueue the binning, the blends, the
+        # loss and the backward faster than the device runs them (~0.45 ms of kernels); the Adam
+        # block (step counts, bias corrections) does not depend on the frame.
+        adam = g.optimizer.fused_step(g) if fuse_adam else None
+        grads = None if fuse_adam else dict(
+            xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad, opacity=g._opacity.grad,
+            scaling=g._scaling.grad, rotation=g._rotation.grad)
+        # densification statistics accumulate per rank; ranks merge them only when densify consumes
+        # them (_finish)
+        stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D) if densify_phase else None
+        gt = self.gt[vidx]
         with torch.no_grad():
             image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass,
                                                      cache=self._bin_cache if self.reuse_binning else None)
-            gt = self.gt[vidx]
             # loss and dL/dimage in one call (bitwise the separate forward / backward)
             loss, _parts, dimg = l1_ssim_forward_backward(image, gt, opt.lambda_dssim)
-            grads = None if fuse_adam else dict(
-                xyz=g._xyz.grad, f_dc=g._features_dc.grad, f_rest=g._features_rest.grad, opacity=g._opacity.grad,
-                scaling=g._scaling.grad, rotation=g._rotation.grad)
-            # densification statistics accumulate per rank; ranks merge them only when densify
-            # consumes them (_finish)
-            stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D) if densify_phase else None
-            fused.backward(st, dimg, grads, stats, adam=g.optimizer.fused_step(g) if fuse_adam else None)
+            fused.backward(st, dimg, grads, stats, adam=adam)
             densified = self._finish(iteration, flat, densify_now, reset_now, adam_done=fuse_adam)
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
                         view=vidx, low_pass=self.low_pass, densified=densified)

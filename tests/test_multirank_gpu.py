@@ -60,14 +60,26 @@ class _LazyGT:
 
 SCENES = {
     "small": dict(P=20_000, W=160, H=120, V=6, iters=range(1, 8), expect=[False, True, False, True, False, True, False]),
+    # c2f on, cameras of two image sizes: the low-pass value of a step must be the same
+    # on every rank; 1000 Gaussians so that the schedule's H*W / N / 9pi exceeds its 0.3 floor
+    # (160x120: 0.68, 128x96: 0.43)
+    "mixed": dict(P=1_000, W=160, H=120, V=6, iters=range(1, 6), expect=[False, True, False, True, False], c2f=True),
     "cfg4": dict(P=1_000_000, W=1920, H=1080, V=200, iters=range(1, 5), expect=[False, True, False, False]),
 }
+
+
+# "mixed": image size per camera index; the first view groups of the tests' seed (5) mix both sizes
+MIXED_SIZES = [(160, 120), (128, 96), (128, 96), (160, 120), (160, 120), (128, 96)]
+
+
+def _c2f(name):
+    return bool(SCENES[name].get("c2f", False))
 
 
 def _opt(name):
     from rain_amd.gaussian_model import OptimizationParams
 
-    if name == "small":
+    if name in ("small", "mixed"):
         o = OptimizationParams(densify_from_iter=1, densification_interval=2, opacity_reset_interval=3)
         o.densify_grad_threshold = 2e-5  # some clones / splits at this tiny scale
         return o
@@ -82,12 +94,16 @@ def _scene(dev, name):
 
     s = SCENES[name]
     P, W, H, V = s["P"], s["W"], s["H"], s["V"]
-    cams = [c.to(dev) for c in cameras.fibonacci_cameras(V, W, H)]
+    if name == "mixed":
+        cams = [cameras.fibonacci_cameras(V, w, h)[i].to(dev) for i, (w, h) in enumerate(MIXED_SIZES)]
+    else:
+        cams = [c.to(dev) for c in cameras.fibonacci_cameras(V, W, H)]
     g = GaussianModel(3, divide_ratio=0.8, device=dev)
     p = synthetic.random_gaussians(P, sh_degree=3, seed=6, bench=True)
     gen = torch.Generator().manual_seed(1)
-    if name == "small":
-        gts = [torch.rand(3, H, W, generator=torch.Generator().manual_seed(20 + i)).to(dev) for i in range(V)]
+    if name in ("small", "mixed"):
+        gts = [torch.rand(3, int(c.image_height), int(c.image_width), generator=torch.Generator().manual_seed(20 + i))
+               .to(dev) for i, c in enumerate(cams)]
         p["scaling"] = p["scaling"] + 0.3 * torch.randn(p["scaling"].shape, generator=gen)
     else:
         gts = _LazyGT(V, W, H, dev)
@@ -127,7 +143,7 @@ def _worker(rank, world, port, out_path, name, chunk_rows=None):
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     g, opt, cams, gts = _scene(dev, name)
-    tr = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=False, seed=5), scene_extent=4.4)
+    tr = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=_c2f(name), seed=5), scene_extent=4.4)
     assert tr.fused and tr.world == world and not tr.exchange.direct and tr._owner is not None
     tr._owner.rec_chunk_rows = chunk_rows
     flags = [tr.step(it).densified for it in SCENES[name]["iters"]]
@@ -157,20 +173,26 @@ def _reference(dev, world, name):
     gradients summed in view order then divided by the world size, statistics accumulated view
     after view, then the world-1 densify/Adam logic."""
     from rain_amd import fused
+    from rain_amd.gaussian_model import low_pass_schedule
     from rain_amd.loss import l1_ssim_backward, l1_ssim_forward
     from rain_amd.train import TrainConfig, Trainer, ViewSampler
 
     g, opt, cams, gts = _scene(dev, name)
-    tr = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=False, seed=5), scene_extent=4.4)
+    tr = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=_c2f(name), seed=5), scene_extent=4.4)
     sampler = ViewSampler(len(cams), world, seed=5)
     bg = torch.zeros(3, device=dev)
     flags = []
+    lp = 0.3
     for it in SCENES[name]["iters"]:
         g.update_learning_rate(it)
         views = sampler.next_group()
+        if _c2f(name) and it == 1:  # train.py:95-107 on the step's first view, as one process would
+            c0 = cams[views[0]]
+            lp = low_pass_schedule(c0.image_height, c0.image_width, g.get_xyz.shape[0], 300.0)
+            assert lp > 0.3 and len({(int(cams[v].image_width), int(cams[v].image_height)) for v in views}) > 1
         acc = None
         for v in views:
-            color, radii, depth, st = fused.forward(g, cams[v], bg, 0.3)
+            color, radii, depth, st = fused.forward(g, cams[v], bg, lp)
             _, _, ws = l1_ssim_forward(color, gts[v], opt.lambda_dssim)
             dimg = l1_ssim_backward(color, gts[v], opt.lambda_dssim, ws)
             grads = {n: torch.empty_like(p) for n, p in zip(NAMES, g.params())}
@@ -233,6 +255,14 @@ def test_view_sharded_fused_step_two_ranks_chunked_exchange(tmp_path):
     """The record exchange in row chunks of 256 (40 chunks per owner; rr_backward_records' chunked
     layout, one all-to-all and one owner launch per chunk) against the same bars."""
     _run(tmp_path, 2, "small", chunk_rows=256)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_view_sharded_fused_step_c2f_mixed_image_sizes(tmp_path, world):
+    """c2f low-pass on and views of two image sizes in one step: every rank must render and run its
+    owner backward with the step's one low-pass value (from the first view of the group), equal to
+    one process rendering the same views (ranks used their own view's size)."""
+    _run(tmp_path, world, "mixed")
 
 
 def test_view_sharded_fused_step_four_ranks(tmp_path):
