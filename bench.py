@@ -79,7 +79,8 @@ def algorithmic_bytes(stage, st, P, W, H, K, world=1, sharded=None):
     bins of 2 x 2 tiles, after exact culling and early-stop binning), not on the reference's larger
     num_rendered, so they are not credited for pairs they never write.  The bin sort ("tile_sort")
     is priced at its minimum: read + write each key and u32 value once; the expand ("ranges") at
-    reading the sorted pairs once (its per-tile list writes are not counted)."""
+    reading the sorted pairs once and gathering each pair's 4-B depth key for the per-bin depth sort
+    (rr_bin.hip k_sortexpand; its per-tile list writes are not counted)."""
     Lb, V, Le, T, N = st["num_binned"], st["num_visible"], st["l_eff"], st["tiles"], W * H
     M = K
     kw = 2 if (W + 31) // 32 * ((H + 31) // 32) <= 65536 else 4
@@ -88,11 +89,11 @@ def algorithmic_bytes(stage, st, P, W, H, K, world=1, sharded=None):
         "scan": 8 * P,
         "duplicate": 4 * P + 16 * V + (kw + 4) * Lb,
         "tile_sort": 2 * (kw + 4) * Lb,
-        "ranges": (kw + 4) * Lb + 8 * T,
+        "ranges": (kw + 8) * Lb + 8 * T,
         "blend_fwd": 8 * T + 44 * Le + 24 * N,
         "blend_bwd": 8 * T + 40 * Le + 20 * N + 44 * V,
         "gauss_bwd": (gauss_bwd_views_bytes(P, K, M, world) if (world > 1 if sharded is None else sharded)
-                      else gauss_bwd_bytes(P, V, K, M)),
+                      else gauss_bwd_bytes(P, V, K, M, next_frame=st.get("next_frame", False))),
     }.get(stage)
 
 
@@ -104,14 +105,17 @@ def gauss_bwd_views_bytes(P, K, M, world):
     return rows * (24 * (11 + 3 * M) + 24) + 40 * rows * world
 
 
-def gauss_bwd_bytes(P, V, K, M, fused_adam=True):
+def gauss_bwd_bytes(P, V, K, M, fused_adam=True, next_frame=False):
     """Per-Gaussian backward.  In the training step (fused_adam) it reads the 64-B gradient
     accumulator line and applies Adam in place: read + write of parameter, exp_avg and exp_avg_sq
     (n_par = 11 + 3M floats each: xyz 3, f_dc 3, f_rest 3(M-1), opacity 1, scaling 3, rotation 4),
-    plus the densification statistics of visible Gaussians (read + write of 3 floats).  The
-    reference-API backward instead zero-fills and writes its gradient tensors."""
+    plus the densification statistics of visible Gaussians (read + write of 3 floats).  With the
+    next frame's preprocess in the same pass (rr_next_frame) it also writes that frame's geometry:
+    radius, pair counts and depth key of every Gaussian (16 B) and the 48-B splat record of the
+    visible ones (V of the next frame, taken as this frame's).  The reference-API backward instead
+    zero-fills and writes its gradient tensors."""
     if fused_adam:
-        return 64 * P + 24 * (11 + 3 * M) * P + 24 * V
+        return 64 * P + 24 * (11 + 3 * M) * P + 24 * V + ((16 * P + 48 * V) if next_frame else 0)
     return 4 * P * (27 + 3 * M) + 4 * P + 88 * V + 4 * P + V * (143 + 24 * K)
 
 
@@ -298,6 +302,8 @@ def main():
                                          0.3)
             stats.append(_C.frame_stats(out[4], out[6], Pn, W, H))
     mean_stats = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
+    # the timed loop's per-Gaussian backward also preprocesses the next step's frame (rr_next_frame)
+    mean_stats["next_frame"] = bool(trainer.fused and trainer.fuse_next and not trainer.sharded)
     # the same frame statistics at the c2f stress dilation (first timed view)
     c2f_stats = {}
     with torch.no_grad():

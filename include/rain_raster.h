@@ -195,7 +195,26 @@ typedef struct rr_grads {
     float* max_radii2D;   /* [P] */
     /* RR_FLAG_RAW_PARAMS only, optional: apply Adam in place; the six gradient outputs may then be NULL */
     const rr_adam* adam;
+    /* Optional, with adam: the NEXT frame's preprocess, run by the per-Gaussian backward on the
+     * parameters it has just updated (struct below) */
+    const struct rr_next_frame* next;
 } rr_grads;
+
+/* Cross-step fusion of the training loop: the per-Gaussian backward kernel of step s holds every
+ * Gaussian's parameters right after its Adam update, which is exactly the input of step s+1's
+ * preprocess (forward.cu:144-246: projection, covariance, SH colour, tile counts).  With
+ * rr_grads.next it runs that preprocess in the same pass — the parameters are not read again — and
+ * fills the next frame's geometry buffer and radii; step s+1 then renders with
+ * rr_forward_from_geometry.  Requires rr_grads.adam, RR_FLAG_RAW_PARAMS, and the same P, M and SH
+ * degree D in both frames (the caller renders normally when the degree steps up or a densify /
+ * opacity reset replaces the parameters). */
+typedef struct rr_next_frame {
+    const rr_frame* frame;   /* the next frame: width, height, tan_fov, scale_modifier, low_pass, flags */
+    const rr_camera* cam;    /* its camera (background unused) */
+    int* radii;              /* [P] out */
+    void* geom_buffer;       /* rr_geometry_bytes(P), filled as rr_forward_geometry's preprocess does */
+    size_t geom_bytes;
+} rr_next_frame;
 
 /*
  * Backward (replaces Rasterizer::backward rasterizer_impl.cu:334-430 and the zero-filled
@@ -261,9 +280,10 @@ int rr_preprocess_rows_views(const rr_frame* f, const rr_view* views, int num_vi
  * pair counts, depth keys, block sums at rr_geometry_layout's offsets) and radii[]. */
 int rr_unpack_rows(int world, int rows_per_rank, const void* recv, size_t chunk_bytes, const size_t field_offsets[5],
                    void* geom_buffer, size_t geom_bytes, int* radii, void* stream);
-/* rr_forward over a geometry buffer whose preprocess arrays are already filled (frame.P rows, a
- * multiple of 256; radii [P]); same outputs, same RR_INCOMPLETE / binning_needed protocol, with
- * rr_forward_render_geometry as the second stage. */
+/* rr_forward over a geometry buffer whose preprocess arrays are already filled (frame.P rows;
+ * radii [P]) — by the sharded step's unpack or by the previous step's backward (rr_next_frame);
+ * same outputs, same RR_INCOMPLETE / binning_needed protocol, with rr_forward_render_geometry as the
+ * second stage. */
 int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
                              size_t geom_bytes, void* image_buffer, size_t image_bytes, void* binning_buffer,
                              size_t binning_bytes, int* num_rendered, int* num_pairs, size_t* binning_needed,

@@ -24,8 +24,8 @@ CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-W
             "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 LIBS = {
-    "librain_raster.so": ["rr_forward.hip", "rr_blend_fwd_s.hip", "rr_blend.hip", "rr_backward.hip", "rr_sort.hip",
-                          "rr_api.hip"],
+    "librain_raster.so": ["rr_forward.hip", "rr_bin.hip", "rr_blend_fwd_s.hip", "rr_blend.hip", "rr_backward.hip",
+                          "rr_sort.hip", "rr_api.hip"],
     "librain_loss.so": ["loss.hip"],
     "librain_knn.so": ["knn.hip"],
     "librain_train.so": ["train.hip", "densify.hip"],
@@ -38,7 +38,15 @@ LIBS = {
 # loss.hip: the SSIM kernels' band loop must unroll fully (compile-time ring / queue slots) and is
 # larger than clang's default pragma-unroll size limit; packed-fp32 formation is off for the same
 # reason as rr_blend.hip (it pairs unrelated scalars: 940 v_mov, 244 VGPRs in k_ssim_fwd).
+# rr_forward.hip / rr_backward.hip: floating-point contraction only inside one source expression
+# (llvm.fmuladd), not across statements by the backend — the forward preprocess and the next
+# frame's preprocess inside the per-Gaussian backward (rr_preprocess.hpp, include/rain_raster.h
+# rr_next_frame) then compile the same arithmetic to the same fma sequence in both kernels, so the
+# fused geometry is bitwise the forward's.
+CONTRACT_ON = ["-ffp-contract=on"]
 EXTRA = {
+    "rr_forward.hip": CONTRACT_ON,
+    "rr_backward.hip": CONTRACT_ON,
     # rr_blend_fwd_s.hip: machine sinking would move the software-pipelined next-group record loads
     # below the blend (next to their use in the loop latch), serialising them again
     "rr_blend_fwd_s.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-mllvm", "-disable-machine-sink"],

@@ -59,11 +59,17 @@ class RRAdam(ctypes.Structure):
                [("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double)]
 
 
+class RRNextFrame(ctypes.Structure):
+    """include/rain_raster.h rr_next_frame: the next frame's preprocess inside the backward."""
+    _fields_ = [("frame", ctypes.POINTER(RRFrame)), ("cam", ctypes.POINTER(RRCamera)), ("radii", ctypes.c_void_p),
+                ("geom_buffer", ctypes.c_void_p), ("geom_bytes", ctypes.c_size_t)]
+
+
 class RRGrads(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D",
                                                 "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations",
                                                 "dL_dsh_rest", "grad_accum", "denom", "max_radii2D")] + \
-               [("adam", ctypes.POINTER(RRAdam))]
+               [("adam", ctypes.POINTER(RRAdam)), ("next", ctypes.POINTER(RRNextFrame))]
 
 
 class RRView(ctypes.Structure):

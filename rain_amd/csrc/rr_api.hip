@@ -66,17 +66,6 @@ inline int grid_x(int W) { return (W + TILE_X - 1) / TILE_X; }
 inline int grid_y(int H) { return (H + TILE_Y - 1) / TILE_Y; }
 
 // ---- temp-storage queries ----
-// The pair-count scan (launch_pair_scan) reads tiles[] in depth order from tiles_sorted, which the
-// depth sort's last pass gathers while it writes idx_sorted (a transform iterator gathering inside
-// a scan measured 21 us per frame, most of it the scan blocks waiting on their random loads); it
-// saturates each component at 2^32 - 1, so an overflowing total is caught by the 2^31 capacity
-// check instead of wrapping silently.
-
-size_t depth_sort_temp(int P) {  // the 3-pass (9-bit digits) sort and the 32-bit fallback
-    return P > 0 ? std::max(radix_sort_temp_bytes<uint32_t>((size_t)P, kDepthKeyBits),
-                            radix_sort_temp_bytes<uint32_t>((size_t)P, 32))
-                 : 0;
-}
 template <typename K>
 size_t tile_sort_temp(int L, int bits) {
     return L > 0 ? radix_sort_temp_bytes<K>((size_t)L, bits) : 0;
@@ -87,16 +76,12 @@ struct Geom {
     Splat* splats;
     uint2* tiles;         // per Gaussian {pairs emitted, bounding-rect tiles}
     uint32_t* depth_keys;
-    uint32_t* depth_keys_sorted;
-    uint32_t* idx_sorted;
-    uint32_t* kept;       // [1] Gaussians the depth sort kept (not culled): its output length
-    uint2* tiles_sorted;  // tiles[] in depth order (written by the depth sort's last pass)
-    uint2* offsets;       // inclusive prefix sum of tiles[] in depth order; .y of the last = num_rendered
+    PhaseLists lists;     // the early-stop phases' Gaussians in index order with their pair offsets
     float4* normals;      // RR_FLAG_AUX_NORMAL: view-space normal per visible Gaussian
     uint2* block_sums;    // [ceil(P/256)] per-preprocess-block sums of tiles[] (pairs, rect tiles)
     uint32_t* block_wide; // [ceil(P/256)] per block: a visible depth key needs more than kDepthKeyBits
-    unsigned long long* totals;  // [3] their sums and the OR of block_wide (device copy of the mailbox)
-    void* temp;
+    FrameTotals* ft;      // the frame's counts and early-stop depth cut (rr_bin.hip)
+    void* temp;           // the pair scan's block totals
     size_t temp_bytes;
     size_t total;
 };
@@ -107,16 +92,15 @@ Geom carve_geom(void* buf, int P) {
     g.splats = c.take<Splat>(n);
     g.tiles = c.take<uint2>(n);
     g.depth_keys = c.take<uint32_t>(n);
-    g.depth_keys_sorted = c.take<uint32_t>(n);
-    g.idx_sorted = c.take<uint32_t>(n);
-    g.tiles_sorted = c.take<uint2>(n);
-    g.offsets = c.take<uint2>(n);
+    g.lists.idx_a = c.take<uint32_t>(n);
+    g.lists.off_a = c.take<uint32_t>(n);
+    g.lists.idx_b = c.take<uint32_t>(n);
+    g.lists.off_b = c.take<uint32_t>(n);
     g.normals = c.take<float4>(n);
     g.block_sums = c.take<uint2>((n + 255) / 256);
     g.block_wide = c.take<uint32_t>((n + 255) / 256);
-    g.totals = c.take<unsigned long long>(3);
-    g.kept = c.take<uint32_t>(1);
-    g.temp_bytes = std::max(depth_sort_temp(P), pair_scan_temp_bytes(P));
+    g.ft = c.take<FrameTotals>(1);
+    g.temp_bytes = split_scan_temp_bytes(P);
     g.temp = c.take<char>(std::max<size_t>(g.temp_bytes, 1));
     g.total = align_up(c.off);
     return g;
@@ -156,42 +140,43 @@ Img carve_img(void* buf, int W, int H) {
     return m;
 }
 
-// Early-stop binning split: phase A bins the first L_A pairs (depth order) for every tile, phase B
-// the rest for the tiles phase A left open (rr_kernels.hpp BlendPhase).  L_A = L/3: on the bench
-// frames (1M Gaussians, 1080p) most tiles saturate inside it (tools/saturation_stats.py).  First
-// measured at L/4 (1.671 ms per training step vs 1.742 ms for one phase; 1.695 / 1.688 / 1.712 for
-// L/2, L/3, L/6); after the phase-B fixed costs shrank and the binning kernels sped up, re-measured
-// interleaved (tools/step_ab.py --split 2,3,4, 8 blocks of 60 steps): 1.509 / 1.491 / 1.525 ms.
-// Frames below kEarlyMin pairs are binned in one phase.  rr_set_binning_config changes both (tests
-// force the split onto small frames).
+// Early-stop binning split (rr_bin.hip k_early_cut): phase A bins the pairs of the Gaussians nearer
+// than a per-frame depth cut holding ~1/den of the pairs, for every tile; phase B the rest, only for
+// the tiles phase A left open (rr_kernels.hpp BlendPhase).  den = 3: on the bench frames (1M
+// Gaussians, 1080p) most tiles saturate inside the first third (tools/saturation_stats.py; with the
+// depth-rank split of rounds 1-3, tools/step_ab.py --split 2,3,4: 1.509 / 1.491 / 1.525 ms per
+// step).  Frames below kEarlyMin pairs are binned in one phase.  rr_set_binning_config changes both
+// (tests force the split onto small frames).
 constexpr uint32_t kEarlyDen = 3, kEarlyMin = 1u << 16;
 uint32_t g_early_den = kEarlyDen, g_early_min = kEarlyMin;
-uint32_t early_split(uint32_t L) {
-    if (g_early_den <= 1 || L < g_early_min) return L;
-    return std::max<uint32_t>(L / g_early_den, 1u);
-}
 
 struct Bin {
-    // FIRST, so the backward finds it without knowing the pair count: the per-tile lists k_expand
-    // writes, 4 slots per (bin, Gaussian) pair (phase A's at [0, 4 LA), phase B's at [4 LA, 4 L))
+    // FIRST, so the backward finds it without knowing the pair count: the per-tile lists
+    // k_sortexpand writes, 4 slots per (bin, Gaussian) pair (phase A's at [0, 4 LA), phase B's
+    // from 4 LA)
     uint32_t* point_list;
-    void* keys;            // bin ids of the (bin, Gaussian) pairs, then sorted
+    void* keys;            // bin ids of the (bin, Gaussian) pairs (phase A at [0, LA), B from LA)
     void* keys_sorted;
     uint32_t* vals;        // Gaussian | tile mask << BIN_SHIFT, then sorted
     uint32_t* vals_sorted;
-    uint32_t* first;     // first Gaussian of every duplicate window (= sort unit), phase A then B
-    uint32_t* unit_len;  // phase B: pairs kept per window
-    void* temp;          // tile-sort scratch, shared by the two phases
+    uint32_t* first;       // first Gaussian of every duplicate window (= sort unit), phase A then B
+    uint32_t* unit_len;    // phase B: pairs kept per window
+    uint2* scr0;           // k_sortexpand's scratch runs for bins of more than kSxCap pairs
+    uint2* scr1;
+    uint2* bounds;         // [bins] each bin's run of the bin-sorted pairs (k_bin_bounds)
+    void* temp;            // bin-sort scratch, shared by the two phases
     size_t temp_bytes;
     bool wide;  // 32-bit bin keys (more than 65536 bins)
     int bits;
-    uint32_t L, LA;  // (bin, Gaussian) pairs, and those binned for every bin in phase A (LA == L: one phase)
+    uint32_t L;  // (bin, Gaussian) pairs of both phases
     size_t total;
 };
 template <typename K>
 RadixPlan tile_plan(void* temp, uint32_t n, int bits) {
     return radix_sort_plan<K>(temp, (size_t)n, 0, bits);
 }
+// The layout depends on the frame's pair count L only (not on its split into LA + LB): the window
+// tables hold both phases' windows, and the sort scratch is sized for L items.
 Bin carve_bin(void* buf, int L, int W, int H) {
     Carver c(buf);
     Bin b;
@@ -199,8 +184,6 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     b.wide = NB > 65536 || g_wide_bin_keys;
     b.bits = std::max(1, (int)higher_msb((uint32_t)NB));  // >= 1: the duplicate windows are sort units
     b.L = (uint32_t)std::max(L, 0);
-    b.LA = early_split(b.L);
-    const uint32_t LB = b.L - b.LA;
     const size_t n = (size_t)std::max(L, 1);
     b.point_list = c.take<uint32_t>(4 * n + kPointListPad);
     if (b.wide) {
@@ -212,15 +195,14 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     }
     b.vals = c.take<uint32_t>(n);
     b.vals_sorted = c.take<uint32_t>(n);
-    const int ua = b.wide ? tile_plan<uint32_t>(nullptr, b.LA, b.bits).units : tile_plan<uint16_t>(nullptr, b.LA, b.bits).units;
-    const int ub = b.wide ? tile_plan<uint32_t>(nullptr, LB, b.bits).units : tile_plan<uint16_t>(nullptr, LB, b.bits).units;
-    b.first = c.take<uint32_t>((size_t)std::max(ua + ub, 1));
-    b.unit_len = c.take<uint32_t>((size_t)std::max(ub, 1));
-    // sized for either path: RR_FLAG_FULL_BINNING sorts all L pairs in one phase
-    b.temp_bytes = b.wide ? std::max({tile_sort_temp<uint32_t>(b.L, b.bits), tile_sort_temp<uint32_t>(b.LA, b.bits),
-                                      tile_sort_temp<uint32_t>(LB, b.bits)})
-                          : std::max({tile_sort_temp<uint16_t>(b.L, b.bits), tile_sort_temp<uint16_t>(b.LA, b.bits),
-                                      tile_sort_temp<uint16_t>(LB, b.bits)});
+    // units of either phase <= those of a sort of L items (rounds only grow with the item count)
+    const int u = b.wide ? tile_plan<uint32_t>(nullptr, b.L, b.bits).units : tile_plan<uint16_t>(nullptr, b.L, b.bits).units;
+    b.first = c.take<uint32_t>((size_t)2 * std::max(u, 1) + 2);
+    b.unit_len = c.take<uint32_t>((size_t)std::max(u, 1) + 1);
+    b.scr0 = c.take<uint2>(n);
+    b.scr1 = c.take<uint2>(n);
+    b.bounds = c.take<uint2>((size_t)std::max(NB, 1));
+    b.temp_bytes = b.wide ? tile_sort_temp<uint32_t>(b.L, b.bits) : tile_sort_temp<uint16_t>(b.L, b.bits);
     b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
     b.total = align_up(c.off);
     return b;
@@ -297,30 +279,30 @@ int check(const rr_frame* f, hipStream_t st, const char* what) {
 // ---------------------------------------------------------------------------------------
 // Readback of the forward's pair counts.  A hipMemcpyAsync into pageable host memory + stream
 // synchronise after the scan costs a blit kernel and the runtime's blocking wait (measured 30-140
-// us of idle GPU per frame before the binning launches).  Instead a one-lane kernel stores the two
-// counts and a sequence number into a coherent pinned host mailbox (system-scope release store)
-// and the host thread spins on the sequence number.  Every few thousand spins the stream
-// is queried: a launch / kernel error is reported, and a stream that went idle without the
-// sequence number becoming visible falls back to the plain copy.
+// us of idle GPU per frame before the binning launches).  Instead the last thread of the split scan
+// (rr_bin.hip publish_counts) stores the counts and a sequence number into a coherent pinned host
+// mailbox (system-scope release store) and the host thread spins on the sequence number.  Once the
+// wait has outlasted any frame the stream is queried: a launch / kernel error is reported, and a
+// stream that went idle without the sequence number becoming visible falls back to the plain copy.
 struct Mailbox {
-    uint32_t* host = nullptr;  // [x, y, seq, wide], coherent pinned
+    uint32_t* host = nullptr;  // [LA, rect, seq, wide, LB], coherent pinned
     uint32_t* dev = nullptr;   // device alias of host
     uint32_t seq = 0;
     bool failed = false;       // allocation failed: always use the copy
 };
 thread_local Mailbox g_mailbox;
 
-// The publish (rr_kernels.hpp publish_pair_counts_block) runs as an extra workgroup of the depth
-// sort's first count launch, right after the preprocess whose block sums give the totals, so the
-// host learns the pair count while the depth sort and the scan still run, and has the binning
-// launches queued before the GPU gets to them.
 struct PairCountRead {
-    const unsigned long long* copy = nullptr;  // device {pairs, rect} for the copy path
+    const FrameTotals* copy = nullptr;  // device totals for the copy path
     uint32_t seq = 0;  // 0: no mailbox (copy + synchronise at wait time)
 };
+struct PairCounts {
+    uint32_t LA = 0, LB = 0, rect = 0;
+    bool wide = false;
+};
 
-PublishJob pair_counts_job(const uint2* block_sums, const uint32_t* block_wide, int nb, unsigned long long* copy,
-                           PairCountRead& r) {
+// The mailbox (allocated on first use) and this read's sequence number; box == null: no mailbox.
+uint32_t* pair_counts_box(const FrameTotals* copy, PairCountRead& r) {
     Mailbox& mb = g_mailbox;
     r.copy = copy;
     r.seq = 0;
@@ -336,17 +318,19 @@ PublishJob pair_counts_job(const uint2* block_sums, const uint32_t* block_wide, 
             mb.failed = true;
         }
     }
-    if (!mb.failed) r.seq = ++mb.seq == 0 ? ++mb.seq : mb.seq;  // 0 is the mailbox's initial value
-    return PublishJob{block_sums, block_wide, nb, mb.failed ? nullptr : mb.dev, r.seq, copy};
+    if (mb.failed) return nullptr;
+    r.seq = ++mb.seq == 0 ? ++mb.seq : mb.seq;  // 0 is the mailbox's initial value
+    return mb.dev;
 }
 
-hipError_t pair_counts_copy(const unsigned long long* src, uint2* out, bool* wide, hipStream_t st) {
-    unsigned long long v[3] = {0ull, 0ull, 0ull};
-    hipError_t e = hipMemcpyAsync(v, src, sizeof(v), hipMemcpyDeviceToHost, st);
+hipError_t pair_counts_copy(const FrameTotals* src, PairCounts* out, hipStream_t st) {
+    FrameTotals v{};
+    hipError_t e = hipMemcpyAsync(&v, src, sizeof(v), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    out->x = (uint32_t)v[0];
-    out->y = (uint32_t)v[1];
-    *wide = v[2] != 0;
+    out->LA = v.LA;
+    out->LB = v.LB;
+    out->rect = v.rect > 0xffffffffull ? 0xffffffffu : (uint32_t)v.rect;
+    out->wide = v.wide != 0;
     return e;
 }
 
@@ -362,15 +346,16 @@ struct WaitClock {  // adds the scope's duration to the host-wait statistics
     }
 };
 
-hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, bool* wide, hipStream_t st) {
+hipError_t pair_counts_wait(const PairCountRead& r, PairCounts* out, hipStream_t st) {
     WaitClock clock;
     Mailbox& mb = g_mailbox;
-    if (r.seq == 0) return pair_counts_copy(r.copy, out, wide, st);
+    if (r.seq == 0) return pair_counts_copy(r.copy, out, st);
     for (uint32_t spin = 1;; spin++) {
         if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) {
-            out->x = __atomic_load_n(mb.host + 0, __ATOMIC_RELAXED);
-            out->y = __atomic_load_n(mb.host + 1, __ATOMIC_RELAXED);
-            *wide = __atomic_load_n(mb.host + 3, __ATOMIC_RELAXED) != 0;
+            out->LA = __atomic_load_n(mb.host + 0, __ATOMIC_RELAXED);
+            out->rect = __atomic_load_n(mb.host + 1, __ATOMIC_RELAXED);
+            out->wide = __atomic_load_n(mb.host + 3, __ATOMIC_RELAXED) != 0;
+            out->LB = __atomic_load_n(mb.host + 4, __ATOMIC_RELAXED);
             return hipSuccess;
         }
         // the stream is queried only once the wait has outlasted any frame (RR_WAIT_QUERY_MS): a query
@@ -381,12 +366,33 @@ hipError_t pair_counts_wait(const PairCountRead& r, uint2* out, bool* wide, hipS
             if (q == hipSuccess) {
                 if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) continue;
                 mb.failed = true;  // idle stream, value not visible: never use the mailbox again
-                return pair_counts_copy(r.copy, out, wide, st);
+                return pair_counts_copy(r.copy, out, st);
             }
             if (q != hipErrorNotReady) return q;
         }
         __builtin_ia32_pause();
     }
+}
+
+// Phase-A pair counts of recent frames by geometry buffer: rr_forward_geometry (and the sharded
+// step's rr_forward_from_geometry) read them with the frame's one device->host read, and the render
+// call that follows with the same buffer needs the split (the C ABI passes only the total).  A
+// buffer not found here (e.g. geometry rendered by another thread) costs one synchronous read.
+struct SplitMemo {
+    const void* geom = nullptr;
+    uint32_t LA = 0, LB = 0;
+};
+thread_local SplitMemo g_split[4];
+thread_local int g_split_next = 0;
+void remember_split(const void* geom, uint32_t LA, uint32_t LB) {
+    for (SplitMemo& m : g_split)
+        if (m.geom == geom) {
+            m.LA = LA;
+            m.LB = LB;
+            return;
+        }
+    g_split[g_split_next] = SplitMemo{geom, LA, LB};
+    g_split_next = (g_split_next + 1) & 3;
 }
 
 int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, bool forward) {
@@ -435,46 +441,49 @@ PreArgs pre_args(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g)
     return a;
 }
 
-// Depth sort -> pair-count scan -> the one device->host read of the forward, over a geometry buffer
-// whose per-Gaussian arrays (splats, tiles, depth keys, block sums) are filled.
+// Depth cut -> split pair-count scan -> the one device->host read of the forward, over a geometry
+// buffer whose per-Gaussian arrays (splats, tiles, depth keys, block sums) are filled.  No depth
+// sort: the bins' runs are put in depth order by k_sortexpand (rr_bin.hip).
 int count_pairs(const rr_frame* f, const Geom& gm, int P, hipStream_t st, int* num_rendered, int* num_pairs) {
     PairCountRead rd;
-    const PublishJob pub = pair_counts_job(gm.block_sums, gm.block_wide, (P + 255) / 256, gm.totals, rd);
-    // depth sort (rasterizer_impl.cu:295 sorts {tile, depth} keys; here the Gaussians by depth,
-    // then the pairs stably by bin) and the scan of the pair counts in depth order
-    auto sort_and_scan = [&](int key_bits, const PublishJob* publish) -> int {
-        {
-            StageTimer tm(RR_STAGE_DEPTH_SORT, st);
-            size_t tb = gm.temp_bytes;
-            // the culled Gaussians (key 0xffffffff) leave in the first pass: the later passes and
-            // the scan see only the V visible ones (~0.68 P on the bench frames)
-            RR_CHECK(radix_sort_pairs<uint32_t>(gm.temp, tb, gm.depth_keys, gm.depth_keys_sorted, nullptr,
-                                                gm.idx_sorted, (size_t)P, 0, key_bits, st, false, nullptr, nullptr,
-                                                gm.tiles, gm.tiles_sorted, publish, gm.kept),
-                     "depth sort");
+    uint32_t* box = pair_counts_box(gm.ft, rd);
+    const bool full = (f->flags & RR_FLAG_FULL_BINNING) != 0;
+    {
+        StageTimer tm(RR_STAGE_SCAN, st);
+        launch_early_cut(P, gm.depth_keys, gm.tiles, gm.block_sums, gm.block_wide, full ? 1u : g_early_den,
+                         g_early_min, gm.ft, st);
+        launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, box, rd.seq, pair_scan_direct_blocks(),
+                          st);
+        RR_CHECK(hipGetLastError(), "pair-count scan");
+    }
+    RR_STAGE_CHECK("scan");
+    // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin per phase,
+    // and the reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
+    PairCounts c;
+    RR_CHECK(pair_counts_wait(rd, &c, st), "read L");
+    if ((uint64_t)c.LA + c.LB > 0x1fffffffull || c.rect > 0x7fffffffu)
+        return fail(RR_ERR_CAPACITY, "more than 2^29 bin/Gaussian pairs");
+    remember_split(gm.splats, c.LA, c.LB);
+    *num_rendered = (int)c.rect;
+    *num_pairs = (int)(c.LA + c.LB);
+    return RR_OK;
+}
+
+// The split of a frame counted by count_pairs into the geometry buffer at `geom` (a synchronous read
+// of its totals if it is not among the recent ones).
+int frame_split(const void* geom_splats, const FrameTotals* ft, uint32_t L, hipStream_t st, uint32_t* LA,
+                uint32_t* LB) {
+    for (const SplitMemo& m : g_split)
+        if (m.geom == geom_splats && m.LA + m.LB == L) {
+            *LA = m.LA;
+            *LB = m.LB;
+            return RR_OK;
         }
-        RR_STAGE_CHECK("depth sort");
-        {
-            StageTimer tm(RR_STAGE_SCAN, st);
-            launch_pair_scan(gm.tiles_sorted, gm.offsets, P, gm.kept, gm.temp, st);
-            RR_CHECK(hipGetLastError(), "tile-count scan");
-        }
-        RR_STAGE_CHECK("scan");
-        return RR_OK;
-    };
-    if (int rc = sort_and_scan(kDepthKeyBits, &pub)) return rc;
-    // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
-    // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
-    uint2 tot = make_uint2(0u, 0u);
-    bool wide = false;
-    RR_CHECK(pair_counts_wait(rd, &tot, &wide, st), "read L");
-    // a visible depth beyond the 27-bit key range (~13107): the 3-pass order is not the depth
-    // order, so sort again on all 32 bits before anything reads the sorted arrays
-    if (wide)
-        if (int rc = sort_and_scan(32, nullptr)) return rc;
-    if (tot.x > 0x1fffffffu || tot.y > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^29 bin/Gaussian pairs");
-    *num_rendered = (int)tot.y;
-    *num_pairs = (int)tot.x;
+    PairCounts c;
+    RR_CHECK(pair_counts_copy(ft, &c, st), "read split");
+    if (c.LA + c.LB != L) return fail(RR_ERR_ARG, "num_pairs does not match the geometry buffer's frame");
+    *LA = c.LA;
+    *LB = c.LB;
     return RR_OK;
 }
 
@@ -524,30 +533,34 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
 
 namespace {
 
-// Tile lists for one frame: duplicate -> tile sort -> ranges -> blend, once (single phase) or as
-// the two phases of early-stop binning (rr_kernels.hpp BlendPhase).
+// Tile lists for one frame: duplicate -> bin sort -> per-bin depth order + tile lists -> blend,
+// once (single phase) or as the two phases of early-stop binning (rr_kernels.hpp BlendPhase).
+// Phase A's pairs are numbered by the split scan's .x offsets [0, LA), phase B's by .y [0, LB) and
+// staged from position LA of the pair arrays.
 template <typename K>
 int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn, const int* radii, int P, int W,
-                 int H, int cull, bool early, BlendFwdArgs b, hipStream_t st) {
+                 int H, int cull, uint32_t LA, uint32_t LB, BlendFwdArgs b, hipStream_t st) {
     const int gx = grid_x(W), gy = grid_y(H);
-    const uint32_t L = bn.L, LA = early ? bn.LA : bn.L, LB = L - LA;
+    const bool early = LB > 0;
     K* keys = static_cast<K*>(bn.keys);
     K* keys_sorted = static_cast<K*>(bn.keys_sorted);
     DupArgs<K> d{};
-    d.P = P; d.idx_sorted = gm.idx_sorted; d.offsets = gm.offsets; d.splats = gm.splats; d.radii = radii;
+    d.P = P; d.splats = gm.splats; d.radii = radii;
     d.gx = gx; d.gy = gy; d.cull = cull;
-    // phase A (or the only phase): pairs [0, LA) for every tile
+    // phase A (or the only phase): its pairs for every tile
     const RadixPlan pa = tile_plan<K>(bn.temp, LA, bn.bits);
     const RadixPlan pb = tile_plan<K>(bn.temp, LB, bn.bits);  // phase B (early-stop binning)
     bool starts_b = false;  // phase B's window starts computed with phase A's
     if (LA > 0) {
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
+            d.n_list = &gm.ft->GA; d.idx = gm.lists.idx_a; d.off = gm.lists.off_a;
             d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L = LA;
             d.zero = reinterpret_cast<uint32_t*>(im.ranges); d.nzero = (int)(im.zero_bytes / sizeof(uint32_t));
             d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
-            if (early && LB > 0) {
-                d.first_b = bn.first + pa.units; d.pair0_b = LA; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
+            if (early) {
+                d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
+                d.n_list_b = &gm.ft->GB; d.off_b = gm.lists.off_b;
             }
             starts_b = launch_duplicate<K>(d, st);
             d.first_b = nullptr; d.nwin_b = 0;
@@ -562,10 +575,10 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         RR_STAGE_CHECK("bin sort");
         {
             StageTimer tm(RR_STAGE_RANGES, st);
-            launch_expand<K>(LA, nullptr, keys_sorted, bn.vals_sorted, gx, gy, 0u, bn.point_list, im.ranges, nullptr,
-                             st);
+            launch_sortexpand<K>(LA, nullptr, keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u,
+                                 bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, bn.bounds, st);
         }
-        RR_STAGE_CHECK("expand");
+        RR_STAGE_CHECK("sort-expand");
     }
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
@@ -576,10 +589,12 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     }
     RR_STAGE_CHECK("blend forward");
     if (!early) return RR_OK;
-    // phase B: pairs [LA, L), only for tiles phase A left open; positions LA.. of the arrays
+    // phase B: its pairs, only for tiles phase A left open; positions LA.. of the pair arrays
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
-        d.first = bn.first + pa.units; d.pair0 = LA; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units; d.L = L;
+        d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b; d.off = gm.lists.off_b;
+        d.first = bn.first + pa.units; d.pair0 = 0; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units;
+        d.L = LB;
         d.keys = keys + LA; d.vals = bn.vals + LA; d.dbits = pb.dbits0; d.counts = pb.counts;
         d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
         // the backward's tile order on phase A's tile_max (counters[1] = T marks it done; the forward
@@ -588,7 +603,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
             d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
         }
         d.zero = nullptr; d.nzero = 0;
-        d.starts_done = starts_b;
+        d.starts_done = starts_b;  // false when phase A had no pairs (render_frame cleared the ranges)
         launch_duplicate<K>(d, st);
     }
     RR_STAGE_CHECK("duplicate (phase B)");
@@ -601,10 +616,11 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     RR_STAGE_CHECK("bin sort (phase B)");
     {
         StageTimer tm(RR_STAGE_RANGES, st);
-        launch_expand<K>(LB, im.counters, keys_sorted + LA, bn.vals_sorted + LA, gx, gy, 4u * LA, bn.point_list,
-                         im.ranges_b, im.open_bits, st);
+        launch_sortexpand<K>(LB, im.counters, keys_sorted + LA, bn.vals_sorted + LA, gm.depth_keys, gm.ft, gx, gy,
+                             4u * LA, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + LA, bn.scr1 + LA, bn.bounds,
+                             st);
     }
-    RR_STAGE_CHECK("expand (phase B)");
+    RR_STAGE_CHECK("sort-expand (phase B)");
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = kBlendPhaseB;
@@ -694,8 +710,10 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
     if (L > 0 && binning_bytes < bn.total) return fail(RR_ERR_CAPACITY, "binning buffer too small");
     hipStream_t st = (hipStream_t)stream;
     const int gx = grid_x(W), gy = grid_y(H);
-    const bool early = L > 0 && bn.LA < bn.L && !(f->flags & RR_FLAG_FULL_BINNING);
-    if (L == 0 || bn.LA == 0) {  // otherwise the first duplicate launch clears them (DupArgs::zero)
+    uint32_t LA = 0, LB = 0;
+    if (L > 0)
+        if (int rc = frame_split(gm.splats, gm.ft, (uint32_t)L, st, &LA, &LB)) return rc;
+    if (L == 0 || LA == 0) {  // otherwise the first duplicate launch clears them (DupArgs::zero)
         StageTimer tm(RR_STAGE_RANGES, st);
         RR_CHECK(hipMemsetAsync(im.ranges, 0, im.zero_bytes, st), "memset ranges");
     }
@@ -706,8 +724,8 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
     b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
     b.out_color = out_color; b.out_depth = out_depth;
     b.normals = out_normal ? gm.normals : nullptr; b.out_normal = out_normal;
-    return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
-                   : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
+    return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, LA, LB, b, st)
+                   : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, LA, LB, b, st);
 }
 
 }  // namespace
@@ -761,6 +779,26 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
     if (out->grad_accum && (!raw || !out->denom || !out->max_radii2D))
         return fail(RR_ERR_ARG, "densification statistics need raw mode and grad_accum, denom, max_radii2D");
     if (workspace_bytes < rr_backward_workspace_bytes(P)) return fail(RR_ERR_CAPACITY, "workspace too small");
+    const rr_next_frame* nx = out->next;
+    if (nx) {  // cross-step fusion: the next frame's preprocess on the stepped parameters
+        if (!ad) return fail(RR_ERR_ARG, "rr_grads.next needs the fused optimizer step (rr_grads.adam)");
+        if (!nx->frame || !nx->cam || !nx->radii || !nx->geom_buffer)
+            return fail(RR_ERR_ARG, "rr_next_frame: null frame / camera / radii / geometry buffer");
+        const rr_frame* nf = nx->frame;
+        if (nf->P != P || nf->M != f->M || nf->D != f->D || !(nf->flags & RR_FLAG_RAW_PARAMS) ||
+            (nf->flags & RR_FLAG_AUX_NORMAL) || nf->prefiltered)
+            return fail(RR_ERR_ARG, "rr_next_frame: the next frame must have the same P, M and SH degree, raw "
+                                    "parameters, no aux normals, no prefiltering");
+        if (nf->width <= 0 || nf->height <= 0) return fail(RR_ERR_ARG, "rr_next_frame: bad width / height");
+        if (!nx->cam->viewmatrix || !nx->cam->projmatrix || !nx->cam->campos)
+            return fail(RR_ERR_ARG, "rr_next_frame: camera arrays are required");
+        if (nx->geom_bytes < carve_geom(nullptr, P).total) return fail(RR_ERR_CAPACITY, "next geometry buffer too small");
+        if (nx->geom_buffer == geom_buffer) return fail(RR_ERR_ARG, "rr_next_frame: the next frame needs its own geometry buffer");
+        const rr_adam_group* gs[6] = {&ad->xyz, &ad->f_dc, &ad->f_rest, &ad->opacity, &ad->scaling, &ad->rotation};
+        for (int i = 0; i < 6; i++)
+            if (!gs[i]->param && !(i == 2 && f->M <= 1))
+                return fail(RR_ERR_ARG, "rr_next_frame: every Adam group must be stepped");
+    }
     hipStream_t st = (hipStream_t)stream;
     float* gacc = static_cast<float*>(workspace);
     if (int rc2 = blend_backward(f, cam, geom_buffer, image_buffer, binning_buffer, L, dL_dpix, gacc, st)) return rc2;
@@ -783,6 +821,14 @@ int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, 
         a.grad_accum = out->grad_accum; a.denom = out->denom; a.max_radii2D = out->max_radii2D;
         a.use_adam = ad ? 1 : 0;
         if (ad) a.adam = *ad;  // by value: the kernel must not dereference host memory
+        if (nx) {
+            const Geom ng = carve_geom(nx->geom_buffer, P);
+            PreArgs n = pre_args(nx->frame, nx->cam, g);
+            n.radii = nx->radii; n.splats = ng.splats; n.tiles = ng.tiles; n.depth_keys = ng.depth_keys;
+            n.block_sums = ng.block_sums; n.block_wide = ng.block_wide; n.n_out = P;
+            a.next = n;
+            a.has_next = 1;
+        }
         launch_gauss_bwd(a, st);
     }
     RR_STAGE_CHECK("gaussian backward");
@@ -919,7 +965,7 @@ int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int*
     *num_pairs = 0;
     *binning_needed = 0;
     const int P = f->P, W = f->width, H = f->height;
-    if (P < 0 || W <= 0 || H <= 0 || (P % 256) != 0) return fail(RR_ERR_ARG, "P must be a multiple of 256");
+    if (P < 0 || W <= 0 || H <= 0) return fail(RR_ERR_ARG, "bad P / width / height");
     if (f->flags & RR_FLAG_AUX_NORMAL) return fail(RR_ERR_ARG, "row blocks carry no aux normals");
     if (P == 0) return RR_OK;
     if (!radii || !geom_buffer || !image_buffer || !out_color || !out_depth || !cam->background)
@@ -1043,10 +1089,10 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     const Geom gm = carve_geom(const_cast<void*>(geom_buffer), P);
     const Img im = carve_img(const_cast<void*>(image_buffer), W, H);
     hipStream_t st = (hipStream_t)stream;
-    uint2 tot = make_uint2(0u, 0u);
+    FrameTotals ft{};
     std::vector<uint32_t> tm(T);
     std::vector<uint2> per((size_t)P);
-    RR_CHECK(hipMemcpyAsync(&tot, gm.offsets + (P - 1), sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
+    RR_CHECK(hipMemcpyAsync(&ft, gm.ft, sizeof(ft), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(per.data(), gm.tiles, (size_t)P * sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
     uint32_t nb = 0;  // phase-B pairs of the last render into this image buffer
@@ -1055,14 +1101,13 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     int64_t vis = 0;
     for (const uint2& v : per) vis += v.y > 0;  // a Gaussian is visible iff its rect is non-empty (radii > 0)
     out->num_visible = vis;
-    out->num_rendered = tot.y;
-    out->num_pairs = tot.x;
+    out->num_rendered = (int64_t)ft.rect;
+    out->num_pairs = (int64_t)ft.LA + ft.LB;
     int64_t s = 0;
     for (uint32_t v : tm) s += v;
     out->l_eff = s;
-    const uint32_t LA = early_split(tot.x);
-    const bool early = LA < tot.x && !(f->flags & RR_FLAG_FULL_BINNING);
-    out->num_binned = early ? (int64_t)LA + nb : (int64_t)tot.x;
+    // phase A's pairs, and the phase-B pairs kept for the tiles phase A left open
+    out->num_binned = ft.LB > 0 ? (int64_t)ft.LA + nb : (int64_t)ft.LA;
     return RR_OK;
 }
 

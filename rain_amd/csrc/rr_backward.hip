@@ -8,6 +8,7 @@
 #include "adam_math.hpp"
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
+#include "rr_preprocess.hpp"
 
 namespace rr {
 
@@ -110,8 +111,8 @@ __device__ __forceinline__ void put(float* grad, size_t e, float g) {
 // math, then the stores (the compiler cannot batch them itself: the arrays may alias).
 template <int N>
 __device__ __forceinline__ void adam_batch(float* const (&pp)[N], float* const (&mp)[N], float* const (&vp)[N],
-                                           const float (&g)[N], const AdamC (&c)[N]) {
-    float p[N], m[N], v[N];
+                                           const float (&g)[N], const AdamC (&c)[N], float (&p)[N]) {
+    float m[N], v[N];
 #pragma unroll
     for (int i = 0; i < N; i++) {
         p[i] = *pp[i];
@@ -128,7 +129,9 @@ __device__ __forceinline__ void adam_batch(float* const (&pp)[N], float* const (
     }
 }
 
-__device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const SmallGrads& sg) {
+// upd: the 11 parameters after the step (xyz 3, opacity 1, scaling 3, rotation 4), for the next
+// frame's preprocess (rr_next_frame); a group that is not stepped keeps its value.
+__device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const SmallGrads& sg, SmallGrads& upd) {
     const rr_adam& ad = a.adam;
     auto consts = [&](const rr_adam_group& G) {
         return adam_consts(G.lr, G.bias_correction1, G.bias_correction2_sqrt, ad.beta1, ad.beta2, ad.eps);
@@ -166,18 +169,20 @@ __device__ __forceinline__ void adam_small(const GaussBwdArgs& a, int idx, const
             mp[i] = gr[i]->exp_avg + e[i];
             vp[i] = gr[i]->exp_avg_sq + e[i];
         }
-        adam_batch<11>(pp, mp, vp, sg.v, cc);
+        adam_batch<11>(pp, mp, vp, sg.v, cc, upd.v);
         return;
     }
     // a group without param is not stepped (the sharded step of an opacity-reset iteration)
 #pragma unroll
     for (int i = 0; i < 11; i++) {
+        upd.v[i] = 0.f;
         if (!gr[i]->param) continue;
         float p = gr[i]->param[e[i]], m = gr[i]->exp_avg[e[i]], v = gr[i]->exp_avg_sq[e[i]];
         adam_elem(p, sg.v[i], m, v, cc[i]);
         gr[i]->param[e[i]] = p;
         gr[i]->exp_avg[e[i]] = m;
         gr[i]->exp_avg_sq[e[i]] = v;
+        upd.v[i] = p;
     }
 }
 
@@ -452,10 +457,14 @@ __device__ __forceinline__ void gauss_bwd_one(const GaussBwdArgs& a, const ViewC
 // M = 16) are staged into LDS one Gaussian row per wave instruction (coalesced 192-B reads instead
 // of 64 lanes each walking its own 192-B record), and dL/dsh leaves the same way.  Row stride
 // kShStride is odd, so the per-thread row accesses are LDS-bank-conflict free.
+// Single-view kernel: 256 Gaussians per workgroup (the preprocess's block size, so the next frame's
+// per-256-row block sums come out of the same workgroup, rr_next_frame; 128 and 256 measured the
+// same, round 3); multi-view kernel: 128 (it holds two LDS row blocks).
 #ifndef RR_GB_THREADS
-#define RR_GB_THREADS 128
+#define RR_GB_THREADS 256
 #endif
-constexpr int kGB = RR_GB_THREADS;
+constexpr int kGB1 = RR_GB_THREADS;
+constexpr int kGB = 128;
 constexpr int kShStride = 49;
 
 // The per-Gaussian backward of one workgroup of kGB Gaussians.  Single view (MULTI false): the
@@ -465,14 +474,14 @@ constexpr int kShStride = 49;
 // (11 small-group values) and into s_gr (the SH gradients; s_sh keeps the coefficients), then
 // scaled by va->grad_scale (1/N, rounded like grad.mul_(1/N)) before the Adam step.
 struct GaussBwdViewsArgs;
-template <int DEG, bool MULTI>
+template <int DEG, bool MULTI, int KGB>
 __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const GaussBwdViewsArgs* va, float* s_sh,
                                                 float* s_gr);
 
 template <int DEG>
-__global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
-    __shared__ float s_sh[kGB * kShStride];
-    gauss_bwd_block<DEG, false>(a, nullptr, s_sh, s_sh);
+__global__ __launch_bounds__(kGB1) void k_gauss_bwd(GaussBwdArgs a) {
+    __shared__ float s_sh[kGB1 * kShStride];
+    gauss_bwd_block<DEG, false, kGB1>(a, nullptr, s_sh, s_sh);
 }
 
 constexpr int kMaxViews = 16;
@@ -490,15 +499,15 @@ template <int DEG>
 __global__ __launch_bounds__(kGB) void k_gauss_bwd_views(GaussBwdViewsArgs va) {
     __shared__ float s_sh[kGB * kShStride];
     __shared__ float s_gr[kGB * kShStride];
-    gauss_bwd_block<DEG, true>(va.g, &va, s_sh, s_gr);
+    gauss_bwd_block<DEG, true, kGB>(va.g, &va, s_sh, s_gr);
 }
 
-template <int DEG, bool MULTI>
+template <int DEG, bool MULTI, int KGB>
 __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const GaussBwdViewsArgs* va, float* s_sh,
                                                 float* s_gr) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int i0 = blockIdx.x * kGB;
-    const int nvalid = min(kGB, a.P - i0);
+    const int i0 = blockIdx.x * KGB;
+    const int nvalid = min(KGB, a.P - i0);
     const int M = a.M, nf = 3 * M;  // floats per Gaussian
     const bool stage = M > 0 && (a.shs != nullptr || a.dL_dsh != nullptr || a.use_adam);
     if (stage && a.shs) {
@@ -518,12 +527,12 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                 float4 buf[12];
 #pragma unroll
                 for (int q = 0; q < 12; q++) {
-                    const int i = t + q * kGB;
+                    const int i = t + q * KGB;
                     buf[q] = i < nv ? reinterpret_cast<const float4*>(base)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
                 for (int q = 0; q < 12; q++) {
-                    const int i = t + q * kGB;
+                    const int i = t + q * KGB;
                     if (i < nv) {
                         put_lds(4 * i, buf[q].x);
                         put_lds(4 * i + 1, buf[q].y);
@@ -531,18 +540,18 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                         put_lds(4 * i + 3, buf[q].w);
                     }
                 }
-                for (int e = 4 * nv + t; e < total; e += kGB) put_lds(e, base[e]);
+                for (int e = 4 * nv + t; e < total; e += KGB) put_lds(e, base[e]);
                 return;
             }
             float buf[48];
 #pragma unroll
             for (int q = 0; q < 48; q++) {
-                const int e = t + q * kGB;
+                const int e = t + q * KGB;
                 buf[q] = e < total ? base[e] : 0.f;
             }
 #pragma unroll
             for (int q = 0; q < 48; q++) {
-                const int e = t + q * kGB;
+                const int e = t + q * KGB;
                 if (e < total) put_lds(e, buf[q]);
             }
         };
@@ -554,6 +563,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
         }
     }
     __syncthreads();
+    SmallGrads upd;  // the small groups' parameters after the fused Adam step (rr_next_frame)
     if (t < nvalid) {
         SmallGrads sg;
         const int idx = i0 + t;
@@ -587,9 +597,11 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
 #pragma unroll
             for (int i = 0; i < 11; i++) sg.v[i] = mul_rounded(sg.v[i], va->grad_scale);
         }
-        if (a.use_adam) adam_small(a, i0 + t, sg);
+        if (a.use_adam) adam_small(a, i0 + t, sg, upd);
     }
     __syncthreads();
+    // the next frame's preprocess reads the updated SH coefficients back from the LDS rows
+    const bool back = !MULTI && a.has_next;
     if (stage && (a.dL_dsh || a.use_adam)) {
         // gradients leave coalesced; with the fused step the SH groups' Adam runs here, on the
         // same flat element order
@@ -608,6 +620,10 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                 const float g = s_gr[j * kShStride + koff + (e - j * w)];
                 return MULTI ? mul_rounded(g, va->grad_scale) : g;
             };
+            auto put_back = [&](int e, float x) {  // the updated coefficient into its LDS row slot
+                const int j = (int)(((float)e + 0.5f) * inv);
+                s_gr[j * kShStride + koff + (e - j * w)] = x;
+            };
             const size_t gb = (size_t)i0 * w;
             const uintptr_t al = (grp ? ((uintptr_t)(grp->param + gb) | (uintptr_t)(grp->exp_avg + gb) |
                                          (uintptr_t)(grp->exp_avg_sq + gb))
@@ -617,11 +633,11 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                 // float4 per lane: kB / 4 vectors per batch, (param, m, v) loads all in flight
                 constexpr int kV = kB / 4 > 0 ? kB / 4 : 1;
                 const int nv = total >> 2;
-                for (int v0 = t; v0 < nv; v0 += kV * kGB) {
+                for (int v0 = t; v0 < nv; v0 += kV * KGB) {
                     float4 g4[kV], p4[kV], m4[kV], s4[kV];
 #pragma unroll
                     for (int q = 0; q < kV; q++) {
-                        const int i = min(v0 + q * kGB, nv - 1);  // clamped duplicates are not stored
+                        const int i = min(v0 + q * KGB, nv - 1);  // clamped duplicates are not stored
                         g4[q] = make_float4(grad_at(4 * i), grad_at(4 * i + 1), grad_at(4 * i + 2), grad_at(4 * i + 3));
                         if (grp) {
                             p4[q] = reinterpret_cast<const float4*>(grp->param + gb)[i];
@@ -631,7 +647,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                     }
 #pragma unroll
                     for (int q = 0; q < kV; q++) {
-                        const int i = v0 + q * kGB;
+                        const int i = v0 + q * KGB;
                         if (i >= nv) break;
                         if (dst) reinterpret_cast<float4*>(dst + gb)[i] = g4[q];
                         if (grp) {
@@ -642,10 +658,16 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                             reinterpret_cast<float4*>(grp->param + gb)[i] = p4[q];
                             reinterpret_cast<float4*>(grp->exp_avg + gb)[i] = m4[q];
                             reinterpret_cast<float4*>(grp->exp_avg_sq + gb)[i] = s4[q];
+                            if (back) {
+                                put_back(4 * i, p4[q].x);
+                                put_back(4 * i + 1, p4[q].y);
+                                put_back(4 * i + 2, p4[q].z);
+                                put_back(4 * i + 3, p4[q].w);
+                            }
                         }
                     }
                 }
-                for (int e = 4 * nv + t; e < total; e += kGB) {  // tail (< 4 elements)
+                for (int e = 4 * nv + t; e < total; e += KGB) {  // tail (< 4 elements)
                     const float g = grad_at(e);
                     put(dst, gb + e, g);
                     if (grp) {
@@ -654,11 +676,12 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                         grp->param[gb + e] = p;
                         grp->exp_avg[gb + e] = m;
                         grp->exp_avg_sq[gb + e] = v;
+                        if (back) put_back(e, p);
                     }
                 }
                 return;
             }
-            for (int e0 = t; e0 < total; e0 += kB * kGB) {
+            for (int e0 = t; e0 < total; e0 += kB * KGB) {
                 float g[kB];
                 float* pp[kB];
                 float* mp[kB];
@@ -667,7 +690,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                 int n = 0;
 #pragma unroll
                 for (int q = 0; q < kB; q++) {
-                    const int e = e0 + q * kGB;
+                    const int e = e0 + q * KGB;
                     const bool ok = e < total;
                     const int ee = ok ? e : e0;  // e0 < total: a valid dummy for the unused lanes of the batch
                     g[q] = grad_at(ee);
@@ -681,9 +704,10 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                         cq[q] = c;
                     }
                 }
+                float pn[kB];
                 if (grp) {
                     if (n == kB) {
-                        adam_batch<kB>(pp, mp, vp, g, cq);
+                        adam_batch<kB>(pp, mp, vp, g, cq, pn);
                     } else {  // tail: one at a time, never touching an element twice
                         for (int q = 0; q < n; q++) {
                             float p = *pp[q], m = *mp[q], v = *vp[q];
@@ -691,8 +715,11 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                             *pp[q] = p;
                             *mp[q] = m;
                             *vp[q] = v;
+                            pn[q] = p;
                         }
                     }
+                    if (back)
+                        for (int q = 0; q < n; q++) put_back(e0 + q * KGB, pn[q]);
                 }
             }
         };
@@ -702,6 +729,33 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
         } else {
             stage_out(a.dL_dsh, ad ? &ad->f_dc : nullptr, 3, 0);
             if (nf > 3) stage_out(a.dL_dsh_rest, ad ? &ad->f_rest : nullptr, nf - 3, 3);
+        }
+    }
+    if constexpr (!MULTI && KGB == 256) {
+        if (back) {
+            // Cross-step fusion (include/rain_raster.h rr_next_frame): the next frame's preprocess
+            // (forward.cu:144-246) of this block's Gaussians on the parameters this pass has just
+            // stepped — xyz / opacity / scaling / rotation from registers, the SH coefficients from
+            // the LDS rows — with the forward preprocess's own code (rr_preprocess.hpp), so the
+            // geometry equals what k_preprocess would compute from the stored parameters.
+            __syncthreads();
+            const PreArgs& nx = a.next;
+            bool wide = false;
+            uint2 c = make_uint2(0u, 0u);
+            if (t < nvalid) {
+                const int idx = i0 + t;
+                preprocess_clear(nx, idx);
+                const v3 p = mk(upd.v[0], upd.v[1], upd.v[2]);
+                const v3 p_view = xform_point_4x3(p, nx.view);  // in_frustum (auxiliary.h:128-153)
+                if (p_view.z > 0.2f) {
+                    const float* row = s_sh + t * kShStride;
+                    c = preprocess_finish<DEG, false>(nx, idx, p, p_view,
+                                                      make_float4(upd.v[7], upd.v[8], upd.v[9], upd.v[10]),
+                                                      mk(upd.v[4], upd.v[5], upd.v[6]), upd.v[3],
+                                                      mk(row[0], row[1], row[2]), row + 3, wide);
+                }
+            }
+            preprocess_block_sums(nx, blockIdx.x, c, wide);
         }
     }
 }
@@ -765,12 +819,12 @@ void launch_pack_records(const float* gacc, const int* radii, int P, int Q, int 
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st) {
     if (a.P == 0) return;
     // a.M <= 16 is validated by the API: the LDS row holds at most 16 coefficients
-    const int nb = (a.P + kGB - 1) / kGB;
+    const int nb = (a.P + kGB1 - 1) / kGB1;
     switch (a.shs ? a.D : 0) {
-        case 0: k_gauss_bwd<0><<<nb, kGB, 0, st>>>(a); break;
-        case 1: k_gauss_bwd<1><<<nb, kGB, 0, st>>>(a); break;
-        case 2: k_gauss_bwd<2><<<nb, kGB, 0, st>>>(a); break;
-        default: k_gauss_bwd<3><<<nb, kGB, 0, st>>>(a); break;
+        case 0: k_gauss_bwd<0><<<nb, kGB1, 0, st>>>(a); break;
+        case 1: k_gauss_bwd<1><<<nb, kGB1, 0, st>>>(a); break;
+        case 2: k_gauss_bwd<2><<<nb, kGB1, 0, st>>>(a); break;
+        default: k_gauss_bwd<3><<<nb, kGB1, 0, st>>>(a); break;
     }
 }
 

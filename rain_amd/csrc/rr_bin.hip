@@ -1,0 +1,613 @@
+// rr_bin.hip — binning without a per-frame depth sort.
+//
+// The reference sorts 64-bit (tile << 32 | depth bits) keys emitted in Gaussian index order
+// (rasterizer_impl.cu:59-100, 292-300), so every tile's list is in (depth, index) order.  Rounds
+// 1-3 of this build got that order from a global stable depth sort of the P Gaussians (3 radix
+// passes = 9 launches per frame) followed by a stable bin sort of the pairs emitted in depth order.
+// Here the pairs are emitted in INDEX order, stable-sorted by bin id only (rr_sort.hip, 2 passes),
+// and every bin's run — index-ordered, ~10^3 pairs — is sorted by depth inside one workgroup
+// (k_sortexpand: stable LSD radix sort in LDS on the Gaussian's depth key), which yields the same
+// (depth, index) order per bin, and so per tile, at a fraction of the launches.
+//
+// Early-stop binning (rr_kernels.hpp BlendPhase) splits the pairs by DEPTH instead of by depth
+// rank: phase A holds the pairs of the Gaussians nearer than a cut chosen per frame from a sampled,
+// pair-weighted depth histogram (k_early_cut: ~1/den of the pairs), phase B the others.  Each
+// tile's phase-A list is then a prefix of its full depth-ordered list and the B list the rest, which
+// is all the two-phase blend needs (any cut gives the full lists' outputs).
+//
+//   k_early_cut        one workgroup: frame totals from the preprocess block sums, the depth cut
+//   k_split_scan_*     inclusive scan of {A pairs, B pairs} per Gaussian in index order; its last
+//                      thread publishes the frame's counts to the host (rr_api.hip mailbox)
+//   k_sortexpand<K>    per bin: depth sort of its run + the split into its four tiles' lists
+#include <algorithm>
+
+#include "rr_common.hpp"
+#include "rr_kernels.hpp"
+
+namespace rr {
+
+// ---- the depth cut of early-stop binning ------------------------------------------------------
+// Pair-weighted histogram of the sampled Gaussians' depth keys (key >> kCutShift, 4096 buckets over
+// the 27-bit key range; deeper keys share the last bucket), then the first bucket whose inclusive
+// prefix reaches 1/den of the sampled pairs: phase A takes the keys below that bucket's end.
+// den <= 1, a frame below min_pairs pairs or no sampled pair: cut = all ones (one phase).
+constexpr int kCutBuckets = 4096;
+constexpr int kCutShift = kDepthKeyBits - 12;
+constexpr int kCutSamplesPerThread = 16;  // <= 16384 samples (one workgroup of 1024 threads)
+
+__global__ __launch_bounds__(1024) void k_early_cut(int P, int stride, const uint32_t* __restrict__ keys,
+                                                    const uint2* __restrict__ tiles,
+                                                    const uint2* __restrict__ block_sums,
+                                                    const uint32_t* __restrict__ block_wide, int nb, uint32_t den,
+                                                    uint32_t min_pairs, FrameTotals* __restrict__ ft) {
+    __shared__ unsigned long long hist[kCutBuckets];
+    __shared__ unsigned long long s_red[3][16];
+    __shared__ uint32_t s_wide, s_cut;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int i = t; i < kCutBuckets; i += 1024) hist[i] = 0ull;
+    if (t == 0) {
+        s_wide = 0u;
+        s_cut = 0xffffffffu;
+    }
+    unsigned long long L = 0, rect = 0, S = 0;
+    uint32_t wide = 0;
+    for (int i = t; i < nb; i += 1024) {
+        const uint2 v = block_sums[i];
+        L += v.x;
+        rect += v.y;
+        wide |= block_wide[i];
+    }
+    __syncthreads();
+    // <= kCutSamplesPerThread samples per thread, all loads in flight before the first LDS atomic
+    const int ns = (P + stride - 1) / stride;
+    uint32_t sn[kCutSamplesPerThread], sk[kCutSamplesPerThread];
+#pragma unroll
+    for (int r = 0; r < kCutSamplesPerThread; r++) {  // unconditional loads (clamped index): no branch
+        const int i = t + r * 1024;                      // and wait per sample
+        const size_t idx = (size_t)min(i, ns - 1) * stride;
+        const uint32_t n = tiles[idx].x, k = keys[idx];
+        sn[r] = i < ns ? n : 0u;
+        sk[r] = k;
+    }
+#pragma unroll
+    for (int r = 0; r < kCutSamplesPerThread; r++)
+        if (sn[r]) {
+            atomicAdd(&hist[min(sk[r] >> kCutShift, (uint32_t)kCutBuckets - 1u)], (unsigned long long)sn[r]);
+            S += sn[r];
+        }
+    if (wide) atomicOr(&s_wide, 1u);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        L += __shfl_xor(L, o);
+        rect += __shfl_xor(rect, o);
+        S += __shfl_xor(S, o);
+    }
+    if (lane == 0) {
+        s_red[0][w] = L;
+        s_red[1][w] = rect;
+        s_red[2][w] = S;
+    }
+    __syncthreads();
+    L = rect = S = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        L += s_red[0][i];
+        rect += s_red[1][i];
+        S += s_red[2][i];
+    }
+    const bool one_phase = den <= 1u || L < (unsigned long long)min_pairs || S == 0ull;
+    if (!one_phase) {
+        // 4 buckets per thread, block-wide inclusive scan of their sums
+        constexpr int BPT = kCutBuckets / 1024;
+        unsigned long long v[BPT], sum = 0;
+#pragma unroll
+        for (int k = 0; k < BPT; k++) {
+            v[k] = hist[BPT * t + k];
+            sum += v[k];
+        }
+        unsigned long long incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        __syncthreads();  // s_red reads above are done
+        if (lane == 63) s_red[0][w] = incl;
+        __syncthreads();
+        unsigned long long run = incl - sum;
+        for (int i = 0; i < w; i++) run += s_red[0][i];
+        // first bucket whose inclusive prefix reaches S / den (prefix * den >= S)
+#pragma unroll
+        for (int k = 0; k < BPT; k++) {
+            run += v[k];
+            if (run * den >= S) {
+                const uint32_t b = (uint32_t)(BPT * t + k);
+                atomicMin(&s_cut, b + 1u >= (uint32_t)kCutBuckets ? 0xffffffffu : (b + 1u) << kCutShift);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        ft->L = L;
+        ft->rect = rect;
+        ft->wide = s_wide;
+        ft->cut = one_phase ? 0xffffffffu : s_cut;
+    }
+}
+
+void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
+                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, hipStream_t st) {
+    // every Gaussian of frames up to 16384, else evenly spaced samples (16384 at most: ~1 in 61 at 1M)
+    const int stride = std::max(1, (P + 16383) / 16384);
+    k_early_cut<<<1, 1024, 0, st>>>(P, stride, keys, tiles, block_sums, block_wide, (P + 255) / 256, den, min_pairs,
+                                    ft);
+}
+
+// ---- the phases' Gaussian lists: scan of {A pairs, B pairs, A rows, B rows} in index order ------
+// Gaussian i has n_i bin pairs; it belongs to phase A if n_i > 0 and its depth key < cut, to phase B
+// if n_i > 0 otherwise.  One inclusive scan of the four counts gives every phase's list in index
+// order: list_X[r] = {Gaussian index, inclusive pair offset} of the phase's r-th Gaussian — what
+// the duplicate walks (its windows cover consecutive pairs of one list, so a window visits only the
+// Gaussians it emits for, as the depth-ordered lists of rounds 1-3 did).  Pair offsets saturate at
+// 2^32 - 1 (the host rejects totals above 2^29).  Blocks of kPairScanItems; the block totals are
+// summed by every later block (2 launches) or first scanned by one workgroup (large P).
+struct Quad {
+    unsigned long long pa, pb, ca, cb;
+};
+__device__ __forceinline__ Quad quad_add(Quad x, Quad y) { return Quad{x.pa + y.pa, x.pb + y.pb, x.ca + y.ca, x.cb + y.cb}; }
+__device__ __forceinline__ Quad quad_shfl_up(Quad x, int o) {
+    return Quad{__shfl_up(x.pa, o), __shfl_up(x.pb, o), __shfl_up(x.ca, o), __shfl_up(x.cb, o)};
+}
+__device__ __forceinline__ Quad quad_shfl_xor(Quad x, int o) {
+    return Quad{__shfl_xor(x.pa, o), __shfl_xor(x.pb, o), __shfl_xor(x.ca, o), __shfl_xor(x.cb, o)};
+}
+__device__ __forceinline__ Quad split_item(const uint2* tiles, const uint32_t* keys, uint32_t cut, size_t i) {
+    const uint32_t n = tiles[i].x;
+    const bool a = keys[i] < cut;
+    return Quad{a ? n : 0ull, a ? 0ull : n, (a && n) ? 1ull : 0ull, (!a && n) ? 1ull : 0ull};
+}
+// block-wide sum of one Quad per thread (256 threads); s: [4] Quads
+__device__ __forceinline__ Quad quad_block_sum(Quad x, Quad* s) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = quad_add(x, quad_shfl_xor(x, o));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) s[w] = x;
+    __syncthreads();
+    return quad_add(quad_add(s[0], s[1]), quad_add(s[2], s[3]));
+}
+
+__global__ __launch_bounds__(256) void k_split_scan_totals(const uint2* __restrict__ tiles,
+                                                           const uint32_t* __restrict__ keys, int P,
+                                                           const FrameTotals* __restrict__ ft, Quad* __restrict__ tot) {
+    __shared__ Quad s[4];
+    const uint32_t cut = ft->cut;
+    const size_t b0 = (size_t)blockIdx.x * kPairScanItems;
+    Quad x{0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < kPairScanItems / 256; r++) {
+        const size_t i = b0 + (size_t)r * 256 + threadIdx.x;
+        if (i < (size_t)P) x = quad_add(x, split_item(tiles, keys, cut, i));
+    }
+    x = quad_block_sum(x, s);
+    if (threadIdx.x == 0) tot[blockIdx.x] = x;
+}
+
+// Exclusive scan, in place, of nb block totals (one workgroup; large P, where re-summing the earlier
+// totals in every block would grow with nb^2).
+__global__ __launch_bounds__(256) void k_split_scan_prefix(Quad* __restrict__ tot, int nb) {
+    __shared__ Quad s_w[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    Quad carry{0, 0, 0, 0};
+    for (int base = 0; base < nb; base += 256) {
+        const int i = base + t;
+        const Quad v = i < nb ? tot[i] : Quad{0, 0, 0, 0};
+        Quad incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const Quad y = quad_shfl_up(incl, o);
+            if (lane >= o) incl = quad_add(incl, y);
+        }
+        __syncthreads();
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        Quad ex = quad_add(carry, Quad{incl.pa - v.pa, incl.pb - v.pb, incl.ca - v.ca, incl.cb - v.cb});
+        for (int k = 0; k < w; k++) ex = quad_add(ex, s_w[k]);
+        if (i < nb) tot[i] = ex;
+        carry = quad_add(carry, quad_add(quad_add(s_w[0], s_w[1]), quad_add(s_w[2], s_w[3])));
+    }
+}
+
+__device__ __forceinline__ uint32_t sat32(unsigned long long v) { return v > 0xffffffffull ? 0xffffffffu : (uint32_t)v; }
+
+// The frame's counts to the host: {L_A, rect, seq, wide, L_B} into the coherent pinned mailbox (the
+// sequence number last, system-scope release; rr_api.hip pair_counts_wait spins on it) and into ft.
+__device__ __forceinline__ void publish_counts(FrameTotals* ft, const Quad& q, uint32_t* box, uint32_t seq) {
+    const uint32_t a = sat32(q.pa), b = sat32(q.pb), r = sat32(ft->rect), wd = ft->wide;
+    ft->LA = a;
+    ft->LB = b;
+    ft->GA = (uint32_t)q.ca;
+    ft->GB = (uint32_t)q.cb;
+    if (box) {
+        __hip_atomic_store(box + 0, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(box + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(box + 3, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(box + 4, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <bool PREFIX>
+__global__ __launch_bounds__(256) void k_split_scan(const uint2* __restrict__ tiles, const uint32_t* __restrict__ keys,
+                                                    int P, const Quad* __restrict__ tot, PhaseLists lists,
+                                                    FrameTotals* __restrict__ ft, uint32_t* box, uint32_t seq) {
+    constexpr int IPT = kPairScanItems / 256;  // 8 consecutive items per thread
+    __shared__ Quad s[4];
+    __shared__ Quad s_w[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t cut = ft->cut;
+    const size_t i0 = (size_t)blockIdx.x * kPairScanItems + (size_t)t * IPT;
+    Quad v[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; k++) v[k] = i0 + k < (size_t)P ? split_item(tiles, keys, cut, i0 + k) : Quad{0, 0, 0, 0};
+    Quad base{0, 0, 0, 0};
+    if (PREFIX) {
+        base = tot[blockIdx.x];
+    } else {
+        for (int j = t; j < (int)blockIdx.x; j += 256) base = quad_add(base, tot[j]);
+        base = quad_block_sum(base, s);
+    }
+    Quad tsum{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < IPT; k++) tsum = quad_add(tsum, v[k]);
+    Quad incl = tsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const Quad y = quad_shfl_up(incl, o);
+        if (lane >= o) incl = quad_add(incl, y);
+    }
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    Quad ex = quad_add(base, Quad{incl.pa - tsum.pa, incl.pb - tsum.pb, incl.ca - tsum.ca, incl.cb - tsum.cb});
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < w) ex = quad_add(ex, s_w[k]);
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+        const size_t i = i0 + k;
+        const Quad e = ex;  // exclusive counts before item i
+        ex = quad_add(ex, v[k]);
+        if (v[k].ca) {
+            lists.idx_a[e.ca] = (uint32_t)i;
+            lists.off_a[e.ca] = sat32(ex.pa);
+        } else if (v[k].cb) {
+            lists.idx_b[e.cb] = (uint32_t)i;
+            lists.off_b[e.cb] = sat32(ex.pb);
+        }
+    }
+    // the last thread of the grid holds the frame's totals (items past P count as 0)
+    if (blockIdx.x == gridDim.x - 1 && t == 255) publish_counts(ft, ex, box, seq);
+}
+
+size_t split_scan_temp_bytes(int P) {
+    return (size_t)std::max((P + kPairScanItems - 1) / kPairScanItems, 1) * sizeof(Quad);
+}
+
+void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
+                       uint32_t* box, uint32_t seq, int direct_blocks, hipStream_t st) {
+    if (P <= 0) return;
+    const int nb = (P + kPairScanItems - 1) / kPairScanItems;
+    Quad* tot = static_cast<Quad*>(temp);
+    k_split_scan_totals<<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot);
+    if (nb <= direct_blocks) {
+        k_split_scan<false><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft, box, seq);
+    } else {
+        k_split_scan_prefix<<<1, 256, 0, st>>>(tot, nb);
+        k_split_scan<true><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft, box, seq);
+    }
+}
+
+// ---- per bin: depth order + the four tile lists -----------------------------------------------
+// A bin's run of the bin-sorted pairs holds one pair per Gaussian in index order (stable bin sort of
+// index-ordered emission).  A stable LSD radix sort on the Gaussians' depth keys (3 passes of 9
+// bits, or 4 of 8 when a visible key needs more than 27 bits) makes it (depth, index) order — the
+// reference's per-tile order (rasterizer_impl.cu:292-300) — and the run is then split stably into
+// its tiles' lists (one ballot per mask bit), written at out_base + 4 lo + b len with the tile's
+// range (rasterizer_impl.cu:105-127).  Runs of up to kSxCap pairs are sorted in LDS, longer ones
+// pass through the scratch arrays in chunks of kSxCap (same ranking, one global digit scan per
+// pass).  Ranking (rr_sort.hip's): wave w owns the contiguous items [w 64 R, (w + 1) 64 R) in
+// rounds of 64; lanes holding the same digit find each other with one ballot per digit bit.
+constexpr int kSxCap = 4096;
+constexpr int kSxMaxR = kSxCap / 256;
+#ifndef RR_SX_GLOBAL
+#define RR_SX_GLOBAL 1  // 0: ISA inspection builds without the long-run path
+#endif
+
+struct SxShared {
+    uint32_t k[kSxCap];
+    uint32_t v[kSxCap];
+    uint32_t wcnt[4][512];  // per-wave digit counts, then per-wave cursors
+    uint32_t cursor[512];   // global path: next slot of each digit across the chunks
+    uint32_t wsum[4][4];
+};
+
+// One chunk's items (registers kr / vr, R rounds, `len` valid) ranked on digit (key >> shift) & mask
+// and stored at base[d] + (rank among the chunk's digit-d items, in input order) — to LDS
+// (dst_lds) or to a global scratch run (dst_g).  base: the digit's first slot (LDS path: the
+// chunk's exclusive digit prefix; global path: cursor[d]).  Ends with the chunk's digit counts
+// added to cursor (global path).
+__device__ __forceinline__ void sx_rank_chunk(SxShared& sh, const uint32_t (&kr)[kSxMaxR],
+                                              const uint32_t (&vr)[kSxMaxR], int R, uint32_t len, int shift, int db,
+                                              bool global, uint2* dst_g) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int ndig = 1 << db;
+    const uint32_t mask = (uint32_t)ndig - 1u;
+    const uint32_t wl = (uint32_t)w * 64 * R;
+    for (int d = lane; d < ndig; d += 64) sh.wcnt[w][d] = 0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < kSxMaxR; r++)
+        if (r < R && wl + (uint32_t)r * 64 + lane < len) atomicAdd(&sh.wcnt[w][(kr[r] >> shift) & mask], 1u);
+    __syncthreads();
+    if (w == 0) {  // digits in order, waves in order inside a digit (DPL consecutive digits per lane)
+        const int dpl = ndig / 64;
+        uint32_t sum = 0;
+        for (int i = 0; i < dpl; i++) {
+            const int d = dpl * lane + i;
+            sum += sh.wcnt[0][d] + sh.wcnt[1][d] + sh.wcnt[2][d] + sh.wcnt[3][d];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += y;
+        }
+        uint32_t run = incl - sum;
+        for (int i = 0; i < dpl; i++) {
+            const int d = dpl * lane + i;
+            uint32_t r2 = global ? sh.cursor[d] : run, tot = 0;
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const uint32_t x = sh.wcnt[v][d];
+                sh.wcnt[v][d] = r2;
+                r2 += x;
+                tot += x;
+            }
+            if (global) sh.cursor[d] += tot;
+            run += tot;
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < kSxMaxR; r++) {
+        if (r >= R || wl + (uint32_t)r * 64 >= len) continue;  // wave-uniform
+        const bool valid = wl + (uint32_t)r * 64 + lane < len;
+        const uint32_t d = (kr[r] >> shift) & mask;
+        uint64_t m = __ballot(valid);
+        for (int b = 0; b < db; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & lt);
+        const uint32_t pos = sh.wcnt[w][d] + rank;  // every lane reads before any leader writes
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rank == 0) sh.wcnt[w][d] = pos + (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+        if (valid) {
+            if (global) {
+                dst_g[pos] = make_uint2(kr[r], vr[r]);
+            } else {
+                sh.k[pos] = kr[r];
+                sh.v[pos] = vr[r];
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// Every bin's run [start, end) of the bin-sorted keys, written by the boundaries around it: between
+// positions i and i + 1 holding bins a < b, bins a+1..b start and bins a..b-1 end at i + 1 (empty
+// bins in the gap get start = end); the head and the tail close the bins below the first key and
+// above the last.  Every bin is written exactly once, so the array needs no clearing.  One launch
+// over the pairs instead of a binary search in every k_sortexpand workgroup.
+template <typename K>
+__global__ __launch_bounds__(256) void k_bin_bounds(uint32_t n_host, const uint32_t* __restrict__ n_dev,
+                                                    const K* __restrict__ keys, int nbins, uint2* __restrict__ bounds) {
+    const uint32_t n = n_dev ? *n_dev : n_host;
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (n == 0) {  // no pairs: every run empty
+        for (uint32_t b = i; b < (uint32_t)nbins; b += gridDim.x * 256u) bounds[b] = make_uint2(0u, 0u);
+        return;
+    }
+    if (i >= n) return;
+    const uint32_t k = (uint32_t)keys[i];
+    const uint32_t kp = i == 0 ? 0xffffffffu : (uint32_t)keys[i - 1];  // "bin -1"
+    const uint32_t kn = i + 1 == n ? (uint32_t)nbins : (uint32_t)keys[i + 1];
+    if (k != kp)  // bins kp+1 .. k start at i (and the empty ones among them end there)
+        for (uint32_t b = kp + 1u; b <= k; b++) {
+            if (b < k) bounds[b] = make_uint2(i, i);
+            else bounds[b].x = i;
+        }
+    if (k != kn) {  // bin k ends at i + 1; the empty bins k+1 .. kn-1 start and end there
+        bounds[k].y = i + 1;
+        for (uint32_t b = k + 1u; b < kn && b < (uint32_t)nbins; b++) bounds[b] = make_uint2(i + 1, i + 1);
+    }
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bounds,
+                                                    const K* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ depth_keys,
+                                                    const FrameTotals* __restrict__ ft, int gx, int gy,
+                                                    uint32_t out_base, uint32_t* __restrict__ point_list,
+                                                    uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits,
+                                                    uint2* __restrict__ scr0, uint2* __restrict__ scr1) {
+    __shared__ SxShared sh;
+    const int bgx = bins_x(gx);
+    const int bin = blockIdx.x;
+    const int X = bin % bgx, Y = bin / bgx;
+    if (open_bits) {  // phase B: a bin whose tiles all closed in phase A holds no pair, and its
+                      // tiles' ranges were cleared with the frame's: nothing to search or write
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int tx = 2 * X + (b & 1), ty = 2 * Y + (b >> 1);
+            if (tx < gx && ty < gy) {
+                const uint32_t tile = (uint32_t)(ty * gx + tx);
+                any = any || ((open_bits[tile >> 5] >> (tile & 31)) & 1u);
+            }
+        }
+        if (!any) return;  // block-uniform
+    }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint2 run = bounds[bin];  // the bin's run [lo, hi) of the bin-sorted pairs
+    const uint32_t lo = run.x, hi = run.y;
+    const uint32_t len = hi - lo;
+    // 27-bit keys in 3 passes of 9 bits, wider frames in 4 of 8
+    const bool wide = ft->wide != 0u;
+    const int passes = wide ? 4 : 3, db = wide ? 8 : 9;
+    const uint2* sorted_g = nullptr;  // global path: the sorted run
+    if (len > 1 && len <= (uint32_t)kSxCap) {
+        const int R = (int)((len + 255) / 256);
+        const uint32_t wl = (uint32_t)w * 64 * R;
+        uint32_t kr[kSxMaxR], vr[kSxMaxR];
+        // every round's loads unconditional, the index clamped into the run: a condition (per lane or
+        // on R) made the compiler branch and wait around each load; the clamped extra loads hit the
+        // cache line of the run's last item and are never used (items past len are not ranked)
+#pragma unroll
+        for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + min(wl + (uint32_t)r * 64 + lane, len - 1)];
+#pragma unroll
+        for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
+        for (int p = 0; p < passes; p++) {
+            sx_rank_chunk(sh, kr, vr, R, len, p * db, db, false, nullptr);
+            if (p + 1 < passes) {
+#pragma unroll
+                for (int r = 0; r < kSxMaxR; r++) {
+                    const uint32_t i = wl + (uint32_t)r * 64 + lane;
+                    if (r < R && i < len) {
+                        kr[r] = sh.k[i];
+                        vr[r] = sh.v[i];
+                    }
+                }
+                __syncthreads();  // every read of this pass's order before the next pass's writes
+            }
+        }
+    } else if (RR_SX_GLOBAL && len > (uint32_t)kSxCap) {
+        // chunks of kSxCap in order; pass p reads run p - 1 (pass 0: the bin-sorted values with their
+        // gathered depth keys) and writes the run at lo of scratch p % 2
+        const int ndig = 1 << db;
+        const uint32_t mask = (uint32_t)ndig - 1u;
+        for (int p = 0; p < passes; p++) {
+            const uint2* src = p == 0 ? nullptr : ((p & 1) ? scr0 : scr1) + lo;
+            uint2* dst = ((p & 1) ? scr1 : scr0) + lo;
+            const int shift = p * db;
+            // digit totals of the whole run -> each digit's first slot
+            for (int d = t; d < ndig; d += 256) sh.cursor[d] = 0;
+            __syncthreads();
+            for (uint32_t i = t; i < len; i += 256) {
+                const uint32_t k = src ? src[i].x : depth_keys[vals[lo + i] & BIN_ID_MASK];
+                atomicAdd(&sh.cursor[(k >> shift) & mask], 1u);
+            }
+            __syncthreads();
+            if (w == 0) {
+                const int dpl = ndig / 64;
+                uint32_t sum = 0;
+                for (int i = 0; i < dpl; i++) sum += sh.cursor[dpl * lane + i];
+                uint32_t incl = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+                    if (lane >= o) incl += y;
+                }
+                uint32_t run = incl - sum;
+                for (int i = 0; i < dpl; i++) {
+                    const uint32_t x = sh.cursor[dpl * lane + i];
+                    sh.cursor[dpl * lane + i] = run;
+                    run += x;
+                }
+            }
+            __syncthreads();
+            for (uint32_t c0 = 0; c0 < len; c0 += kSxCap) {
+                const uint32_t clen = min((uint32_t)kSxCap, len - c0);
+                const int R = (int)((clen + 255) / 256);
+                const uint32_t wl = (uint32_t)w * 64 * R;
+                uint32_t kr[kSxMaxR], vr[kSxMaxR];
+                if (src) {
+#pragma unroll
+                    for (int r = 0; r < kSxMaxR; r++) {  // clamped, unconditional loads (see above)
+                        const uint2 e = src[c0 + min(wl + (uint32_t)r * 64 + lane, clen - 1)];
+                        kr[r] = e.x;
+                        vr[r] = e.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + c0 + min(wl + (uint32_t)r * 64 + lane, clen - 1)];
+#pragma unroll
+                    for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];
+                }
+                sx_rank_chunk(sh, kr, vr, R, clen, shift, db, true, dst);
+            }
+            __syncthreads();
+        }
+        sorted_g = (((passes - 1) & 1) ? scr1 : scr0) + lo;
+    }
+    // the four tile lists, stable, from the depth-ordered run (LDS, global scratch, or the single /
+    // empty run straight from vals)
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t dst0 = out_base + 4u * lo;
+    uint32_t carry[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t r0 = 0; r0 < len; r0 += 256) {
+        const uint32_t j = r0 + (uint32_t)t;
+        uint32_t v = 0u;
+        if (j < len) v = len <= 1 ? vals[lo + j] : sorted_g ? sorted_g[j].y : sh.v[j];
+        const uint32_t m = j < len ? v >> BIN_SHIFT : 0u;
+        uint32_t rank[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint64_t bal = __ballot((m >> b) & 1u);
+            rank[b] = (uint32_t)__popcll(bal & lt);
+            if (lane == 0) sh.wsum[w][b] = (uint32_t)__popcll(bal);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            uint32_t pre = carry[b], tot = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                pre += i < w ? sh.wsum[i][b] : 0u;
+                tot += sh.wsum[i][b];
+            }
+            if ((m >> b) & 1u) point_list[dst0 + (uint32_t)b * len + pre + rank[b]] = v & BIN_ID_MASK;
+            carry[b] += tot;
+        }
+        __syncthreads();
+    }
+    if (t < 4) {
+        const int tx = 2 * X + (t & 1), ty = 2 * Y + (t >> 1);
+        const uint32_t s = dst0 + (uint32_t)t * len;
+        if (tx < gx && ty < gy) ranges[ty * gx + tx] = make_uint2(s, s + carry[t]);
+    }
+}
+
+template <typename K>
+void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
+                       const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
+                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
+                       uint2* bounds, hipStream_t st) {
+    const int nb = bins_x(gx) * bins_y(gy);
+    if (nb <= 0) return;
+    k_bin_bounds<K><<<std::max<uint32_t>(1u, (L + 255) / 256), 256, 0, st>>>(L, n_dev, keys, nb, bounds);
+    k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
+                                        open_bits, scr0, scr1);
+}
+template void launch_sortexpand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, const uint32_t*,
+                                          const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
+                                          uint2*, uint2*, uint2*, hipStream_t);
+template void launch_sortexpand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                                          const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
+                                          uint2*, uint2*, uint2*, hipStream_t);
+
+}  // namespace rr

@@ -27,6 +27,13 @@
 
 namespace rr {
 
+#ifndef RR_BWD_DEFER
+#define RR_BWD_DEFER 0
+#endif
+#ifndef RR_BWD_BF
+#define RR_BWD_BF 0
+#endif
+
 // OCC: minimum waves per SIMD requested from the register allocator.  The default 3 leaves the
 // compiler its 132 VGPRs without spills; 4 caps it at 128 with 96 B/lane of scratch in the
 // per-round flush (0.2446 / 0.2424 vs 0.2411 / 0.2413 ms/step in an interleaved A/B; a variant
@@ -105,6 +112,95 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             load_splat(a.splats, nid, na, nb, nc);
         }
         const int cnt = min(B, nmax - base);
+#if RR_BWD_DEFER
+        // Software-pipelined by hand: the block after pair j's branched pixel bodies holds pair
+        // j's nine per-lane sums, the LDS record reads and the four exp2 chains of pair j + 1, and
+        // the wave reduction of pair j — independent dependency chains for the scheduler to
+        // interleave, where the reduction's permlane / DPP chain and the next record's LDS latency
+        // otherwise each ran alone.  The reduction is unconditional (skipping an empty pair measured
+        // neutral, and its branch would split the block); the last pair reads its own record again.
+        float4 A = s_a[0], Bv = s_b[0], Cc = s_c[0];
+        float ev[PPL], av[PPL];
+        bool ok[PPL];
+        auto alphas = [&](int jp) {
+            const int contrib_next = nmax - 1 - (base + jp);
+            (void)contrib_next;
+            const float dx = A.x - pfx;
+            const P2X px2 = blend_p2_x(A.z, A.w, Bv.y, dx);
+#pragma unroll
+            for (int q = 0; q < PPL; q++) {
+                const float dy = A.y - (float)(py0 + 4 * q);
+                const float e2 = blend_e2(px2, Bv.x, dy);
+                ev[q] = __builtin_amdgcn_exp2f(e2);  // o G
+                av[q] = fminf(0.99f, ev[q]);
+                // keep every exp chain in this block (LLVM would sink each into its pixel's branch)
+                asm volatile("" : "+v"(ev[q]), "+v"(av[q]));
+                ok[q] = (e2 <= Bv.y) & (av[q] >= 1.0f / 255.0f);
+#if RR_BWD_BF
+                // branch-free bodies: an inactive pixel runs the body with alpha = e = 0, which
+                // leaves T (1 / (1 - 0) = 1 exactly), R and every sum bit for bit unchanged
+                ok[q] = ok[q] & (contrib_next < last[q]);
+                av[q] = ok[q] ? av[q] : 0.f;
+                ev[q] = ok[q] ? ev[q] : 0.f;
+#endif
+            }
+        };
+        alphas(0);
+        for (int j = 0; j < cnt; j++) {
+            const int contributor = nmax - 1 - (base + j);
+            (void)contributor;
+            const float dx = A.x - pfx;
+            float sv = 0.f, svdy = 0.f, svdy2 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
+            auto body = [&](int q) {
+                const float dy = A.y - (float)(py0 + 4 * q);
+                const float e = ev[q], alpha = av[q];
+                const float inv = rcp_nr(1.f - alpha);
+                T[q] = T[q] * inv;
+                const float dchannel_dcolor = alpha * T[q];
+                const float cdp = Cc.x * dp0[q] + Cc.y * dp1[q] + Cc.z * dp2[q];
+                g6 += dchannel_dcolor * dp0[q];
+                g7 += dchannel_dcolor * dp1[q];
+                g8 += dchannel_dcolor * dp2[q];
+                const float d = cdp - R[q];
+                const float dL_dalpha = d * T[q] + tfbg[q] * inv;
+                R[q] = __builtin_fmaf(alpha, d, R[q]);
+                const float v = e * dL_dalpha;
+                const float vdy = v * dy;
+                sv += v;
+                svdy += vdy;
+                svdy2 = __builtin_fmaf(vdy, dy, svdy2);
+            };
+#if RR_BWD_BF == 1
+#pragma unroll
+            for (int q = 0; q < PPL; q++) body(q);
+#elif RR_BWD_BF == 2
+            // one branch per two pixels of the lane (tile rows 0-7 / 8-15)
+#pragma unroll
+            for (int q = 0; q < PPL; q += 2) {
+                if (q + 1 >= PPL) {
+                    if (ok[q]) body(q);
+                } else if (ok[q] | ok[q + 1]) {
+                    body(q);
+                    body(q + 1);
+                }
+            }
+#else
+#pragma unroll
+            for (int q = 0; q < PPL; q++)
+                if ((contributor < last[q]) & ok[q]) body(q);
+#endif
+            const float p0 = sv * dx, p1 = svdy, p2 = p0 * dx, p3 = p1 * dx, p4 = svdy2;
+            const float p5 = sv * Cc.w;  // 1 / opacity
+            const int jn = min(j + 1, cnt - 1);
+            A = s_a[jn];
+            Bv = s_b[jn];
+            Cc = s_c[jn];
+            alphas(jn);
+            float t0, t1, t2;
+            wave_sum9(p0, p1, p2, p3, p4, p5, g6, g7, g8, t0, t1, t2);
+            red9_store(&s_g[w][j * NGRAD], lane, t0, t1, t2);
+        }
+#else
         for (int j = 0; j < cnt; j++) {
             const int contributor = nmax - 1 - (base + j);
             const float4 A = s_a[j];
@@ -181,6 +277,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             if (__ballot(any) != 0ull) wave_sum9(g0, g1, g2, g3, g4, g5, g6, g7, g8, t0, t1, t2);
             red9_store(sg, lane, t0, t1, t2);
         }
+#endif
         __syncthreads();
         // one atomic per (pair, component); consecutive lanes hit consecutive components of a pair
 #pragma unroll

@@ -1,31 +1,28 @@
 // rr_forward.hip — forward kernels of the MI355X rasterizer.
 //
-//   k_preprocess<DEG>  one thread per Gaussian (forward.cu:144-246 semantics)
-//   k_duplicate<K>     (bin, Gaussian) pairs in depth order, key = bin id only, value = Gaussian |
-//                      tile mask << BIN_SHIFT (LDS windows; bins: rr_common.hpp)
-//   k_expand<K>        per bin of the bin-sorted list: its four per-tile lists (stable) and their
-//                      [start, end) (rasterizer_impl.cu:105-127's ranges)
-//   k_blend_fwd        per-tile front-to-back alpha blend (forward.cu:251-369)
+//   k_preprocess<DEG>  one thread per Gaussian (forward.cu:144-246 semantics; rr_preprocess.hpp)
+//   k_duplicate<K>     (bin, Gaussian) pairs of one early-stop phase in Gaussian index order, key =
+//                      bin id only, value = Gaussian | tile mask << BIN_SHIFT (LDS windows; bins:
+//                      rr_common.hpp)
 //   k_mark_visible     frustum test (rasterizer_impl.cu:43-55)
 //
 // Binning order: the reference sorts 64-bit (tile << 32 | depth_bits) keys emitted in Gaussian
-// index order with a stable radix sort.  Here visible Gaussians are first stable-sorted by
-// depth bits (P keys, 32 bits), their pairs are emitted in that order, and the pairs are then
-// stable-sorted by tile id only (msb(T) <= 15 bits, 16-bit keys).  Within a tile this yields the
-// same (depth, index) order as the reference, at a fraction of the sort traffic.
+// index order with a stable radix sort.  Here the pairs are emitted in index order too, stable-
+// sorted by bin id only (rr_sort.hip, <= 16-bit keys), and each bin's run is then stable-sorted by
+// depth inside one workgroup (rr_bin.hip k_sortexpand) and split into its four tiles' lists.
+// Within a tile this yields the reference's (depth, index) order, without a sort of 64-bit keys
+// and without a per-frame depth sort of the Gaussians.
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
+#include "rr_preprocess.hpp"
 
 namespace rr {
 
-// No global atomics here: per-Gaussian counts go to tiles[idx] = {pairs, rect area} and are
-// prefix-summed in depth order (the rect-area sum is the reference's num_rendered).
+// No global atomics here: per-Gaussian counts go to tiles[idx] = {pairs, rect area} (the rect-area
+// sum is the reference's num_rendered).  The arithmetic is rr_preprocess.hpp's preprocess_finish.
 template <int DEG>
 __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx, bool& wide) {
-    a.radii[idx] = 0;
-    a.tiles[idx] = make_uint2(0u, 0u);
-    if (a.depth_keys) a.depth_keys[idx] = 0xffffffffu;  // culled Gaussians sort behind every visible one
-
+    preprocess_clear(a, idx);
     const v3 p = load3(a.means3D + 3 * (size_t)idx);
     // in_frustum (auxiliary.h:128-153)
     const v3 p_view = xform_point_4x3(p, a.view);
@@ -46,104 +43,12 @@ __device__ __forceinline__ uint2 preprocess_one(const PreArgs& a, int idx, bool&
     const float o_in = a.opacities[idx];
     const float* dc = a.raw ? a.shs + 3 * (size_t)idx : a.shs + (size_t)idx * a.M * 3;
     const v3 c0 = load3(a.colors_precomp ? a.colors_precomp + 3 * (size_t)idx : dc);
-
-    const float4 p_hom = xform_point_4x4(p, a.proj);
-    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
-    const float ppx = p_hom.x * p_w, ppy = p_hom.y * p_w;
-
-    float cov[6];
-    if (a.cov3D_precomp) {
-        const float* c = a.cov3D_precomp + 6 * (size_t)idx;
-#pragma unroll
-        for (int i = 0; i < 6; i++) cov[i] = c[i];
-    } else {
-        if (a.raw) {
-            q = act_rot(q);
-            sc = act_scale(sc);
-        }
-        cov3d_from_scale_rot(sc, a.scale_modifier, q, cov);
-    }
-    const Proj2D pr = ewa_setup(p, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view);
-    float ca, cb, cc;
-    ewa_cov2d(pr, cov, ca, cb, cc);
-    ca += a.low_pass;
-    cc += a.low_pass;
-
-    const float det = ca * cc - cb * cb;
-    if (det == 0.0f) return make_uint2(0u, 0u);
-    const float det_inv = 1.f / det;
-    const float cx = cc * det_inv, cy = -cb * det_inv, cz = ca * det_inv;
-    const float mid = 0.5f * (ca + cc);
-    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
-    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
-    const int radius = (int)my_radius;
-    const float px = ndc2pix(ppx, a.W), py = ndc2pix(ppy, a.H);
-    int x0, y0, x1, y1;
-    tile_rect(px, py, radius, a.gx, a.gy, x0, y0, x1, y1);
-    const int area = (x1 - x0) * (y1 - y0);
-    if (area == 0) return make_uint2(0u, 0u);
-
-    float4 rgb;
-    if (a.colors_precomp) {
-        rgb = make_float4(c0.x, c0.y, c0.z, 0.f);
-    } else {
-        const v3 cp = load3(a.campos);
-        v3 dir = p - cp;
-        const float len = sqrtf(dot(dir, dir));
-        dir = mk(dir.x / len, dir.y / len, dir.z / len);
-        const float* rest = a.raw ? a.shs_rest + (size_t)idx * (a.M - 1) * 3 : dc + 3;
-        // the coefficients this degree uses, in 16-B loads (dword-aligned: a record is 180 or 192 B,
-        // one lane's loads touch ~4x fewer cache lines per instruction than 45 dword loads)
-        constexpr int NR = ((DEG + 1) * (DEG + 1) - 1) * 3;
-        float rr[NR > 0 ? NR : 1];
-        load_floats_u<NR>(rest, rr);
-        const v3 c = sh_eval<DEG>(dir, c0, rr);
-        rgb = make_float4(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f), 0.f);
-    }
-    const float opacity = a.raw ? act_opacity(o_in) : o_in;
-    float log2o, inv_o;
-    splat_derived(opacity, log2o, inv_o);
-    Splat s;
-    s.a = make_float4(px, py, kQHalf * cx, kQFull * cy);
-    s.b = make_float4(kQHalf * cz, log2o, p_view.z, opacity);
-    s.c = make_float4(rgb.x, rgb.y, rgb.z, inv_o);
-    if (a.wire) {
-        float2* w = reinterpret_cast<float2*>(a.wire + (size_t)kWireFloats * idx);
-        w[0] = make_float2(s.a.x, s.a.y);
-        w[1] = make_float2(s.a.z, s.a.w);
-        w[2] = make_float2(s.b.x, s.b.z);
-        w[3] = make_float2(s.b.w, s.c.x);
-        w[4] = make_float2(s.c.y, s.c.z);
-    } else {
-        a.splats[idx] = s;
-    }
-    if (a.normals) a.normals[idx] = gaussian_normal(sc, q, a.view, p_view);
-    a.radii[idx] = radius;
-    // (bin, Gaussian) pairs: bins (2 x 2 tiles, rr_common.hpp) holding a tile the Gaussian reaches
-    // (exact culling) or a tile of its bounding rect
-    // culling on the conic as the duplicate reads it back from the record (splat_conic), so both
-    // kernels count the same pairs
-    float ccx, ccy, ccz;
-    splat_conic(s.a, s.b, ccx, ccy, ccz);
-    const CullEll ell = cull_setup(px, py, ccx, ccy, ccz, a.cull ? cull_qmax(opacity) : 0.f);
-    uint32_t n = 0;
-    for (int Y = y0 >> 1; Y < (y1 + 1) >> 1; Y++) {
-        int l0, h0, l1, h1;
-        bin_row_spans(ell, a.cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
-        n += bin_count(l0, h0, l1, h1);
-    }
-    a.tiles[idx] = make_uint2(n, (uint32_t)area);
-    // > 0.2, so the bit pattern orders like the value, and so does its offset from kDepthKeyBase
-    const uint32_t key = __float_as_uint(p_view.z) - kDepthKeyBase;
-    if (a.depth_keys) a.depth_keys[idx] = key;
-    wide = key >= (1u << kDepthKeyBits);
-    return make_uint2(n, (uint32_t)area);
+    const float* rest = a.raw ? a.shs_rest + (size_t)idx * (a.M - 1) * 3 : dc + 3;
+    return preprocess_finish<DEG, true>(a, idx, p, p_view, q, sc, o_in, c0, rest, wide);
 }
 
 // The block's sums of {pairs, rect tiles} go to a.block_sums[blockIdx.x] (plain stores; a single
-// contended 64-bit atomic per block measured +37 us on 1M Gaussians): the frame's pair count is
-// then known right after this kernel (rr_api.hip pair_counts_publish reduces them).
+// contended 64-bit atomic per block measured +37 us on 1M Gaussians).
 template <int DEG>
 __device__ __forceinline__ void preprocess_block(const PreArgs& a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -152,31 +57,10 @@ __device__ __forceinline__ void preprocess_block(const PreArgs& a) {
     if (idx < a.P) {
         c = preprocess_one<DEG>(a, idx, wide);
     } else if (idx < a.n_out) {  // padding row of a row block: culled
-        a.radii[idx] = 0;
-        a.tiles[idx] = make_uint2(0u, 0u);
-        if (a.depth_keys) a.depth_keys[idx] = 0xffffffffu;
+        preprocess_clear(a, idx);
     }
     if (!a.block_sums) return;
-    __shared__ uint2 s_sum[4];
-    __shared__ uint32_t s_wide[4];
-    uint32_t n = c.x, r = c.y;  // per block <= 256 * T, below 2^32 for T < 2^24
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        n += (uint32_t)__shfl_xor((int)n, o);
-        r += (uint32_t)__shfl_xor((int)r, o);
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool wave_wide = __any(wide);
-    if (lane == 0) {
-        s_sum[w] = make_uint2(n, r);
-        s_wide[w] = wave_wide ? 1u : 0u;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a.block_sums[blockIdx.x] = make_uint2(s_sum[0].x + s_sum[1].x + s_sum[2].x + s_sum[3].x,
-                                              s_sum[0].y + s_sum[1].y + s_sum[2].y + s_sum[3].y);
-        a.block_wide[blockIdx.x] = s_wide[0] | s_wide[1] | s_wide[2] | s_wide[3];
-    }
+    preprocess_block_sums(a, blockIdx.x, c, wide);
 }
 
 // 5 waves per SIMD: the SH-3 instance fits 88 VGPRs without spills (the compiler's own choice,
@@ -266,237 +150,39 @@ void launch_unpack_rows(int world, int rows_per_rank, const char* recv, size_t c
         field_offsets[3], field_offsets[4], splats, tiles, depth_keys, radii, block_sums, block_wide);
 }
 
-// ---- scan of the pair counts in depth order (replaces a device-wide decoupled-look-back scan:
-// its state-init launch plus a look-back chain over ~500 blocks measured 18.5 us per frame) ----
-// SatAdd2 (min(a + b, 2^32 - 1) per component) is associative, so the scan equals the exact 64-bit
-// prefix sums clamped to 32 bits: both kernels sum in 64 bits and clamp only on output.
-__device__ __forceinline__ void block_sum2_u64(unsigned long long& x, unsigned long long& y,
-                                               unsigned long long* s) {  // s: [8], 256 threads
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        x += __shfl_xor(x, o);
-        y += __shfl_xor(y, o);
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (lane == 0) {
-        s[w] = x;
-        s[4 + w] = y;
-    }
-    __syncthreads();
-    x = s[0] + s[1] + s[2] + s[3];
-    y = s[4] + s[5] + s[6] + s[7];
-}
-
-// n_dev (may be null): only the first min(P, *n_dev) items are read, the rest count as {0, 0}
-// (the depth sort that dropped the culled Gaussians leaves its output past its count unwritten)
-__device__ __forceinline__ int scan_len(int P, const uint32_t* n_dev) {
-    return n_dev ? (int)min((uint32_t)P, *n_dev) : P;
-}
-
-__global__ __launch_bounds__(256) void k_pair_scan_totals(const uint2* __restrict__ in, int P,
-                                                          ulonglong2* __restrict__ tot, const uint32_t* n_dev) {
-    P = scan_len(P, n_dev);
-    __shared__ unsigned long long s[8];
-    const size_t b0 = (size_t)blockIdx.x * kPairScanItems;
-    unsigned long long x = 0, y = 0;
-#pragma unroll
-    for (int r = 0; r < kPairScanItems / 256; r++) {
-        const size_t i = b0 + (size_t)r * 256 + threadIdx.x;
-        if (i < (size_t)P) {
-            const uint2 v = in[i];
-            x += v.x;
-            y += v.y;
-        }
-    }
-    block_sum2_u64(x, y, s);
-    if (threadIdx.x == 0) tot[blockIdx.x] = make_ulonglong2(x, y);
-}
-
-// Exclusive scan, in place, of the nb block totals (one workgroup, 2048 per round, carried in
-// 64 bits): the large-P path, where re-summing every earlier total in each block would grow with
-// nb^2 (at P = 16.7M that is ~0.5 GB of L2 reads per frame).
-__global__ __launch_bounds__(256) void k_pair_scan_prefix(ulonglong2* __restrict__ tot, int nb) {
-    constexpr int IPT = kPairScanItems / 256;
-    __shared__ unsigned long long s_wx[4], s_wy[4];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    unsigned long long cx = 0, cy = 0;  // sum of all earlier rounds
-    for (int base = 0; base < nb; base += kPairScanItems) {
-        ulonglong2 v[IPT];
-        unsigned long long tx = 0, ty = 0;
-#pragma unroll
-        for (int k = 0; k < IPT; k++) {
-            const int i = base + t * IPT + k;
-            v[k] = i < nb ? tot[i] : make_ulonglong2(0ull, 0ull);
-            tx += v[k].x;
-            ty += v[k].y;
-        }
-        unsigned long long ix = tx, iy = ty;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned long long ux = __shfl_up(ix, o), uy = __shfl_up(iy, o);
-            if (lane >= o) {
-                ix += ux;
-                iy += uy;
-            }
-        }
-        __syncthreads();  // the previous round's reads of s_wx / s_wy are done
-        if (lane == 63) {
-            s_wx[w] = ix;
-            s_wy[w] = iy;
-        }
-        __syncthreads();
-        unsigned long long ex = cx + ix - tx, ey = cy + iy - ty;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (k < w) {
-                ex += s_wx[k];
-                ey += s_wy[k];
-            }
-#pragma unroll
-        for (int k = 0; k < IPT; k++) {
-            const int i = base + t * IPT + k;
-            if (i < nb) tot[i] = make_ulonglong2(ex, ey);
-            ex += v[k].x;
-            ey += v[k].y;
-        }
-        cx += s_wx[0] + s_wx[1] + s_wx[2] + s_wx[3];
-        cy += s_wy[0] + s_wy[1] + s_wy[2] + s_wy[3];
-    }
-}
-
-// PREFIX: tot[b] already holds the exclusive prefix of the block totals (k_pair_scan_prefix);
-// otherwise it holds block b's own total and every block sums those of the blocks before it.
-template <bool PREFIX>
-__global__ __launch_bounds__(256) void k_pair_scan(const uint2* __restrict__ in, uint2* __restrict__ out, int P,
-                                                   const ulonglong2* __restrict__ tot, const uint32_t* n_dev) {
-    constexpr int IPT = kPairScanItems / 256;  // 8 consecutive items per thread
-    const int n = scan_len(P, n_dev);  // items read; all P are written
-    __shared__ unsigned long long s[8];
-    __shared__ unsigned long long s_wx[4], s_wy[4];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const size_t i0 = (size_t)blockIdx.x * kPairScanItems + (size_t)t * IPT;
-    // this thread's items: four 16-B loads (two items each) when the run is in range
-    uint2 v[IPT];
-    if (i0 + IPT <= (size_t)n) {
-        const uint4* p = reinterpret_cast<const uint4*>(in + i0);
-#pragma unroll
-        for (int k = 0; k < IPT / 2; k++) {
-            const uint4 q = p[k];
-            v[2 * k] = make_uint2(q.x, q.y);
-            v[2 * k + 1] = make_uint2(q.z, q.w);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < IPT; k++) v[k] = i0 + k < (size_t)n ? in[i0 + k] : make_uint2(0u, 0u);
-    }
-    // sum of the totals of all earlier blocks
-    unsigned long long bx = 0, by = 0;
-    if (PREFIX) {
-        const ulonglong2 q = tot[blockIdx.x];
-        bx = q.x;
-        by = q.y;
-    } else {
-        for (int j = t; j < (int)blockIdx.x; j += 256) {
-            const ulonglong2 q = tot[j];
-            bx += q.x;
-            by += q.y;
-        }
-        block_sum2_u64(bx, by, s);
-    }
-    // exclusive scan of the thread sums (wave shuffles, then the 4 wave totals)
-    unsigned long long tx = 0, ty = 0;
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        tx += v[k].x;
-        ty += v[k].y;
-    }
-    unsigned long long ix = tx, iy = ty;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long ux = __shfl_up(ix, o), uy = __shfl_up(iy, o);
-        if (lane >= o) {
-            ix += ux;
-            iy += uy;
-        }
-    }
-    if (lane == 63) {
-        s_wx[w] = ix;
-        s_wy[w] = iy;
-    }
-    __syncthreads();
-    unsigned long long ex = bx + ix - tx, ey = by + iy - ty;
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (k < w) {
-            ex += s_wx[k];
-            ey += s_wy[k];
-        }
-    uint2 o[IPT];
-#pragma unroll
-    for (int k = 0; k < IPT; k++) {
-        ex += v[k].x;
-        ey += v[k].y;
-        o[k] = make_uint2(ex > 0xffffffffull ? 0xffffffffu : (uint32_t)ex, ey > 0xffffffffull ? 0xffffffffu : (uint32_t)ey);
-    }
-    if (i0 + IPT <= (size_t)P) {
-        uint4* p = reinterpret_cast<uint4*>(out + i0);
-#pragma unroll
-        for (int k = 0; k < IPT / 2; k++) p[k] = make_uint4(o[2 * k].x, o[2 * k].y, o[2 * k + 1].x, o[2 * k + 1].y);
-    } else {
-#pragma unroll
-        for (int k = 0; k < IPT; k++)
-            if (i0 + k < (size_t)P) out[i0 + k] = o[k];
-    }
-}
-
-size_t pair_scan_temp_bytes(int P) {
-    return (size_t)std::max((P + kPairScanItems - 1) / kPairScanItems, 1) * sizeof(ulonglong2);
-}
 
 namespace {
 int g_pair_scan_direct = kPairScanDirectBlocks;
 }
 void set_pair_scan_direct_blocks(int nb) { g_pair_scan_direct = nb >= 0 ? nb : kPairScanDirectBlocks; }
+int pair_scan_direct_blocks() { return g_pair_scan_direct; }
 
-void launch_pair_scan(const uint2* in, uint2* out, int P, const uint32_t* n_dev, void* temp, hipStream_t st) {
-    if (P <= 0) return;
-    const int nb = (P + kPairScanItems - 1) / kPairScanItems;
-    ulonglong2* tot = static_cast<ulonglong2*>(temp);
-    k_pair_scan_totals<<<nb, 256, 0, st>>>(in, P, tot, n_dev);
-    if (nb <= g_pair_scan_direct) {
-        k_pair_scan<false><<<nb, 256, 0, st>>>(in, out, P, tot, n_dev);
-    } else {
-        k_pair_scan_prefix<<<1, 256, 0, st>>>(tot, nb);
-        k_pair_scan<true><<<nb, 256, 0, st>>>(in, out, P, tot, n_dev);
-    }
-}
-
-// First Gaussian (depth rank) of every window of `win` consecutive pairs starting at pair0:
-// window k = [pair0 + k*win, pair0 + (k+1)*win) starts inside the pair range [a, b) of exactly
-// one Gaussian.
-// A second window set (pair0_b, win_b, nwin_b, first_b; nwin_b = 0: none) is marked in the same pass.
-__global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __restrict__ offsets, uint32_t pair0,
-                                                       uint32_t win, int nwin, uint32_t* __restrict__ first,
-                                                       uint32_t pair0_b, uint32_t win_b, int nwin_b,
-                                                       uint32_t* __restrict__ first_b, uint32_t* __restrict__ zero,
-                                                       int nzero) {
+// First list entry of every window of `win` consecutive pairs starting at pair0: window k =
+// [pair0 + k*win, pair0 + (k+1)*win) starts inside the pair range [a, b) of exactly one entry.
+// A second window set (over a second list: the phase-B windows; nwin_b = 0: none) is marked in the
+// same pass.  List lengths come from the device (n / n_b); the grid covers the capacity.
+__global__ __launch_bounds__(256) void k_window_starts(const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ off,
+                                                       uint32_t pair0, uint32_t win, int nwin,
+                                                       uint32_t* __restrict__ first, const uint32_t* __restrict__ n_dev_b,
+                                                       const uint32_t* __restrict__ off_b, uint32_t pair0_b,
+                                                       uint32_t win_b, int nwin_b, uint32_t* __restrict__ first_b,
+                                                       uint32_t* __restrict__ zero, int nzero) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     for (int i = s; i < nzero; i += gridDim.x * blockDim.x) zero[i] = 0u;
-    if (s >= P) return;
-    const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
-    if (a == b) return;
-    auto mark = [&](uint32_t p0, uint32_t w, int nw, uint32_t* f) {
-        if (nw <= 0 || b <= p0) return;
+    auto mark = [&](const uint32_t* o, uint32_t p0, uint32_t w, int nw, uint32_t* f) {
+        const uint32_t a = s == 0 ? 0u : o[s - 1], b = o[s];
+        if (nw <= 0 || a == b || b <= p0) return;
         const uint32_t k0 = a <= p0 ? 0u : (a - p0 + w - 1) / w;
         for (uint32_t k = k0; k <= (b - 1 - p0) / w && k < (uint32_t)nw; k++) f[k] = (uint32_t)s;
     };
-    mark(pair0, win, nwin, first);
-    mark(pair0_b, win_b, nwin_b, first_b);
+    if (nwin > 0 && (uint32_t)s < *n_dev) mark(off, pair0, win, nwin, first);
+    if (nwin_b > 0 && (uint32_t)s < *n_dev_b) mark(off_b, pair0_b, win_b, nwin_b, first_b);
 }
 
 // duplicateWithKeys (rasterizer_impl.cu:59-100), output-driven: workgroup k produces exactly the
-// pairs [pair0 + k*win, pair0 + (k+1)*win) of the depth-ordered pair list.  Its Gaussians (from
-// first[k] on) emit into an LDS window, which then leaves with coalesced stores — the
+// pairs [pair0 + k*win, pair0 + (k+1)*win) of the phase's index-ordered pair list (offsets .x for
+// phase A, .y for phase B: rr_bin.hip's split scan).  Its Gaussians (from first[k] on) emit into an
+// LDS window, which then leaves with coalesced stores — the
 // per-Gaussian form scatters every pair to its own cache line — and the window's histogram of
 // the lowest `dbits` key bits is written as the tile sort's first-pass digit counts (rr_sort.hip
 // units == windows).  Output of window k goes to [k*win, ...) of keys / vals.
@@ -508,8 +194,8 @@ __global__ __launch_bounds__(256) void k_window_starts(int P, const uint2* __res
 // into *n_total.  (A two-pass variant — count the kept pairs, one block scan per round, then write
 // them compacted — measured slower: 0.104 vs 0.083 ms/step for both duplicate launches.)
 template <typename K, bool FILTER>
-__global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __restrict__ idx_sorted,
-                                                   const uint2* __restrict__ offsets,
+__global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ idx,
+                                                   const uint32_t* __restrict__ offsets,
                                                    const Splat* __restrict__ splats, const int* __restrict__ radii,
                                                    int gx, int gy, int cull, const uint32_t* __restrict__ first,
                                                    uint32_t pair0, uint32_t win, uint32_t L, K* __restrict__ keys,
@@ -577,16 +263,17 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     };
     const int bgx = bins_x(gx);
     const int s0 = (int)first[wb];
+    const int P = (int)*n_dev;  // entries of the phase's list
     for (int base = s0;; base += 256) {
         const int s = base + t;
         if (s < P) {
-            // two dependent load steps per Gaussian: {offsets, id} then {radius, record} (the id is
-            // part of the branch condition and the culling setup precedes the open-tile test, so
-            // the compiler cannot sink these loads behind a wait into the branches that use them)
-            const uint32_t a = s == 0 ? 0u : offsets[s - 1].x, b = offsets[s].x;
-            const uint32_t g = idx_sorted[s];
+            // two dependent load steps per Gaussian: {offsets, index} then {radius, record} (the
+            // index is part of the branch condition and the culling setup precedes the open-tile
+            // test, so the compiler cannot sink these loads behind a wait into the branches)
+            const uint32_t a = s == 0 ? 0u : offsets[s - 1], b = offsets[s];
+            const uint32_t g = idx[s];
             const uint32_t lo = max(a, w0), hi = min(b, w1);
-            if (lo < hi && g != 0xffffffffu) {
+            if (lo < hi) {
                 const int r = radii[g];
                 const float4 A = splats[g].a;
                 const float4 Bv = splats[g].b;
@@ -628,7 +315,7 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
         }
         // another round only if this round's last Gaussian ends before the window does
         const int last = min(base + 255, P - 1);
-        if (last >= P - 1 || offsets[last].x >= w1) break;
+        if (last >= P - 1 || offsets[last] >= w1) break;
     }
     __syncthreads();
     const uint32_t mask = (uint32_t)ndig - 1u;
@@ -679,104 +366,6 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, const uint32_t* __rest
     for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + wb] = hist[d];
 }
 
-// One workgroup per bin.  The bin's run [lo, hi) of the bin-sorted list (two binary searches over
-// the sorted keys) holds its pairs in (depth, index) order with their tile masks; each of the bin's
-// (up to) four tiles gets the stable sub-list of the pairs whose mask has its bit, written at
-// out_base + 4 lo + b (hi - lo) (capacity 4x the bin pairs, so no global scan), and its range
-// (rasterizer_impl.cu:105-127 identifyTileRanges).  Every tile of the grid gets a range, so the
-// ranges need no clearing.  n_dev: device-side count of a filtered (phase B) list.
-template <typename K>
-__global__ __launch_bounds__(256) void k_expand(uint32_t n_host, const uint32_t* __restrict__ n_dev,
-                                                const K* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                int gx, int gy, uint32_t out_base, uint32_t* __restrict__ point_list,
-                                                uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits) {
-    __shared__ uint32_t wsum[4][4];
-    const int bgx = bins_x(gx);
-    const int bin = blockIdx.x;
-    const int X = bin % bgx, Y = bin / bgx;
-    if (open_bits) {  // phase B: a bin whose tiles all closed in phase A holds no pair, and its
-                      // tiles' ranges were cleared with the frame's: nothing to search or write
-        bool any = false;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int tx = 2 * X + (b & 1), ty = 2 * Y + (b >> 1);
-            if (tx < gx && ty < gy) {
-                const uint32_t tile = (uint32_t)(ty * gx + tx);
-                any = any || ((open_bits[tile >> 5] >> (tile & 31)) & 1u);
-            }
-        }
-        if (!any) return;  // block-uniform
-    }
-    const uint32_t n = n_dev ? *n_dev : n_host;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    // 256-ary searches for the bin's first pair and the next bin's: each round probes 256 evenly
-    // spaced keys at once (one load latency per round, 3 rounds for 16M pairs, instead of a 24-deep
-    // chain of dependent loads), and the two searches share their rounds (their loads in flight
-    // together)
-    const uint32_t v0 = (uint32_t)bin, v1 = (uint32_t)bin + 1u;
-    uint32_t l0 = 0, h0 = n, l1 = 0, h1 = n;  // answers in [l, h]
-    while (h0 - l0 > 1 || h1 - l1 > 1) {
-        const bool a0 = h0 - l0 > 1, a1 = h1 - l1 > 1;
-        const uint32_t s0 = (h0 - l0 + 255) / 256, s1 = (h1 - l1 + 255) / 256;
-        const uint32_t i0 = l0 + (uint32_t)t * s0, i1 = l1 + (uint32_t)t * s1;
-        const bool q0 = a0 && i0 < h0, q1 = a1 && i1 < h1;
-        const uint32_t k0 = q0 ? (uint32_t)keys[i0] : 0u, k1 = q1 ? (uint32_t)keys[i1] : 0u;
-        const int c0 = __syncthreads_count(q0 && k0 < v0);  // probes below v
-        const int c1 = __syncthreads_count(q1 && k1 < v1);
-        // probes 0..c-1 are below v: the answer lies in (l + (c-1) step, l + c step]
-        if (a0) {
-            const uint32_t nl = c0 == 0 ? l0 : l0 + (uint32_t)(c0 - 1) * s0 + 1u;
-            h0 = min(h0, l0 + (uint32_t)c0 * s0);
-            l0 = nl;
-        }
-        if (a1) {
-            const uint32_t nl = c1 == 0 ? l1 : l1 + (uint32_t)(c1 - 1) * s1 + 1u;
-            h1 = min(h1, l1 + (uint32_t)c1 * s1);
-            l1 = nl;
-        }
-    }
-    {
-        const uint32_t k0 = l0 < h0 ? (uint32_t)keys[l0] : 0u, k1 = l1 < h1 ? (uint32_t)keys[l1] : 0u;
-        if (l0 < h0) l0 += k0 < v0 ? 1u : 0u;  // block-uniform: every thread read the same key
-        if (l1 < h1) l1 += k1 < v1 ? 1u : 0u;
-    }
-    const uint32_t lo = l0, hi = l1;
-    const uint32_t len = hi - lo;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const uint32_t dst0 = out_base + 4u * lo;
-    uint32_t carry[4] = {0u, 0u, 0u, 0u};
-    for (uint32_t r0 = 0; r0 < len; r0 += 256) {
-        const uint32_t j = r0 + (uint32_t)t;
-        const uint32_t v = j < len ? vals[lo + j] : 0u;
-        const uint32_t m = j < len ? v >> BIN_SHIFT : 0u;
-        uint32_t rank[4];
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const uint64_t bal = __ballot((m >> b) & 1u);
-            rank[b] = (uint32_t)__popcll(bal & lt);
-            if (lane == 0) wsum[w][b] = (uint32_t)__popcll(bal);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            uint32_t pre = carry[b], tot = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                pre += i < w ? wsum[i][b] : 0u;
-                tot += wsum[i][b];
-            }
-            if ((m >> b) & 1u) point_list[dst0 + (uint32_t)b * len + pre + rank[b]] = v & BIN_ID_MASK;
-            carry[b] += tot;
-        }
-        __syncthreads();
-    }
-    if (t < 4) {
-        const int tx = 2 * X + (t & 1), ty = 2 * Y + (t >> 1);
-        const uint32_t s = dst0 + (uint32_t)t * len;
-        if (tx < gx && ty < gy) ranges[ty * gx + tx] = make_uint2(s, s + carry[t]);
-    }
-}
-
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
                                                       const float* __restrict__ view, uint8_t* __restrict__ present) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -822,12 +411,13 @@ bool launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
     }
     const bool second = d.first_b && d.nwin_b > 0 && d.win_b > 0 && d.win_b <= (uint32_t)kSortMaxUnit;
     if (!d.starts_done)
-        k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.P, d.offsets, d.pair0, d.win, d.nwin, d.first, d.pair0_b,
-                                                         second ? d.win_b : 1u, second ? d.nwin_b : 0,
+        k_window_starts<<<blocks_for(d.P), 256, 0, st>>>(d.n_list, d.off, d.pair0, d.win, d.nwin, d.first,
+                                                         second ? d.n_list_b : d.n_list, second ? d.off_b : d.off,
+                                                         d.pair0_b, second ? d.win_b : 1u, second ? d.nwin_b : 0,
                                                          d.first_b, d.zero, d.zero ? d.nzero : 0);
     auto kern = d.open_bits ? k_duplicate<K, true> : k_duplicate<K, false>;
     const bool ord = d.open_bits && d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
-    kern<<<d.nwin + (ord ? 1 : 0), 256, 0, st>>>(d.P, d.idx_sorted, d.offsets, d.splats, d.radii, d.gx, d.gy, d.cull,
+    kern<<<d.nwin + (ord ? 1 : 0), 256, 0, st>>>(d.n_list, d.idx, d.off, d.splats, d.radii, d.gx, d.gy, d.cull,
                                                   d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts,
                                                   d.nwin, d.open_bits, d.unit_len, d.n_total, ord ? d.order_cost : nullptr,
                                                   ord ? d.order_out : nullptr, d.order_flag, d.order_T);
@@ -835,17 +425,6 @@ bool launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
 }
 template bool launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
 template bool launch_duplicate<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
-
-template <typename K>
-void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,
-                   uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, hipStream_t st) {
-    const int nb = bins_x(gx) * bins_y(gy);
-    if (nb > 0) k_expand<K><<<nb, 256, 0, st>>>(L, n_dev, keys, vals, gx, gy, out_base, point_list, ranges, open_bits);
-}
-template void launch_expand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, int, int, uint32_t,
-                                      uint32_t*, uint2*, const uint32_t*, hipStream_t);
-template void launch_expand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, int, int, uint32_t,
-                                      uint32_t*, uint2*, const uint32_t*, hipStream_t);
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;

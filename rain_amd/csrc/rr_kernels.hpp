@@ -5,56 +5,25 @@
 
 namespace rr {
 
-// The frame's pair counts, published to the host: the preprocess's per-block sums of {pairs, rect
-// tiles} are added in 64 bits (fixed order), saturated to 32 bits (the host rejects anything above
-// 2^31 anyway) and stored with the OR of the blocks' wide-depth-key flags into a coherent pinned
-// mailbox (system-scope release of the sequence number; rr_api.hip pair_counts_wait spins on it)
-// and into a device copy for the no-mailbox path.  One workgroup of 256 threads.
-struct PublishJob {
-    const uint2* src;
-    const uint32_t* src_wide;
-    int nb;
-    uint32_t* box;  // null: no mailbox
-    uint32_t seq;
-    unsigned long long* copy;  // [3]
+// Per-frame scalars of the depth-sort-free binning (rr_bin.hip), in the geometry buffer: written by
+// k_early_cut (L, rect, wide, cut) and by the split scan's last thread (LA, LB), which also copies
+// them to the host mailbox.  Also the device copy the no-mailbox read-back path reads.
+struct FrameTotals {
+    unsigned long long L;     // (bin, Gaussian) pairs of the frame
+    unsigned long long rect;  // bounding-rect tiles (the reference's num_rendered)
+    uint32_t cut;             // early-stop split: phase A = Gaussians with depth key < cut
+    uint32_t wide;            // a visible depth key needs more than kDepthKeyBits bits
+    uint32_t LA, LB;          // pairs of phase A / phase B (saturated to 32 bits)
+    uint32_t GA, GB;          // Gaussians of phase A / phase B (lengths of the PhaseLists)
 };
-__device__ inline void publish_pair_counts_block(const PublishJob& j) {
-    __shared__ unsigned long long s_n[4], s_r[4];
-    unsigned long long n = 0, r = 0;
-    uint32_t wide = 0;
-    for (int i = threadIdx.x; i < j.nb; i += 256) {
-        const uint2 v = j.src[i];
-        n += v.x;
-        r += v.y;
-        wide |= j.src_wide[i];
-    }
-    wide = __syncthreads_or(wide != 0) ? 1u : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        n += __shfl_xor(n, o);
-        r += __shfl_xor(r, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        s_n[threadIdx.x >> 6] = n;
-        s_r[threadIdx.x >> 6] = r;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        n = s_n[0] + s_n[1] + s_n[2] + s_n[3];
-        r = s_r[0] + s_r[1] + s_r[2] + s_r[3];
-        const uint32_t x = n > 0xffffffffull ? 0xffffffffu : (uint32_t)n;
-        const uint32_t y = r > 0xffffffffull ? 0xffffffffu : (uint32_t)r;
-        j.copy[0] = x;
-        j.copy[1] = y;
-        j.copy[2] = wide;
-        if (j.box) {
-            __hip_atomic_store(j.box + 0, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(j.box + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(j.box + 3, wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(j.box + 2, j.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
+// The two phases' Gaussian lists in index order (rr_bin.hip launch_split_scan): entry r of a phase
+// is its r-th Gaussian's index and the inclusive sum of the phase's pairs up to it.
+struct PhaseLists {
+    uint32_t* idx_a;
+    uint32_t* off_a;
+    uint32_t* idx_b;
+    uint32_t* off_b;
+};
 
 struct PreArgs {
     int P, D, M, W, H, gx, gy, prefiltered;
@@ -184,6 +153,10 @@ struct GaussBwdArgs {
     // rr_adam lives in host memory); use_adam says whether it is valid
     rr_adam adam;
     int use_adam;
+    // with use_adam: the next frame's preprocess on the stepped parameters (rr_next_frame): its
+    // camera, frame values and output arrays (geometry buffer, radii); has_next says whether valid
+    PreArgs next;
+    int has_next;
 };
 
 void launch_preprocess(const PreArgs& a, hipStream_t st);
@@ -204,22 +177,34 @@ struct PreViews {
     int V;
 };
 void launch_preprocess_views(const PreArgs& a, const PreViews& vs, hipStream_t st);
-// Inclusive scan of the per-Gaussian {pairs, rect tiles} in depth order, saturating at 2^32 - 1
-// per component (rasterizer_impl.cu:269).  Per-block totals, then each block scans its items on
-// top of the sum of the earlier totals: up to kPairScanDirectBlocks blocks (P <= 1,048,576) every
-// block sums those totals itself (2 launches), above it one workgroup scans them first (3
-// launches; rr_set_tuning "pair_scan_direct_blocks" moves the cut-over, tests force both paths).
-// temp: pair_scan_temp_bytes(P).
+// The pair-count scan (rasterizer_impl.cu:269; rr_bin.hip launch_split_scan) in blocks of
+// kPairScanItems: per-block totals, then each block scans its items on top of the sum of the earlier
+// totals: up to kPairScanDirectBlocks blocks (P <= 1,048,576) every block sums those totals itself
+// (2 launches), above it one workgroup scans them first (3 launches; rr_set_tuning
+// "pair_scan_direct_blocks" moves the cut-over, tests force both paths).
 constexpr int kPairScanItems = 2048;                 // items per block (256 threads x 8)
 constexpr int kPairScanDirectBlocks = 512;
-size_t pair_scan_temp_bytes(int P);
-void launch_pair_scan(const uint2* in, uint2* out, int P, const uint32_t* n_dev, void* temp, hipStream_t st);
 void set_pair_scan_direct_blocks(int nb);
+int pair_scan_direct_blocks();
+// rr_bin.hip: the depth-sort-free binning
+void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
+                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, hipStream_t st);
+// The phases' Gaussian lists (PhaseLists, ft->GA / GB entries); the last thread publishes {LA, rect,
+// seq, wide, LB} to box (may be null) and ft.  temp: split_scan_temp_bytes(P)
+size_t split_scan_temp_bytes(int P);
+void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
+                       uint32_t* box, uint32_t seq, int direct_blocks, hipStream_t st);
+template <typename K>
+void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
+                       const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
+                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
+                       uint2* bounds, hipStream_t st);  // bounds: [bins] scratch for the bins' runs
 template <typename K>
 struct DupArgs {
-    int P;
-    const uint32_t* idx_sorted;
-    const uint2* offsets;
+    int P;                       // capacity of the lists (the frame's Gaussians)
+    const uint32_t* n_list;      // device: entries of the phase's list (FrameTotals GA / GB)
+    const uint32_t* idx;         // the phase's Gaussians in index order (PhaseLists)
+    const uint32_t* off;         // their inclusive pair offsets
     const Splat* splats;
     const int* radii;
     int gx, gy, cull;
@@ -248,12 +233,14 @@ struct DupArgs {
     // readback)
     uint32_t* zero;
     int nzero;
-    // optional second window set (the phase-B windows, computed in the phase-A launch of the
-    // window-starts kernel: one launch less on the path); starts_done: this pass's windows were
-    // computed that way, skip the kernel
+    // optional second window set (the phase-B windows over the phase-B list, computed in the
+    // phase-A launch of the window-starts kernel: one launch less on the path); starts_done: this
+    // pass's windows were computed that way, skip the kernel
     uint32_t* first_b;
     uint32_t pair0_b, win_b;
     int nwin_b;
+    const uint32_t* n_list_b;
+    const uint32_t* off_b;
     bool starts_done;
 };
 // returns whether the window starts (both sets) were computed
@@ -289,17 +276,7 @@ template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
-                            const uint32_t* n_dev = nullptr, const uint2* gather_src = nullptr,
-                            uint2* gather_dst = nullptr, const struct PublishJob* publish = nullptr,
-                            uint32_t* kept = nullptr);
-// publish (optional, needs !first_counts_ready): one extra workgroup of the first count launch
-// runs the pair-count publish (rr_api.hip pair_counts_publish) beside the counting instead of a
-// launch of its own between the preprocess and the sort.
-// gather_src / gather_dst (optional): the last pass also writes gather_dst[i] = gather_src[vals_out[i]]
-// (the depth sort hands the scan its {pairs, rect} in depth order, a contiguous array).
-// kept (optional, a device word; not with unit_len / n_dev): the first pass drops every item whose
-// key is all ones (the preprocess's culled Gaussians) and writes the number it kept to *kept; the
-// later passes sort only those, and the output past *kept is left unwritten.
+                            const uint32_t* n_dev = nullptr);
 const char* radix_sort_last_error();
 void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
 void set_sort_min_units_tile(int units);  // the same for the bin sorts (<= 16-bit keys; default 1024)

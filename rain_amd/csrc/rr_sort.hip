@@ -1,8 +1,9 @@
 // rr_sort.hip — stable LSD radix sort of (key, u32 value) pairs, written for CDNA4.
 //
-// Used for the per-frame depth sort (P keys, 32 bits) and the tile sort (L pairs, <= 16 bits);
+// Used for the bin sorts of the binning (L pairs, <= 16-bit bin keys, or 32 beyond 65536 bins);
 // replaces rocPRIM's device radix sort (Onesweep look-back latency bound here; merge path below
-// 2^20 items).
+// 2^20 items).  (Rounds 1-3 also ran a per-frame depth sort of the P Gaussians on it; the bins'
+// depth order now comes from k_sortexpand, rr_bin.hip.)
 //
 // Each pass sorts by one digit of <= 8 bits with a count / scan / scatter split over "units" of
 // one workgroup (4 wave64s) x R rounds x 64 items (R chosen per call so that small inputs still
@@ -65,13 +66,7 @@ __device__ __forceinline__ uint32_t unit_length(const uint32_t* unit_len, const 
 template <typename K, int MAXR, int DB>
 __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ keys, size_t n, int shift, int dbits,
                                                           int rounds, uint32_t* __restrict__ counts, int units,
-                                                          const uint32_t* __restrict__ n_dev, PublishJob pub,
-                                                          int has_pub, int drop_ones) {
-    static_assert(64 * kWaves == 256, "publish_pair_counts_block runs on 256 threads");
-    if (has_pub && (int)blockIdx.x == units) {  // the extra workgroup (block-uniform)
-        publish_pair_counts_block(pub);
-        return;
-    }
+                                                          const uint32_t* __restrict__ n_dev) {
     __shared__ uint32_t hist[1 << DB];
     const int t = threadIdx.x;
     const int ndig = 1 << dbits;
@@ -85,9 +80,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_rs_count(const K* __restrict__ 
 #pragma unroll
     for (int r = 0; r < MAXR; r++) {  // all loads in flight before the first LDS atomic
         const uint32_t li = (uint32_t)r * 64 * kWaves + t;
-        const K k = (r < rounds && li < len) ? keys[base + li] : (K)~(K)0;
-        dr[r] = (r < rounds && li < len && !(drop_ones && k == (K)~(K)0)) ? (((uint32_t)k >> shift) & mask)
-                                                                             : 0xffffffffu;
+        dr[r] = (r < rounds && li < len) ? (((uint32_t)keys[base + li] >> shift) & mask) : 0xffffffffu;
     }
     __syncthreads();
 #pragma unroll
@@ -174,10 +167,7 @@ __global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ ke
                                                             const uint32_t* __restrict__ offsets, int units,
                                                             const uint32_t* __restrict__ totals,
                                                             const uint32_t* __restrict__ unit_len,
-                                                            const uint32_t* __restrict__ n_dev,
-                                                            const uint2* __restrict__ gather_src,
-                                                            uint2* __restrict__ gather_dst, int drop_ones,
-                                                            uint32_t* __restrict__ kept) {
+                                                            const uint32_t* __restrict__ n_dev) {
     constexpr int ND = 1 << DB;  // digits the kernel is compiled for (>= 1 << dbits)
     constexpr int DPL = ND / 64;  // digits per lane in the digit scans
     __shared__ uint32_t dbase[ND];         // first output slot of each digit
@@ -186,7 +176,7 @@ __global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ ke
     __shared__ uint32_t goff[ND];          // global slot of block-local position 0 of each digit's run
     __shared__ uint32_t s_val[64 * SW * MAXR];
     __shared__ K s_key[64 * SW * MAXR];
-    __shared__ uint32_t s_nu;  // items staged (len minus the dropped ones)
+    __shared__ uint32_t s_nu;  // items staged
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int ndig = 1 << dbits;
     const uint32_t mask = (uint32_t)ndig - 1u;
@@ -220,7 +210,6 @@ __global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ ke
             dbase[DPL * lane + i] = run;
             run += tv[i];
         }
-        if (kept && unit == 0 && lane == 63) kept[0] = run;  // every digit's total: the items kept
     }
     // the wave's items go to registers once (all loads in flight together); counting, ranking
     // and staging then run from registers
@@ -233,10 +222,7 @@ __global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ ke
         kr[r] = valid ? keys_in[i] : (K)~(K)0;
         vr[r] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
     }
-    // an item takes part when it is in range and (drop_ones) its key is not all ones
-    auto live = [&](int r) {
-        return r < rounds && wl + (uint32_t)r * 64 + lane < len && !(drop_ones && kr[r] == (K)~(K)0);
-    };
+    auto live = [&](int r) { return r < rounds && wl + (uint32_t)r * 64 + lane < len; };
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < MAXR; r++) {
@@ -313,9 +299,7 @@ __global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ ke
         const uint32_t d = ((uint32_t)k >> shift) & mask;
         const uint32_t pos = goff[d] + (uint32_t)j;
         if (keys_out) keys_out[pos] = k;
-        const uint32_t v = s_val[j];
-        vals_out[pos] = v;
-        if (gather_dst) gather_dst[pos] = gather_src[v];
+        vals_out[pos] = s_val[j];
     }
 }
 
@@ -407,16 +391,12 @@ const char* radix_sort_last_error() { return g_why; }
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
-                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev,
-                            const uint2* gather_src, uint2* gather_dst, const PublishJob* publish, uint32_t* kept) {
+                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
     g_why = "";
     if (n > 0xffffffffull || bits <= 0 || bits > (int)(8 * sizeof(K))) return g_why = "bad size/bits", hipErrorInvalidValue;
     if (unit_len && !n_dev) return g_why = "sparse units without n_dev", hipErrorInvalidValue;
-    if (publish && first_counts_ready) return g_why = "publish rides on the first count launch", hipErrorInvalidValue;
-    if (kept && (unit_len || n_dev || first_counts_ready))
-        return g_why = "dropping all-ones keys needs a dense first pass", hipErrorInvalidValue;
     const SortLayout s = sort_layout<K>(temp, n, bits);
     if (temp_bytes < s.total) return g_why = "temp too small", hipErrorInvalidValue;
     const int passes = sort_passes(bits);
@@ -444,11 +424,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                                       : rounds <= 4 ? k_rs_count<K, 4, 8>
                                       : rounds <= 8 ? k_rs_count<K, 8, 8>
                                                     : k_rs_count<K, kMaxRounds, 8>);
-            const bool pub = p == 0 && publish;
-            const uint32_t* nd = p > 0 && kept ? kept : n_dev;
-            count<<<units + (pub ? 1 : 0), 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, nd,
-                                                                 pub ? *publish : PublishJob{}, pub ? 1 : 0,
-                                                                 p == 0 && kept ? 1 : 0);
+            count<<<units, 64 * kWaves, 0, st>>>(ksrc, n, shift, dbits, rounds, s.counts, units, n_dev);
         }
         k_rs_scan_rows<<<1 << dbits, 256, 0, st>>>(s.counts, s.offsets, units, s.totals);
         // the scatter ranks a unit with kScatterWaves waves (the same unit_items: rounds_s rounds
@@ -469,9 +445,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                                     : rs <= 8 ? k_rs_scatter<K, 8, 8, 4>
                                               : k_rs_scatter<K, kMaxRounds, 8, 4>));
         scatter<<<units, 64 * sw, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rs, s.offsets, units,
-                                               s.totals, p == 0 ? unit_len : nullptr, p > 0 && kept ? kept : n_dev,
-                                               last ? gather_src : nullptr, last ? gather_dst : nullptr,
-                                               p == 0 && kept ? 1 : 0, p == 0 ? kept : nullptr);
+                                               s.totals, p == 0 ? unit_len : nullptr, n_dev);
         ksrc = kdst;
         vsrc = vdst;
         shift += dbits;
@@ -485,10 +459,10 @@ template size_t radix_sort_temp_bytes<uint16_t>(size_t, int);
 template size_t radix_sort_temp_bytes<uint32_t>(size_t, int);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, const uint2*, uint2*, const PublishJob*, uint32_t*);
+                                               const uint32_t*);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, const uint2*, uint2*, const PublishJob*, uint32_t*);
+                                               const uint32_t*);
 template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int);
 template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int);
 

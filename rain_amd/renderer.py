@@ -3,17 +3,49 @@
 Identical contract: builds GaussianRasterizationSettings from the camera, creates the
 ``means2D`` gradient sink (its .grad receives the NDC-space screen gradient), picks the SH /
 precomputed-colour and scale-rotation / precomputed-covariance inputs from the pipeline flags,
-and returns {render, viewspace_points, visibility_filter, radii, depth}.
+and returns {render, viewspace_points, visibility_filter, radii, depth}.  When the model's getters
+are GaussianModel's own and the pipeline flags are the defaults, the rasterizer takes the raw
+parameters and applies the getters in-kernel (rain_amd.fused.RasterizeRawParams): the same
+outputs and leaf gradients without the getters' elementwise autograd chain and the get_features
+concatenation (RAIN_RENDER_RAW=0 disables it).
 """
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
 
 from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
 from .sh_utils import eval_sh
+
+
+# render()'s raw-parameter fast path (rain_amd.fused.RasterizeRawParams): RAIN_RENDER_RAW=0 keeps every
+# call on the getters + GaussianRasterizer route.
+RAW_RENDER = os.environ.get("RAIN_RENDER_RAW", "1") != "0"
+
+
+def _raw_path_ok(pc, pipe, override_color) -> bool:
+    """The getters of `pc` are GaussianModel's own (exp / normalize / sigmoid / concatenation,
+    gaussian_model.py:85-105) on contiguous fp32 device tensors, and the pipeline asks for the
+    default SH and scale/rotation inputs: the rasterizer may then take the raw parameters and
+    apply the getters in-kernel (identical arithmetic, one autograd node)."""
+    from .gaussian_model import GaussianModel
+
+    if not RAW_RENDER or override_color is not None or pipe.convert_SHs_python or pipe.compute_cov3D_python \
+            or pipe.debug or not isinstance(pc, GaussianModel):
+        return False
+    cls = type(pc)
+    if any(getattr(cls, n) is not getattr(GaussianModel, n)
+           for n in ("get_xyz", "get_features", "get_scaling", "get_rotation", "get_opacity")):
+        return False
+    if pc.scaling_activation is not torch.exp or pc.opacity_activation is not torch.sigmoid \
+            or pc.rotation_activation is not torch.nn.functional.normalize:
+        return False
+    ts = (pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation)
+    return all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in ts) \
+        and pc._features_rest.shape[1] + 1 <= 16
 
 
 @dataclass
@@ -41,6 +73,16 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=
         viewmatrix=viewpoint_camera.world_view_transform, projmatrix=viewpoint_camera.full_proj_transform,
         sh_degree=pc.active_sh_degree, campos=viewpoint_camera.camera_center, prefiltered=False, debug=pipe.debug,
         low_pass=low_pass)
+    if _raw_path_ok(pc, pipe, override_color):
+        from .fused import RasterizeRawParams
+
+        rendered_image, radii, depth = RasterizeRawParams.apply(
+            pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation, screenspace_points,
+            pc.active_sh_degree, raster_settings.image_width, raster_settings.image_height, tanfovx, tanfovy,
+            raster_settings.viewmatrix, raster_settings.projmatrix, raster_settings.campos, bg_color, low_pass,
+            scaling_modifier)
+        return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
+                "radii": radii, "depth": depth}
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
 
     means3D = xyz

@@ -212,6 +212,13 @@ class Trainer:
         self.fused = auto if fused is None else bool(fused)
         self._bin_cache = None
         self.reuse_binning = True  # fused step: one native forward call over a reused binning buffer
+        # fused step, single GPU: the backward of step s also preprocesses step s+1's frame on the
+        # parameters it has just stepped (rain_amd.fused.prepare_next / include/rain_raster.h
+        # rr_next_frame); step s+1 then renders from that geometry.  Step s+1's view, learning rate,
+        # SH degree and low-pass are decided at step s (after s's optimizer block is built), in the
+        # order the unfused step would decide them.
+        self.fuse_next = True
+        self._pending = None  # (iteration, view index, camera, low_pass, NextFrame or None)
         self._shard = None
         # the fused step on N > 1 ranks (or a forced exchange): Gaussian-sharded, view-parallel
         # (rain_amd/sharded.py); the autograd step keeps the replicated gradient exchange
@@ -250,6 +257,15 @@ class Trainer:
         else:
             self.low_pass = 0.3
         return vidx, cam
+
+    def _sh_steps_up(self, iteration) -> bool:
+        """Whether _low_pass_and_view(iteration) raises the active SH degree (train.py:79-85)."""
+        g, cfg = self.g, self.cfg
+        if g.active_sh_degree >= g.max_sh_degree:
+            return False
+        if cfg.ours or cfg.ours_new:
+            return iteration >= 5000 and iteration % 1000 == 0
+        return iteration % 1000 == 0
 
     def _events(self, iteration):
         """(densify/prune now, opacity reset now) — train.py:136-143."""
@@ -346,7 +362,14 @@ class Trainer:
         if self._bin_cache is None:
             self._bin_cache = fused.BinningCache()
         g, opt = self.g, self.opt
-        vidx, cam = self._low_pass_and_view(iteration)
+        pend, self._pending = self._pending, None
+        if pend is not None and pend[0] == iteration:  # decided (and maybe preprocessed) by step s-1
+            _it, vidx, cam, self.low_pass, nxt = pend
+            if nxt is not None and (nxt.P != g.get_xyz.shape[0] or nxt.frame.D != g.active_sh_degree):
+                nxt = None  # the model changed since (cannot happen inside step(); defensive)
+        else:
+            vidx, cam = self._low_pass_and_view(iteration)
+            nxt = None
         densify_phase = iteration < opt.densify_until_iter
         densify_now, reset_now = self._events(iteration)
         # Single GPU, and no densify/prune or opacity reset this iteration (they replace parameter
@@ -370,12 +393,25 @@ class Trainer:
         # them (_finish)
         stats = (g.xyz_gradient_accum, g.denom, g.max_radii2D) if densify_phase else None
         gt = self.gt[vidx]
+        # the next step's frame, preprocessed by this step's backward: only when this step's Adam runs
+        # inside that backward (no densify / reset replacing parameters) and the SH degree stays
+        next_frame = None
+        if (fuse_adam and self.fuse_next and not self.sharded and iteration + 1 < opt.iterations
+                and not self._sh_steps_up(iteration + 1)):
+            low_pass_now = self.low_pass
+            vidx1, cam1 = self._low_pass_and_view(iteration + 1)
+            next_frame = fused.prepare_next(g, cam1, self.background, self.low_pass)
+            self._pending = (iteration + 1, vidx1, cam1, self.low_pass, next_frame)
+            self.low_pass = low_pass_now
         with torch.no_grad():
-            image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass,
-                                                     cache=self._bin_cache if self.reuse_binning else None)
+            cache = self._bin_cache if self.reuse_binning else None
+            if nxt is not None:
+                image, radii, _depth, st = fused.forward_next(nxt, g, cache=cache)
+            else:
+                image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass, cache=cache)
             # loss and dL/dimage in one call (bitwise the separate forward / backward)
             loss, _parts, dimg = l1_ssim_forward_backward(image, gt, opt.lambda_dssim)
-            fused.backward(st, dimg, grads, stats, adam=adam)
+            fused.backward(st, dimg, grads, stats, adam=adam, next_frame=next_frame)
             densified = self._finish(iteration, flat, densify_now, reset_now, adam_done=fuse_adam)
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
                         view=vidx, low_pass=self.low_pass, densified=densified)

@@ -9,6 +9,7 @@ import torch
 from rain_amd import cameras, fused, synthetic
 from rain_amd.gaussian_model import GaussianModel, OptimizationParams
 from rain_amd.loss import fused_l1_ssim_loss, l1_ssim_backward, l1_ssim_forward
+from rain_amd import renderer as renderer_mod
 from rain_amd.renderer import PipelineParams, render
 from rain_amd.train import TrainConfig, Trainer
 
@@ -38,8 +39,14 @@ def _params(g):
     return dict(zip(NAMES, (g._xyz, g._features_dc, g._features_rest, g._opacity, g._scaling, g._rotation)))
 
 
+@pytest.fixture
+def getters_route(monkeypatch):
+    """render() through the getters and GaussianRasterizer (its raw-parameter fast path off)."""
+    monkeypatch.setattr(renderer_mod, "RAW_RENDER", False)
+
+
 @pytest.mark.parametrize("sh_degree,active,low_pass", [(3, 3, 0.3), (3, 1, 0.3), (0, 0, 0.3), (3, 3, 300.0)])
-def test_raw_mode_matches_reference_api(gpu, sh_degree, active, low_pass):
+def test_raw_mode_matches_reference_api(gpu, getters_route, sh_degree, active, low_pass):
     P, W, H = 30_000, 200, 150
     g = _model(P, sh_degree, active)
     cam = cameras.fibonacci_cameras(8, W, H)[3].to("cuda")
@@ -48,6 +55,7 @@ def test_raw_mode_matches_reference_api(gpu, sh_degree, active, low_pass):
 
     # reference-API path: getters -> render() -> loss -> autograd (train.py:109-116)
     pkg = render(cam, g, PipelineParams(), bg, low_pass=low_pass)
+    assert pkg["viewspace_points"].grad_fn is not None
     loss, _ = fused_l1_ssim_loss(pkg["render"], gt, 0.2)
     loss.backward()
     ref = {k: v.grad.clone() for k, v in _params(g).items()}
@@ -89,6 +97,45 @@ def test_raw_mode_matches_reference_api(gpu, sh_degree, active, low_pass):
     assert torch.equal(mr, mr_ref)
 
 
+@pytest.mark.parametrize("sh_degree,active,low_pass", [(3, 3, 0.3), (3, 2, 30.0), (0, 0, 0.3)])
+def test_render_raw_fast_path_matches_getters_route(gpu, monkeypatch, sh_degree, active, low_pass):
+    """render()'s raw-parameter fast path (rain_amd.fused.RasterizeRawParams) against the same call
+    through the getters and GaussianRasterizer: image, radii, depth, the six leaf gradients and
+    viewspace_points.grad (the densification statistics' input, train.py:133) — the train.py loop
+    sees the same values either way."""
+    P, W, H = 30_000, 200, 150
+    cam = cameras.fibonacci_cameras(8, W, H)[5].to("cuda")
+    bg = torch.tensor([0.3, 0.1, 0.2], device="cuda")
+    gt = torch.rand(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(9))
+    outs = []
+    for raw in (False, True):
+        monkeypatch.setattr(renderer_mod, "RAW_RENDER", raw)
+        g = _model(P, sh_degree, active, seed=4)
+        pkg = render(cam, g, PipelineParams(), bg, low_pass=low_pass)
+        assert (pkg["render"].grad_fn.__class__.__name__.startswith("RasterizeRawParams")) == raw
+        loss, _ = fused_l1_ssim_loss(pkg["render"], gt, 0.2)
+        loss.backward()
+        outs.append((pkg, {k: v.grad.clone() for k, v in _params(g).items()}))
+    (pa, ga), (pb, gb) = outs
+    assert torch.equal(pa["radii"], pb["radii"])
+    assert torch.equal(pa["visibility_filter"], pb["visibility_filter"])
+    assert rel_l1(pb["render"], pa["render"]) < 1e-6
+    assert rel_l1(pb["depth"], pa["depth"]) < 1e-6
+    for k in NAMES:
+        if ga[k].numel() == 0:
+            continue
+        assert torch.isfinite(gb[k]).all(), k
+        if ga[k].abs().sum() == 0:
+            assert gb[k].abs().max() < 1e-8, k
+        else:  # bars and the SH-0 exception as in test_raw_mode_matches_reference_api
+            tol = 2e-4 if (sh_degree == 0 and k in ("xyz", "scaling", "rotation")) else 1e-4
+            assert rel_l1(gb[k], ga[k]) < tol, (k, rel_l1(gb[k], ga[k]))
+    va, vb = pa["viewspace_points"].grad, pb["viewspace_points"].grad
+    assert vb.shape == va.shape == (P, 3)
+    assert float(vb[:, 2].abs().max()) == 0.0
+    assert rel_l1(vb, va) < 1e-4
+
+
 @pytest.mark.parametrize("impl", ["foreach", "fused"])
 def test_fused_adam_matches_torch_adam(gpu, impl):
     """FusedAdam == torch.optim.Adam: the default (foreach) implementation the reference's
@@ -128,8 +175,11 @@ def test_fused_adam_matches_torch_adam(gpu, impl):
         assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=rtol, atol=atol_v)
 
 
-def test_fused_trainer_matches_autograd_trainer(gpu):
-    """Same seeds, same views: parameters after a window with a densify/prune event agree."""
+@pytest.mark.parametrize("raw_render", [True, False])
+def test_fused_trainer_matches_autograd_trainer(gpu, monkeypatch, raw_render):
+    """Same seeds, same views: parameters after a window with a densify/prune event agree (the
+    autograd trainer through render()'s raw fast path, and through the getters route)."""
+    monkeypatch.setattr(renderer_mod, "RAW_RENDER", raw_render)
     P, W, H, V = 20_000, 160, 120, 6
     cams = [c.to("cuda") for c in cameras.fibonacci_cameras(V, W, H)]
     gts = [torch.rand(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(10 + i))
@@ -194,6 +244,88 @@ def test_adam_fused_into_backward_matches_separate_step(gpu):
             scale = max(float(y.abs().max()), 1e-30)
             assert float((x - y).abs().max()) <= 1e-4 * scale, (m, float((x - y).abs().max()), scale)
             assert rel_l1(x, y) < 1e-4, (m, rel_l1(x, y))
+
+
+def _geometry_arrays(geom, radii, P):
+    """(splat records, pair counts, depth keys, block sums, wide flags, radii) of a geometry buffer,
+    as bytes (rr_geometry_layout's offsets)."""
+    import ctypes
+
+    from rain_amd import _native as N
+
+    offs = (ctypes.c_size_t * 5)()
+    N.check(N.raster().rr_geometry_layout(P, offs), "layout")
+    nb = (P + 255) // 256
+    sizes = (48 * P, 8 * P, 4 * P, 8 * nb, 4 * nb)
+    out = [geom[offs[k]:offs[k] + sizes[k]].clone() for k in range(5)]
+    return out + [radii.clone()]
+
+
+@pytest.mark.parametrize("sh_degree,active,low_pass,wh", [(3, 3, 0.3, (160, 120)), (3, 2, 30.0, (200, 150)),
+                                                          (1, 1, 0.3, (96, 64))])
+def test_next_frame_preprocess_in_backward_equals_preprocess(gpu, sh_degree, active, low_pass, wh):
+    """rr_next_frame: the next frame's preprocess run by the backward on the parameters it has just
+    stepped writes, bit for bit, the geometry (splat records, pair counts, depth keys, block sums)
+    and radii that the forward preprocess computes from the stored stepped parameters."""
+    P = 20_000
+    W, H = wh
+    cams = [c.to("cuda") for c in cameras.fibonacci_cameras(8, W, H)]
+    bg = torch.zeros(3, device="cuda")
+    gt = torch.rand(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(9))
+    g = _model(P, sh_degree, active, seed=6)
+    g.training_setup(OptimizationParams())
+    for it in range(3):
+        color, radii, depth, st = fused.forward(g, cams[it], bg, low_pass)
+        _, _, ws = l1_ssim_forward(color, gt, 0.2)
+        dimg = l1_ssim_backward(color, gt, 0.2, ws)
+        nxt = fused.prepare_next(g, cams[it + 3], bg, low_pass)
+        fused.backward(st, dimg, None, None, adam=g.optimizer.fused_step(g), next_frame=nxt)
+        got = _geometry_arrays(nxt.geom, nxt.radii, P)
+        # the forward preprocess of the same camera over the parameters the backward stored
+        _c, ref_radii, _d, ref_st = fused.forward(g, cams[it + 3], bg, low_pass)
+        ref = _geometry_arrays(ref_st.geom, ref_radii, P)
+        names = ("splats", "tiles", "depth_keys", "block_sums", "block_wide", "radii")
+        vis = ref[5] > 0
+        assert vis.any()
+        for n, x, y in zip(names, got, ref):
+            if n == "splats":  # a culled row's record is never written (nor read): visible rows only
+                x, y = x.view(P, 48)[vis].view(torch.float32), y.view(P, 48)[vis].view(torch.float32)
+                bad = (x != y)
+                diag = [(k, int(bad[:, k].sum()), float((x[:, k] - y[:, k]).abs().max())) for k in range(12)]
+                assert not bad.any(), (it, n, diag)
+            assert torch.equal(x, y), (it, n)
+        # and the frame rendered from the precomputed geometry equals the plain forward
+        c2, r2, d2, _st2 = fused.forward_next(nxt, g)
+        assert torch.equal(c2, _c) and torch.equal(d2, _d) and torch.equal(r2, ref_radii)
+
+
+def test_trainer_next_frame_fusion_matches_unfused(gpu):
+    """Trainer.fuse_next (step s's backward preprocesses step s+1's frame) against the same run with
+    it off, through a densify / prune event, an opacity reset and an SH-degree step-up."""
+    P, W, H, V = 20_000, 160, 120, 6
+    cams = [c.to("cuda") for c in cameras.fibonacci_cameras(V, W, H)]
+    gts = [torch.rand(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(20 + i))
+           for i in range(V)]
+    res = []
+    for fuse_next in (False, True):
+        g = _model(P, 3, 1, seed=2)
+        opt = OptimizationParams(densify_from_iter=2, densification_interval=5, opacity_reset_interval=8)
+        g.training_setup(opt)
+        t = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=True, seed=3), scene_extent=4.4, fused=True)
+        t.fuse_next = fuse_next
+        its = list(range(995, 1010))  # the SH degree steps up at 1000
+        losses = [t.step(it, sync_loss=True).loss for it in its]
+        res.append((g, losses))
+    (ga, la), (gb, lb) = res
+    assert ga.active_sh_degree == gb.active_sh_degree == 2
+    assert ga.get_xyz.shape == gb.get_xyz.shape
+    for x, y in zip(la, lb):
+        assert abs(x - y) <= 1e-5 * abs(y)
+    for k, x in _params(ga).items():
+        y = _params(gb)[k]
+        assert rel_l1(x.detach(), y.detach()) < 1e-5, (k, rel_l1(x.detach(), y.detach()))
+    assert torch.equal(ga.denom, gb.denom)
+    assert torch.equal(ga.max_radii2D, gb.max_radii2D)
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])

@@ -82,7 +82,10 @@ def main():
         it += 1
     torch.cuda.synchronize()
     ms = 1000.0 * (time.perf_counter() - t0) / a.steps
-    out = {"tag": a.tag, "ms_per_step": round(ms, 4),
+    # a coarse sanity value of the trained state (float atomics make it differ in the last bits
+    # between runs, so compare it approximately across variants)
+    chk = float(sum(float(t.detach().double().abs().sum()) for t in g.params()))
+    out = {"tag": a.tag, "ms_per_step": round(ms, 4), "state_abs_sum": chk,
            "stages_ms": {k: round(v[0] / 20, 4) for k, v in br.items() if v[1]}}
     if a.api:
         tr2 = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(seed=1), scene_extent=4.4, fused=False)
