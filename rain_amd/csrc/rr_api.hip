@@ -65,11 +65,6 @@ uint32_t higher_msb(uint32_t n) {
 inline int grid_x(int W) { return (W + TILE_X - 1) / TILE_X; }
 inline int grid_y(int H) { return (H + TILE_Y - 1) / TILE_Y; }
 
-// ---- temp-storage queries ----
-template <typename K>
-size_t tile_sort_temp(int L, int bits) {
-    return L > 0 ? radix_sort_temp_bytes<K>((size_t)L, bits) : 0;
-}
 
 // ---- scratch layouts ----
 struct Geom {
@@ -116,6 +111,8 @@ struct Img {
     uint32_t* tile_max;
     uint8_t* open;      // [T] tile still open after phase A
     uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask (in the zeroed block; the phase-A blend sets it)
+    uint2* bounds_a;      // [bins] phase A's (or the single phase's) bin runs (zeroed block; k_bin_bounds)
+    uint2* bounds_b;      // [bins] phase B's
     uint32_t* order;      // [T] backward blend dispatch order (heaviest tiles first)
     size_t total;
 };
@@ -126,13 +123,18 @@ Img carve_img(void* buf, int W, int H) {
     const size_t T = (size_t)std::max(grid_x(W) * grid_y(H), 1);
     m.final_T = c.take<float>(N);
     m.n_contrib = c.take<uint32_t>(N);
-    // one block: ranges [T], ranges_b [T], counters [4], open_bits [ceil(T/32)]
+    // one block, cleared before every render: ranges [T], ranges_b [T], counters [4],
+    // open_bits [ceil(T/32)], bounds_a [bins], bounds_b [bins]
     const size_t nbits = ((size_t)T + 31) / 32;
-    m.ranges = c.take<uint2>(2 * (size_t)T + 2 + (nbits + 1) / 2);
+    const size_t NB = (size_t)std::max(bins_x(grid_x(W)) * bins_y(grid_y(H)), 1);
+    const size_t nz = 2 * (size_t)T + 2 + (nbits + 1) / 2 + 2 * NB;
+    m.ranges = c.take<uint2>(nz);
     m.ranges_b = m.ranges ? m.ranges + T : nullptr;
     m.counters = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T) : nullptr;
     m.open_bits = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T + 2) : nullptr;
-    m.zero_bytes = (2 * (size_t)T + 2 + (nbits + 1) / 2) * sizeof(uint2);
+    m.bounds_a = m.ranges ? m.ranges + 2 * T + 2 + (nbits + 1) / 2 : nullptr;
+    m.bounds_b = m.ranges ? m.bounds_a + NB : nullptr;
+    m.zero_bytes = nz * sizeof(uint2);
     m.tile_max = c.take<uint32_t>(T);
     m.open = c.take<uint8_t>(T);
     m.order = c.take<uint32_t>(T);
@@ -152,10 +154,11 @@ uint32_t g_early_den = kEarlyDen, g_early_min = kEarlyMin;
 
 struct Bin {
     // FIRST, so the backward finds it without knowing the pair count: the per-tile lists
-    // k_sortexpand writes, 4 slots per (bin, Gaussian) pair (phase A's at [0, 4 LA), phase B's
-    // from 4 LA)
+    // k_sortexpand writes, 4 slots per (bin, Gaussian) pair.  The host knows only the frame's
+    // total L (the phases' split LA + LB = L stays on the device), so every pair array has a phase-A
+    // region [0, L) and a phase-B region [L, 2L) (point_list: [0, 4L) and [4L, 8L)).
     uint32_t* point_list;
-    void* keys;            // bin ids of the (bin, Gaussian) pairs (phase A at [0, LA), B from LA)
+    void* keys;            // bin ids of the (bin, Gaussian) pairs
     void* keys_sorted;
     uint32_t* vals;        // Gaussian | tile mask << BIN_SHIFT, then sorted
     uint32_t* vals_sorted;
@@ -163,7 +166,6 @@ struct Bin {
     uint32_t* unit_len;    // phase B: pairs kept per window
     uint2* scr0;           // k_sortexpand's scratch runs for bins of more than kSxCap pairs
     uint2* scr1;
-    uint2* bounds;         // [bins] each bin's run of the bin-sorted pairs (k_bin_bounds)
     void* temp;            // bin-sort scratch, shared by the two phases
     size_t temp_bytes;
     bool wide;  // 32-bit bin keys (more than 65536 bins)
@@ -171,12 +173,22 @@ struct Bin {
     uint32_t L;  // (bin, Gaussian) pairs of both phases
     size_t total;
 };
-template <typename K>
-RadixPlan tile_plan(void* temp, uint32_t n, int bits) {
-    return radix_sort_plan<K>(temp, (size_t)n, 0, bits);
+// Window (= sort unit) length of each phase's sort, chosen for the pairs it is expected to hold
+// (k_early_cut aims phase A at ~1/den of the pairs) while its windows cover the capacity L.
+struct PhaseHints {
+    size_t a, b;
+};
+PhaseHints phase_hints(uint32_t L, bool early) {
+    const size_t n = std::max<size_t>(L, 1);
+    const size_t a = std::max<size_t>(n / std::max<uint32_t>(g_early_den, 1u), 1);
+    return early ? PhaseHints{a, std::max<size_t>(n - a, 1)} : PhaseHints{n, n};
 }
-// The layout depends on the frame's pair count L only (not on its split into LA + LB): the window
-// tables hold both phases' windows, and the sort scratch is sized for L items.
+template <typename K>
+RadixPlan tile_plan(void* temp, uint32_t n, int bits, size_t hint) {
+    return radix_sort_plan<K>(temp, (size_t)n, 0, bits, hint);
+}
+// The layout depends on the frame's pair count L only, sized for the early-stop split (its
+// phase-A hint has the most windows; a single-phase frame uses fewer).
 Bin carve_bin(void* buf, int L, int W, int H) {
     Carver c(buf);
     Bin b;
@@ -185,24 +197,32 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     b.bits = std::max(1, (int)higher_msb((uint32_t)NB));  // >= 1: the duplicate windows are sort units
     b.L = (uint32_t)std::max(L, 0);
     const size_t n = (size_t)std::max(L, 1);
-    b.point_list = c.take<uint32_t>(4 * n + kPointListPad);
+    b.point_list = c.take<uint32_t>(8 * n + kPointListPad);
     if (b.wide) {
-        b.keys = c.take<uint32_t>(n);
-        b.keys_sorted = c.take<uint32_t>(n);
+        b.keys = c.take<uint32_t>(2 * n);
+        b.keys_sorted = c.take<uint32_t>(2 * n);
     } else {
-        b.keys = c.take<uint16_t>(n);
-        b.keys_sorted = c.take<uint16_t>(n);
+        b.keys = c.take<uint16_t>(2 * n);
+        b.keys_sorted = c.take<uint16_t>(2 * n);
     }
-    b.vals = c.take<uint32_t>(n);
-    b.vals_sorted = c.take<uint32_t>(n);
-    // units of either phase <= those of a sort of L items (rounds only grow with the item count)
-    const int u = b.wide ? tile_plan<uint32_t>(nullptr, b.L, b.bits).units : tile_plan<uint16_t>(nullptr, b.L, b.bits).units;
-    b.first = c.take<uint32_t>((size_t)2 * std::max(u, 1) + 2);
-    b.unit_len = c.take<uint32_t>((size_t)std::max(u, 1) + 1);
-    b.scr0 = c.take<uint2>(n);
-    b.scr1 = c.take<uint2>(n);
-    b.bounds = c.take<uint2>((size_t)std::max(NB, 1));
-    b.temp_bytes = b.wide ? tile_sort_temp<uint32_t>(b.L, b.bits) : tile_sort_temp<uint16_t>(b.L, b.bits);
+    b.vals = c.take<uint32_t>(2 * n);
+    b.vals_sorted = c.take<uint32_t>(2 * n);
+    const PhaseHints h = phase_hints(b.L, true);
+    auto units = [&](size_t hint) {
+        return b.wide ? tile_plan<uint32_t>(nullptr, b.L, b.bits, hint).units
+                      : tile_plan<uint16_t>(nullptr, b.L, b.bits, hint).units;
+    };
+    const int ua = std::max(units(h.a), 1), ub = std::max(units(h.b), 1);
+    b.first = c.take<uint32_t>((size_t)ua + ub + 2);
+    b.unit_len = c.take<uint32_t>((size_t)ub + 1);
+    b.scr0 = c.take<uint2>(2 * n);
+    b.scr1 = c.take<uint2>(2 * n);
+    auto temp = [&](size_t hint) {
+        return b.L == 0 ? (size_t)0
+               : b.wide ? radix_sort_temp_bytes<uint32_t>(b.L, b.bits, hint)
+                        : radix_sort_temp_bytes<uint16_t>(b.L, b.bits, hint);
+    };
+    b.temp_bytes = std::max(temp(h.a), temp(h.b));
     b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
     b.total = align_up(c.off);
     return b;
@@ -279,13 +299,14 @@ int check(const rr_frame* f, hipStream_t st, const char* what) {
 // ---------------------------------------------------------------------------------------
 // Readback of the forward's pair counts.  A hipMemcpyAsync into pageable host memory + stream
 // synchronise after the scan costs a blit kernel and the runtime's blocking wait (measured 30-140
-// us of idle GPU per frame before the binning launches).  Instead the last thread of the split scan
-// (rr_bin.hip publish_counts) stores the counts and a sequence number into a coherent pinned host
+// us of idle GPU per frame before the binning launches).  Instead the depth-cut kernel (rr_bin.hip
+// k_early_cut, the first launch after the preprocess; the split scan runs on while the host reads)
+// stores the counts and a sequence number into a coherent pinned host
 // mailbox (system-scope release store) and the host thread spins on the sequence number.  Once the
 // wait has outlasted any frame the stream is queried: a launch / kernel error is reported, and a
 // stream that went idle without the sequence number becoming visible falls back to the plain copy.
 struct Mailbox {
-    uint32_t* host = nullptr;  // [LA, rect, seq, wide, LB], coherent pinned
+    uint32_t* host = nullptr;  // [L, rect, seq, wide], coherent pinned
     uint32_t* dev = nullptr;   // device alias of host
     uint32_t seq = 0;
     bool failed = false;       // allocation failed: always use the copy
@@ -297,7 +318,7 @@ struct PairCountRead {
     uint32_t seq = 0;  // 0: no mailbox (copy + synchronise at wait time)
 };
 struct PairCounts {
-    uint32_t LA = 0, LB = 0, rect = 0;
+    uint32_t L = 0, rect = 0;  // saturated to 32 bits
     bool wide = false;
 };
 
@@ -327,8 +348,7 @@ hipError_t pair_counts_copy(const FrameTotals* src, PairCounts* out, hipStream_t
     FrameTotals v{};
     hipError_t e = hipMemcpyAsync(&v, src, sizeof(v), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    out->LA = v.LA;
-    out->LB = v.LB;
+    out->L = v.L > 0xffffffffull ? 0xffffffffu : (uint32_t)v.L;
     out->rect = v.rect > 0xffffffffull ? 0xffffffffu : (uint32_t)v.rect;
     out->wide = v.wide != 0;
     return e;
@@ -352,10 +372,9 @@ hipError_t pair_counts_wait(const PairCountRead& r, PairCounts* out, hipStream_t
     if (r.seq == 0) return pair_counts_copy(r.copy, out, st);
     for (uint32_t spin = 1;; spin++) {
         if (__atomic_load_n(mb.host + 2, __ATOMIC_ACQUIRE) == r.seq) {
-            out->LA = __atomic_load_n(mb.host + 0, __ATOMIC_RELAXED);
+            out->L = __atomic_load_n(mb.host + 0, __ATOMIC_RELAXED);
             out->rect = __atomic_load_n(mb.host + 1, __ATOMIC_RELAXED);
             out->wide = __atomic_load_n(mb.host + 3, __ATOMIC_RELAXED) != 0;
-            out->LB = __atomic_load_n(mb.host + 4, __ATOMIC_RELAXED);
             return hipSuccess;
         }
         // the stream is queried only once the wait has outlasted any frame (RR_WAIT_QUERY_MS): a query
@@ -372,27 +391,6 @@ hipError_t pair_counts_wait(const PairCountRead& r, PairCounts* out, hipStream_t
         }
         __builtin_ia32_pause();
     }
-}
-
-// Phase-A pair counts of recent frames by geometry buffer: rr_forward_geometry (and the sharded
-// step's rr_forward_from_geometry) read them with the frame's one device->host read, and the render
-// call that follows with the same buffer needs the split (the C ABI passes only the total).  A
-// buffer not found here (e.g. geometry rendered by another thread) costs one synchronous read.
-struct SplitMemo {
-    const void* geom = nullptr;
-    uint32_t LA = 0, LB = 0;
-};
-thread_local SplitMemo g_split[4];
-thread_local int g_split_next = 0;
-void remember_split(const void* geom, uint32_t LA, uint32_t LB) {
-    for (SplitMemo& m : g_split)
-        if (m.geom == geom) {
-            m.LA = LA;
-            m.LB = LB;
-            return;
-        }
-    g_split[g_split_next] = SplitMemo{geom, LA, LB};
-    g_split_next = (g_split_next + 1) & 3;
 }
 
 int validate(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, bool forward) {
@@ -451,39 +449,19 @@ int count_pairs(const rr_frame* f, const Geom& gm, int P, hipStream_t st, int* n
     {
         StageTimer tm(RR_STAGE_SCAN, st);
         launch_early_cut(P, gm.depth_keys, gm.tiles, gm.block_sums, gm.block_wide, full ? 1u : g_early_den,
-                         g_early_min, gm.ft, st);
-        launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, box, rd.seq, pair_scan_direct_blocks(),
-                          st);
+                         g_early_min, gm.ft, gm.temp, box, rd.seq, st);
+        launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(), st);
         RR_CHECK(hipGetLastError(), "pair-count scan");
     }
     RR_STAGE_CHECK("scan");
-    // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin per phase,
-    // and the reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged
+    // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
+    // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged; the
+    // split into the early-stop phases stays on the device
     PairCounts c;
     RR_CHECK(pair_counts_wait(rd, &c, st), "read L");
-    if ((uint64_t)c.LA + c.LB > 0x1fffffffull || c.rect > 0x7fffffffu)
-        return fail(RR_ERR_CAPACITY, "more than 2^29 bin/Gaussian pairs");
-    remember_split(gm.splats, c.LA, c.LB);
+    if (c.L > 0x1fffffffu || c.rect > 0x7fffffffu) return fail(RR_ERR_CAPACITY, "more than 2^29 bin/Gaussian pairs");
     *num_rendered = (int)c.rect;
-    *num_pairs = (int)(c.LA + c.LB);
-    return RR_OK;
-}
-
-// The split of a frame counted by count_pairs into the geometry buffer at `geom` (a synchronous read
-// of its totals if it is not among the recent ones).
-int frame_split(const void* geom_splats, const FrameTotals* ft, uint32_t L, hipStream_t st, uint32_t* LA,
-                uint32_t* LB) {
-    for (const SplitMemo& m : g_split)
-        if (m.geom == geom_splats && m.LA + m.LB == L) {
-            *LA = m.LA;
-            *LB = m.LB;
-            return RR_OK;
-        }
-    PairCounts c;
-    RR_CHECK(pair_counts_copy(ft, &c, st), "read split");
-    if (c.LA + c.LB != L) return fail(RR_ERR_ARG, "num_pairs does not match the geometry buffer's frame");
-    *LA = c.LA;
-    *LB = c.LB;
+    *num_pairs = (int)c.L;
     return RR_OK;
 }
 
@@ -535,51 +513,51 @@ namespace {
 
 // Tile lists for one frame: duplicate -> bin sort -> per-bin depth order + tile lists -> blend,
 // once (single phase) or as the two phases of early-stop binning (rr_kernels.hpp BlendPhase).
-// Phase A's pairs are numbered by the split scan's .x offsets [0, LA), phase B's by .y [0, LB) and
-// staged from position LA of the pair arrays.
+// The host knows the frame's total L only: phase A's pairs (split-scan offsets .x, [0, LA)) go to
+// region [0, L) of the pair arrays and phase B's (.y, [0, LB)) to region [L, 2L); every launch is
+// sized for L and reads its phase's count from FrameTotals (empty windows and units past it).
 template <typename K>
 int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn, const int* radii, int P, int W,
-                 int H, int cull, uint32_t LA, uint32_t LB, BlendFwdArgs b, hipStream_t st) {
+                 int H, int cull, bool early, BlendFwdArgs b, hipStream_t st) {
     const int gx = grid_x(W), gy = grid_y(H);
-    const bool early = LB > 0;
+    const uint32_t L = bn.L;
     K* keys = static_cast<K*>(bn.keys);
     K* keys_sorted = static_cast<K*>(bn.keys_sorted);
     DupArgs<K> d{};
     d.P = P; d.splats = gm.splats; d.radii = radii;
     d.gx = gx; d.gy = gy; d.cull = cull;
+    const PhaseHints h = phase_hints(L, early);
     // phase A (or the only phase): its pairs for every tile
-    const RadixPlan pa = tile_plan<K>(bn.temp, LA, bn.bits);
-    const RadixPlan pb = tile_plan<K>(bn.temp, LB, bn.bits);  // phase B (early-stop binning)
+    const RadixPlan pa = tile_plan<K>(bn.temp, L, bn.bits, h.a);
+    const RadixPlan pb = tile_plan<K>(bn.temp, L, bn.bits, h.b);  // phase B (early-stop binning)
     bool starts_b = false;  // phase B's window starts computed with phase A's
-    if (LA > 0) {
-        {
-            StageTimer tm(RR_STAGE_DUPLICATE, st);
-            d.n_list = &gm.ft->GA; d.idx = gm.lists.idx_a; d.off = gm.lists.off_a;
-            d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L = LA;
-            d.zero = reinterpret_cast<uint32_t*>(im.ranges); d.nzero = (int)(im.zero_bytes / sizeof(uint32_t));
-            d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
-            if (early) {
-                d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
-                d.n_list_b = &gm.ft->GB; d.off_b = gm.lists.off_b;
-            }
-            starts_b = launch_duplicate<K>(d, st);
-            d.first_b = nullptr; d.nwin_b = 0;
+    {
+        StageTimer tm(RR_STAGE_DUPLICATE, st);
+        d.n_list = &gm.ft->GA; d.idx = gm.lists.idx_a; d.off = gm.lists.off_a;
+        d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L_dev = &gm.ft->LA;
+        d.zero = reinterpret_cast<uint32_t*>(im.ranges); d.nzero = (int)(im.zero_bytes / sizeof(uint32_t));
+        d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
+        if (early) {
+            d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
+            d.n_list_b = &gm.ft->GB; d.off_b = gm.lists.off_b;
         }
-        RR_STAGE_CHECK("duplicate");
-        {
-            StageTimer tm(RR_STAGE_TILE_SORT, st);
-            RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.vals_sorted, LA, 0,
-                                         bn.bits, st, true),
-                     std::string("bin sort (") + radix_sort_last_error() + ")");
-        }
-        RR_STAGE_CHECK("bin sort");
-        {
-            StageTimer tm(RR_STAGE_RANGES, st);
-            launch_sortexpand<K>(LA, nullptr, keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u,
-                                 bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, bn.bounds, st);
-        }
-        RR_STAGE_CHECK("sort-expand");
+        starts_b = launch_duplicate<K>(d, st);
+        d.first_b = nullptr; d.nwin_b = 0;
     }
+    RR_STAGE_CHECK("duplicate");
+    {
+        StageTimer tm(RR_STAGE_TILE_SORT, st);
+        RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.vals_sorted, L, 0, bn.bits,
+                                     st, true, nullptr, &gm.ft->LA, h.a),
+                 std::string("bin sort (") + radix_sort_last_error() + ")");
+    }
+    RR_STAGE_CHECK("bin sort");
+    {
+        StageTimer tm(RR_STAGE_RANGES, st);
+        launch_sortexpand<K>(L, &gm.ft->LA, keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u,
+                             bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, im.bounds_a, st);
+    }
+    RR_STAGE_CHECK("sort-expand");
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = early ? kBlendPhaseA : kBlendSingle;
@@ -589,35 +567,35 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     }
     RR_STAGE_CHECK("blend forward");
     if (!early) return RR_OK;
-    // phase B: its pairs, only for tiles phase A left open; positions LA.. of the pair arrays
+    // phase B: its pairs, only for tiles phase A left open; region [L, 2L) of the pair arrays
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
         d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b; d.off = gm.lists.off_b;
         d.first = bn.first + pa.units; d.pair0 = 0; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units;
-        d.L = LB;
-        d.keys = keys + LA; d.vals = bn.vals + LA; d.dbits = pb.dbits0; d.counts = pb.counts;
+        d.L_dev = &gm.ft->LB;
+        d.keys = keys + L; d.vals = bn.vals + L; d.dbits = pb.dbits0; d.counts = pb.counts;
         d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
         // the backward's tile order on phase A's tile_max (counters[1] = T marks it done; the forward
         // blends' own order, when enabled, shares im.order and keeps the prologue's sort instead)
-        if (bwd_tile_order() && !fwd_tile_order()) {
+        if (bwd_tile_order() && !fwd_tile_order() && dup_tile_order()) {
             d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
         }
         d.zero = nullptr; d.nzero = 0;
-        d.starts_done = starts_b;  // false when phase A had no pairs (render_frame cleared the ranges)
+        d.starts_done = starts_b;
         launch_duplicate<K>(d, st);
     }
     RR_STAGE_CHECK("duplicate (phase B)");
     {
         StageTimer tm(RR_STAGE_TILE_SORT, st);
-        RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys + LA, keys_sorted + LA, bn.vals + LA,
-                                     bn.vals_sorted + LA, LB, 0, bn.bits, st, true, bn.unit_len, im.counters),
+        RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys + L, keys_sorted + L, bn.vals + L,
+                                     bn.vals_sorted + L, L, 0, bn.bits, st, true, bn.unit_len, im.counters, h.b),
                  std::string("bin sort, phase B (") + radix_sort_last_error() + ")");
     }
     RR_STAGE_CHECK("bin sort (phase B)");
     {
         StageTimer tm(RR_STAGE_RANGES, st);
-        launch_sortexpand<K>(LB, im.counters, keys_sorted + LA, bn.vals_sorted + LA, gm.depth_keys, gm.ft, gx, gy,
-                             4u * LA, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + LA, bn.scr1 + LA, bn.bounds,
+        launch_sortexpand<K>(L, im.counters, keys_sorted + L, bn.vals_sorted + L, gm.depth_keys, gm.ft, gx, gy,
+                             4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + L, bn.scr1 + L, im.bounds_b,
                              st);
     }
     RR_STAGE_CHECK("sort-expand (phase B)");
@@ -710,10 +688,7 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
     if (L > 0 && binning_bytes < bn.total) return fail(RR_ERR_CAPACITY, "binning buffer too small");
     hipStream_t st = (hipStream_t)stream;
     const int gx = grid_x(W), gy = grid_y(H);
-    uint32_t LA = 0, LB = 0;
-    if (L > 0)
-        if (int rc = frame_split(gm.splats, gm.ft, (uint32_t)L, st, &LA, &LB)) return rc;
-    if (L == 0 || LA == 0) {  // otherwise the first duplicate launch clears them (DupArgs::zero)
+    if (L == 0) {  // otherwise the first duplicate launch clears them (DupArgs::zero)
         StageTimer tm(RR_STAGE_RANGES, st);
         RR_CHECK(hipMemsetAsync(im.ranges, 0, im.zero_bytes, st), "memset ranges");
     }
@@ -724,8 +699,17 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
     b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
     b.out_color = out_color; b.out_depth = out_depth;
     b.normals = out_normal ? gm.normals : nullptr; b.out_normal = out_normal;
-    return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, LA, LB, b, st)
-                   : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, LA, LB, b, st);
+    if (L == 0) {  // no pairs: every tile keeps the background (one blend over empty lists)
+        StageTimer tm(RR_STAGE_BLEND_FWD, st);
+        b.phase = kBlendSingle;
+        launch_blend_fwd(b, st);
+        return check(f, st, "blend forward");
+    }
+    // the split k_early_cut makes (its one-phase conditions but "no sampled pair", which leaves
+    // phase B empty on the device)
+    const bool early = !(f->flags & RR_FLAG_FULL_BINNING) && g_early_den > 1 && (uint32_t)L >= g_early_min;
+    return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
+                   : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
 }
 
 }  // namespace

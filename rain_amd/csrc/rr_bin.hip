@@ -15,9 +15,11 @@
 // tile's phase-A list is then a prefix of its full depth-ordered list and the B list the rest, which
 // is all the two-phase blend needs (any cut gives the full lists' outputs).
 //
+//   k_cut_sample       evenly spaced {depth key, pairs} samples into a dense array
 //   k_early_cut        one workgroup: frame totals from the preprocess block sums, the depth cut
+//   k_early_cut        ... and publishes the frame's total pairs to the host (rr_api.hip mailbox)
 //   k_split_scan_*     inclusive scan of {A pairs, B pairs} per Gaussian in index order; its last
-//                      thread publishes the frame's counts to the host (rr_api.hip mailbox)
+//                      thread leaves the phases' counts in FrameTotals (device-side only)
 //   k_sortexpand<K>    per bin: depth sort of its run + the split into its four tiles' lists
 #include <algorithm>
 
@@ -33,21 +35,43 @@ namespace rr {
 // den <= 1, a frame below min_pairs pairs or no sampled pair: cut = all ones (one phase).
 constexpr int kCutBuckets = 4096;
 constexpr int kCutShift = kDepthKeyBits - 12;
-constexpr int kCutSamplesPerThread = 16;  // <= 16384 samples (one workgroup of 1024 threads)
+// evenly spaced Gaussians: every one up to 8192, ~1 in 123 at 1M (the cut only steers the split's
+// balance; any cut gives the same lists).  Per-bucket sums fit 32 bits: <= 8192 samples of at most
+// 2^18 bins each.
+constexpr int kCutSamples = 8192;
+constexpr int kCutSamplesPerThread = kCutSamples / 1024;
 
-__global__ __launch_bounds__(1024) void k_early_cut(int P, int stride, const uint32_t* __restrict__ keys,
-                                                    const uint2* __restrict__ tiles,
+// The samples {depth key, pairs} gathered by many workgroups into a dense array (one workgroup
+// gathering 16384 scattered cache lines itself took 70 us: a single CU's outstanding-miss limit).
+__global__ __launch_bounds__(256) void k_cut_sample(int ns, int stride, const uint32_t* __restrict__ keys,
+                                                    const uint2* __restrict__ tiles, uint2* __restrict__ samples) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= ns) return;
+    const size_t idx = (size_t)i * stride;
+    samples[i] = make_uint2(keys[idx], tiles[idx].x);
+}
+
+__global__ __launch_bounds__(1024) void k_early_cut(int ns, const uint2* __restrict__ samples,
                                                     const uint2* __restrict__ block_sums,
                                                     const uint32_t* __restrict__ block_wide, int nb, uint32_t den,
-                                                    uint32_t min_pairs, FrameTotals* __restrict__ ft) {
-    __shared__ unsigned long long hist[kCutBuckets];
+                                                    uint32_t min_pairs, FrameTotals* __restrict__ ft, uint32_t* box,
+                                                    uint32_t seq) {
+    __shared__ uint32_t hist[kCutBuckets];
     __shared__ unsigned long long s_red[3][16];
     __shared__ uint32_t s_wide, s_cut;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    for (int i = t; i < kCutBuckets; i += 1024) hist[i] = 0ull;
+    for (int i = t; i < kCutBuckets; i += 1024) hist[i] = 0u;
     if (t == 0) {
         s_wide = 0u;
         s_cut = 0xffffffffu;
+    }
+    // the dense sample array: coalesced, every load in flight before the first LDS atomic
+    uint2 sm[kCutSamplesPerThread];
+#pragma unroll
+    for (int r = 0; r < kCutSamplesPerThread; r++) {
+        const int i = t + r * 1024;
+        sm[r] = samples[min(i, ns - 1)];
+        if (i >= ns) sm[r].y = 0u;
     }
     unsigned long long L = 0, rect = 0, S = 0;
     uint32_t wide = 0;
@@ -58,22 +82,12 @@ __global__ __launch_bounds__(1024) void k_early_cut(int P, int stride, const uin
         wide |= block_wide[i];
     }
     __syncthreads();
-    // <= kCutSamplesPerThread samples per thread, all loads in flight before the first LDS atomic
-    const int ns = (P + stride - 1) / stride;
-    uint32_t sn[kCutSamplesPerThread], sk[kCutSamplesPerThread];
-#pragma unroll
-    for (int r = 0; r < kCutSamplesPerThread; r++) {  // unconditional loads (clamped index): no branch
-        const int i = t + r * 1024;                      // and wait per sample
-        const size_t idx = (size_t)min(i, ns - 1) * stride;
-        const uint32_t n = tiles[idx].x, k = keys[idx];
-        sn[r] = i < ns ? n : 0u;
-        sk[r] = k;
-    }
 #pragma unroll
     for (int r = 0; r < kCutSamplesPerThread; r++)
-        if (sn[r]) {
-            atomicAdd(&hist[min(sk[r] >> kCutShift, (uint32_t)kCutBuckets - 1u)], (unsigned long long)sn[r]);
-            S += sn[r];
+        if (sm[r].y) {
+            const uint32_t n = min(sm[r].y, 1u << 18);
+            atomicAdd(&hist[min(sm[r].x >> kCutShift, (uint32_t)kCutBuckets - 1u)], n);
+            S += n;
         }
     if (wide) atomicOr(&s_wide, 1u);
 #pragma unroll
@@ -133,15 +147,29 @@ __global__ __launch_bounds__(1024) void k_early_cut(int P, int stride, const uin
         ft->rect = rect;
         ft->wide = s_wide;
         ft->cut = one_phase ? 0xffffffffu : s_cut;
+        // the frame's counts to the host (rr_api.hip pair_counts_wait) now, while the split scan
+        // runs: the host sizes the binning by the total and leaves the phases' split on the device
+        if (box) {
+            const uint32_t sat = 0xffffffffu;
+            __hip_atomic_store(box + 0, L > sat ? sat : (uint32_t)L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + 1, rect > sat ? sat : (uint32_t)rect, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + 3, s_wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
 void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
-                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, hipStream_t st) {
-    // every Gaussian of frames up to 16384, else evenly spaced samples (16384 at most: ~1 in 61 at 1M)
-    const int stride = std::max(1, (P + 16383) / 16384);
-    k_early_cut<<<1, 1024, 0, st>>>(P, stride, keys, tiles, block_sums, block_wide, (P + 255) / 256, den, min_pairs,
-                                    ft);
+                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, void* temp,
+                      uint32_t* box, uint32_t seq, hipStream_t st) {
+    if (P <= 0) return;
+    const int stride = std::max(1, (P + kCutSamples - 1) / kCutSamples);
+    const int ns = (P + stride - 1) / stride;
+    uint2* samples = static_cast<uint2*>(temp);
+    k_cut_sample<<<(ns + 255) / 256, 256, 0, st>>>(ns, stride, keys, tiles, samples);
+    k_early_cut<<<1, 1024, 0, st>>>(ns, samples, block_sums, block_wide, (P + 255) / 256, den, min_pairs, ft, box,
+                                    seq);
 }
 
 // ---- the phases' Gaussian lists: scan of {A pairs, B pairs, A rows, B rows} in index order ------
@@ -221,27 +249,18 @@ __global__ __launch_bounds__(256) void k_split_scan_prefix(Quad* __restrict__ to
 
 __device__ __forceinline__ uint32_t sat32(unsigned long long v) { return v > 0xffffffffull ? 0xffffffffu : (uint32_t)v; }
 
-// The frame's counts to the host: {L_A, rect, seq, wide, L_B} into the coherent pinned mailbox (the
-// sequence number last, system-scope release; rr_api.hip pair_counts_wait spins on it) and into ft.
-__device__ __forceinline__ void publish_counts(FrameTotals* ft, const Quad& q, uint32_t* box, uint32_t seq) {
-    const uint32_t a = sat32(q.pa), b = sat32(q.pb), r = sat32(ft->rect), wd = ft->wide;
-    ft->LA = a;
-    ft->LB = b;
+// The phases' counts stay on the device (the duplicate and sort launches read them from ft).
+__device__ __forceinline__ void store_split(FrameTotals* ft, const Quad& q) {
+    ft->LA = sat32(q.pa);
+    ft->LB = sat32(q.pb);
     ft->GA = (uint32_t)q.ca;
     ft->GB = (uint32_t)q.cb;
-    if (box) {
-        __hip_atomic_store(box + 0, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(box + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(box + 3, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(box + 4, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
 }
 
 template <bool PREFIX>
 __global__ __launch_bounds__(256) void k_split_scan(const uint2* __restrict__ tiles, const uint32_t* __restrict__ keys,
                                                     int P, const Quad* __restrict__ tot, PhaseLists lists,
-                                                    FrameTotals* __restrict__ ft, uint32_t* box, uint32_t seq) {
+                                                    FrameTotals* __restrict__ ft) {
     constexpr int IPT = kPairScanItems / 256;  // 8 consecutive items per thread
     __shared__ Quad s[4];
     __shared__ Quad s_w[4];
@@ -287,24 +306,26 @@ __global__ __launch_bounds__(256) void k_split_scan(const uint2* __restrict__ ti
         }
     }
     // the last thread of the grid holds the frame's totals (items past P count as 0)
-    if (blockIdx.x == gridDim.x - 1 && t == 255) publish_counts(ft, ex, box, seq);
+    if (blockIdx.x == gridDim.x - 1 && t == 255) store_split(ft, ex);
 }
 
+// the split scan's block totals, or (first) k_early_cut's samples
 size_t split_scan_temp_bytes(int P) {
-    return (size_t)std::max((P + kPairScanItems - 1) / kPairScanItems, 1) * sizeof(Quad);
+    return std::max((size_t)std::max((P + kPairScanItems - 1) / kPairScanItems, 1) * sizeof(Quad),
+                    (size_t)kCutSamples * sizeof(uint2));
 }
 
 void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
-                       uint32_t* box, uint32_t seq, int direct_blocks, hipStream_t st) {
+                       int direct_blocks, hipStream_t st) {
     if (P <= 0) return;
     const int nb = (P + kPairScanItems - 1) / kPairScanItems;
     Quad* tot = static_cast<Quad*>(temp);
     k_split_scan_totals<<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot);
     if (nb <= direct_blocks) {
-        k_split_scan<false><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft, box, seq);
+        k_split_scan<false><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft);
     } else {
         k_split_scan_prefix<<<1, 256, 0, st>>>(tot, nb);
-        k_split_scan<true><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft, box, seq);
+        k_split_scan<true><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft);
     }
 }
 
@@ -318,7 +339,10 @@ void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLis
 // pass through the scratch arrays in chunks of kSxCap (same ranking, one global digit scan per
 // pass).  Ranking (rr_sort.hip's): wave w owns the contiguous items [w 64 R, (w + 1) 64 R) in
 // rounds of 64; lanes holding the same digit find each other with one ballot per digit bit.
-constexpr int kSxCap = 4096;
+#ifndef RR_SX_CAP
+#define RR_SX_CAP 2048  // 4096: ranges stage 0.110 vs 0.095 ms/step (profiles/r04h_sortexpand_cap_ab.jsonl)
+#endif
+constexpr int kSxCap = RR_SX_CAP;
 constexpr int kSxMaxR = kSxCap / 256;
 #ifndef RR_SX_GLOBAL
 #define RR_SX_GLOBAL 1  // 0: ISA inspection builds without the long-run path
@@ -408,33 +432,20 @@ __device__ __forceinline__ void sx_rank_chunk(SxShared& sh, const uint32_t (&kr)
     __syncthreads();
 }
 
-// Every bin's run [start, end) of the bin-sorted keys, written by the boundaries around it: between
-// positions i and i + 1 holding bins a < b, bins a+1..b start and bins a..b-1 end at i + 1 (empty
-// bins in the gap get start = end); the head and the tail close the bins below the first key and
-// above the last.  Every bin is written exactly once, so the array needs no clearing.  One launch
-// over the pairs instead of a binary search in every k_sortexpand workgroup.
+// Every bin's run [start, end) of the bin-sorted keys into `bounds`, which the caller zeroed (it
+// lives in the image buffer's cleared block): the first item of a bin writes its start, the last its
+// end; a bin without pairs keeps {0, 0}.  One launch over the pairs instead of a binary search in
+// every k_sortexpand workgroup (and no loop over the empty bins between two keys: phase B's keys are
+// sparse, and such loops cost 24 us there).
 template <typename K>
 __global__ __launch_bounds__(256) void k_bin_bounds(uint32_t n_host, const uint32_t* __restrict__ n_dev,
-                                                    const K* __restrict__ keys, int nbins, uint2* __restrict__ bounds) {
+                                                    const K* __restrict__ keys, uint2* __restrict__ bounds) {
     const uint32_t n = n_dev ? *n_dev : n_host;
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (n == 0) {  // no pairs: every run empty
-        for (uint32_t b = i; b < (uint32_t)nbins; b += gridDim.x * 256u) bounds[b] = make_uint2(0u, 0u);
-        return;
-    }
     if (i >= n) return;
     const uint32_t k = (uint32_t)keys[i];
-    const uint32_t kp = i == 0 ? 0xffffffffu : (uint32_t)keys[i - 1];  // "bin -1"
-    const uint32_t kn = i + 1 == n ? (uint32_t)nbins : (uint32_t)keys[i + 1];
-    if (k != kp)  // bins kp+1 .. k start at i (and the empty ones among them end there)
-        for (uint32_t b = kp + 1u; b <= k; b++) {
-            if (b < k) bounds[b] = make_uint2(i, i);
-            else bounds[b].x = i;
-        }
-    if (k != kn) {  // bin k ends at i + 1; the empty bins k+1 .. kn-1 start and end there
-        bounds[k].y = i + 1;
-        for (uint32_t b = k + 1u; b < kn && b < (uint32_t)nbins; b++) bounds[b] = make_uint2(i + 1, i + 1);
-    }
+    if (i == 0 || (uint32_t)keys[i - 1] != k) bounds[k].x = i;
+    if (i + 1 == n || (uint32_t)keys[i + 1] != k) bounds[k].y = i + 1;
 }
 
 template <typename K>
@@ -599,7 +610,7 @@ void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const u
                        uint2* bounds, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0) return;
-    k_bin_bounds<K><<<std::max<uint32_t>(1u, (L + 255) / 256), 256, 0, st>>>(L, n_dev, keys, nb, bounds);
+    if (L > 0) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
                                         open_bits, scr0, scr1);
 }

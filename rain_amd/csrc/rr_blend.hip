@@ -392,6 +392,7 @@ void launch_bwd_prologue(float* gacc, size_t nfloats, int T, const uint32_t* til
 
 namespace {
 int g_bwd_waves = 0;
+int g_dup_order = 1;
 int g_bwd_order = -1;  // -1: RAIN_BWD_TILE_ORDER or the default (on)
 int g_fwd_order = -1;  // -1: RAIN_FWD_TILE_ORDER or the default (off)
 int g_fwd_s_waves = 2, g_fwd_s_b_waves = 4;
@@ -419,6 +420,10 @@ bool bwd_tile_order() {
     }
     return g_bwd_order != 0;
 }
+
+// the backward's tile order computed by an extra workgroup of the phase-B duplicate (default) or
+// by the backward prologue (rr_set_tuning "dup_tile_order" 0)
+bool dup_tile_order() { return g_dup_order != 0; }
 
 bool fwd_tile_order() {
     if (g_fwd_order < 0) {
@@ -451,6 +456,7 @@ int set_tuning(const char* key, int value) {
     else if (k == "sort_max_rounds") set_sort_max_rounds(value);
     else if (k == "pair_scan_direct_blocks") set_pair_scan_direct_blocks(value);
     else if (k == "wide_bin_keys") set_wide_bin_keys(value != 0);
+    else if (k == "dup_tile_order") g_dup_order = value != 0;
     else return 1;
     return 0;
 }

@@ -504,14 +504,34 @@ __device__ __forceinline__ void tile_order_body256(int T, const uint32_t* __rest
     __shared__ uint32_t hist[1024];
     __shared__ uint32_t wsum[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    auto bucket = [&](int i) {
-        if (open_bits && ((open_bits[i >> 5] >> (i & 31)) & 1u)) return 0u;
-        return 1023u - min(cost[i] >> 2, 1023u);
+    // the buckets of a batch of kTB tiles per thread, every load in flight at once (clamped
+    // indices, no per-tile condition: a load inside the atomic loop made each of the T / 256
+    // iterations wait for its own memory round trip, ~50 us at T = 8160)
+    constexpr int kTB = 16;
+    auto buckets = [&](int base, uint32_t (&bk)[kTB]) {
+        uint32_t c[kTB], ob[kTB];
+#pragma unroll
+        for (int k = 0; k < kTB; k++) {
+            const int i = min(base + k * 256 + t, T - 1);
+            c[k] = cost[i];
+            ob[k] = open_bits ? open_bits[i >> 5] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kTB; k++) {
+            const int i = min(base + k * 256 + t, T - 1);
+            bk[k] = ((ob[k] >> (i & 31)) & 1u) ? 0u : 1023u - min(c[k] >> 2, 1023u);
+        }
     };
 #pragma unroll
     for (int k = 0; k < 4; k++) hist[4 * t + k] = 0;
     __syncthreads();
-    for (int i = t; i < T; i += 256) atomicAdd(&hist[bucket(i)], 1u);
+    for (int base = 0; base < T; base += kTB * 256) {
+        uint32_t bk[kTB];
+        buckets(base, bk);
+#pragma unroll
+        for (int k = 0; k < kTB; k++)
+            if (base + k * 256 + t < T) atomicAdd(&hist[bk[k]], 1u);
+    }
     __syncthreads();
     uint32_t v[4], sum = 0;
 #pragma unroll
@@ -535,7 +555,16 @@ __device__ __forceinline__ void tile_order_body256(int T, const uint32_t* __rest
         run += v[k];
     }
     __syncthreads();
-    for (int i = t; i < T; i += 256) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
+    // order inside a bucket is free (atomic slot claims)
+    for (int base = 0; base < T; base += kTB * 256) {
+        uint32_t bk[kTB];
+        buckets(base, bk);
+#pragma unroll
+        for (int k = 0; k < kTB; k++) {
+            const int i = base + k * 256 + t;
+            if (i < T) order[atomicAdd(&hist[bk[k]], 1u)] = (uint32_t)i;
+        }
+    }
 }
 
 }  // namespace rr

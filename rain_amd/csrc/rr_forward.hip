@@ -198,7 +198,8 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ offsets,
                                                    const Splat* __restrict__ splats, const int* __restrict__ radii,
                                                    int gx, int gy, int cull, const uint32_t* __restrict__ first,
-                                                   uint32_t pair0, uint32_t win, uint32_t L, K* __restrict__ keys,
+                                                   uint32_t pair0, uint32_t win, const uint32_t* __restrict__ L_dev,
+                                                   K* __restrict__ keys,
                                                    uint32_t* __restrict__ vals, int dbits,
                                                    uint32_t* __restrict__ counts, int units,
                                                    const uint32_t* __restrict__ open_bits,
@@ -225,7 +226,10 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
     const int ndig = 1 << dbits;
     constexpr bool filter = FILTER;
     for (int d = t; d < ndig; d += 256) hist[d] = 0;
-    const uint32_t w0 = pair0 + wb * win, w1 = min(w0 + win, L);
+    // the phase's pair count is device-side: the grid covers the frame's total, and a window past
+    // the phase's end is empty (zero counts, zero length)
+    const uint32_t L = *L_dev;
+    const uint32_t w0 = pair0 + wb * win, w1 = max(w0, min(w0 + win, L));
     const uint32_t wn = w1 - w0;
     if (filter) {
         for (uint32_t j = t; j < wn; j += 256) s_val[j] = 0xffffffffu;  // not emitted
@@ -264,7 +268,7 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
     const int bgx = bins_x(gx);
     const int s0 = (int)first[wb];
     const int P = (int)*n_dev;  // entries of the phase's list
-    for (int base = s0;; base += 256) {
+    for (int base = s0; wn > 0; base += 256) {
         const int s = base + t;
         if (s < P) {
             // two dependent load steps per Gaussian: {offsets, index} then {radius, record} (the
@@ -418,7 +422,7 @@ bool launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
     auto kern = d.open_bits ? k_duplicate<K, true> : k_duplicate<K, false>;
     const bool ord = d.open_bits && d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
     kern<<<d.nwin + (ord ? 1 : 0), 256, 0, st>>>(d.n_list, d.idx, d.off, d.splats, d.radii, d.gx, d.gy, d.cull,
-                                                  d.first, d.pair0, d.win, d.L, d.keys, d.vals, d.dbits, d.counts,
+                                                  d.first, d.pair0, d.win, d.L_dev, d.keys, d.vals, d.dbits, d.counts,
                                                   d.nwin, d.open_bits, d.unit_len, d.n_total, ord ? d.order_cost : nullptr,
                                                   ord ? d.order_out : nullptr, d.order_flag, d.order_T);
     return !d.starts_done && second;

@@ -6,8 +6,9 @@
 namespace rr {
 
 // Per-frame scalars of the depth-sort-free binning (rr_bin.hip), in the geometry buffer: written by
-// k_early_cut (L, rect, wide, cut) and by the split scan's last thread (LA, LB), which also copies
-// them to the host mailbox.  Also the device copy the no-mailbox read-back path reads.
+// k_early_cut (L, rect, wide, cut; it also copies L, rect and wide to the host mailbox) and by the
+// split scan's last thread (LA, LB, GA, GB: read on the device only).  Also the device copy the
+// no-mailbox read-back path reads.
 struct FrameTotals {
     unsigned long long L;     // (bin, Gaussian) pairs of the frame
     unsigned long long rect;  // bounding-rect tiles (the reference's num_rendered)
@@ -188,17 +189,18 @@ void set_pair_scan_direct_blocks(int nb);
 int pair_scan_direct_blocks();
 // rr_bin.hip: the depth-sort-free binning
 void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
-                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, hipStream_t st);
+                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, void* temp,
+                      uint32_t* box, uint32_t seq, hipStream_t st);  // temp: split_scan_temp_bytes(P)
 // The phases' Gaussian lists (PhaseLists, ft->GA / GB entries); the last thread publishes {LA, rect,
 // seq, wide, LB} to box (may be null) and ft.  temp: split_scan_temp_bytes(P)
 size_t split_scan_temp_bytes(int P);
 void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
-                       uint32_t* box, uint32_t seq, int direct_blocks, hipStream_t st);
+                       int direct_blocks, hipStream_t st);
 template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
                        uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                       uint2* bounds, hipStream_t st);  // bounds: [bins] scratch for the bins' runs
+                       uint2* bounds, hipStream_t st);  // bounds: [bins], zero on entry (the bins' runs)
 template <typename K>
 struct DupArgs {
     int P;                       // capacity of the lists (the frame's Gaussians)
@@ -212,7 +214,7 @@ struct DupArgs {
     uint32_t pair0;      // pair index of window 0
     uint32_t win;        // pairs per window (= sort unit)
     int nwin;
-    uint32_t L;          // end of the pair range
+    const uint32_t* L_dev;  // device: end of the pair range (FrameTotals LA / LB)
     K* keys;             // window k writes [k*win, ...)
     uint32_t* vals;
     int dbits;           // first-pass digit width of the tile sort
@@ -246,9 +248,6 @@ struct DupArgs {
 // returns whether the window starts (both sets) were computed
 template <typename K>
 bool launch_duplicate(const DupArgs<K>& d, hipStream_t st);
-template <typename K>
-void launch_expand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals, int gx, int gy,
-                   uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
@@ -270,13 +269,15 @@ constexpr int kPointListPad = 16;
 // vals_in == nullptr means values = input index.  keys_out may be nullptr only for a single pass.
 // n is the (host-known) capacity; unit_len (per-unit item counts of a sparse first pass, counts
 // produced by the caller) and n_dev (device-side item count after compaction) are optional.
+// n_hint (0: n) is the expected count the unit length is chosen for when n is only a capacity
+// (units then cover n; those past the device count are empty).
 template <typename K>
-size_t radix_sort_temp_bytes(size_t n, int bits);
+size_t radix_sort_temp_bytes(size_t n, int bits, size_t n_hint = 0);
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
-                            const uint32_t* n_dev = nullptr);
+                            const uint32_t* n_dev = nullptr, size_t n_hint = 0);
 const char* radix_sort_last_error();
 void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
 void set_sort_min_units_tile(int units);  // the same for the bin sorts (<= 16-bit keys; default 1024)
@@ -290,7 +291,7 @@ struct RadixPlan {
     int units, unit_items, rounds, dbits0;
 };
 template <typename K>
-RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit);
+RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit, size_t n_hint = 0);
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st);
 // The Gaussian-sharded multi-GPU step (rr_gauss_backward_views): one view's camera as the
 // per-Gaussian backward reads it.
@@ -312,6 +313,7 @@ namespace rr {
 // Tuning knob: waves per tile (1, 2, 4) of the blend kernels; 0 = default / env override.
 void set_blend_config(int fwd_waves, int bwd_waves);
 bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_set_tuning "bwd_tile_order")
+bool dup_tile_order();  // the phase-B duplicate computes the backward's tile order (rr_set_tuning "dup_tile_order")
 bool fwd_tile_order();  // forward blends dispatch tiles longest list first (rr_set_tuning "fwd_tile_order")
 int blend_fwd_s_waves(bool phase_b);  // waves per tile of the forward blend ("fwd_s_waves" / "fwd_b_waves")
 void set_fwd_trace(void* dev_buf);

@@ -335,11 +335,13 @@ int rounds_for(size_t n, int bits) {
     return r;
 }
 
+// n_hint (0: n): the size the unit length is chosen for, where n is only a capacity and the device
+// holds the count (the binning's phases: sized by the frame's pair total, filled ~1/3 and ~2/3)
 template <typename K>
-SortLayout sort_layout(void* buf, size_t n, int bits) {
+SortLayout sort_layout(void* buf, size_t n, int bits, size_t n_hint) {
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     SortLayout s{};
-    const int rounds = rounds_for(n, bits);
+    const int rounds = rounds_for(n_hint ? n_hint : n, bits);
     const size_t units = (n + (size_t)64 * kWaves * rounds - 1) / ((size_t)64 * kWaves * rounds);
     const int dmax = sort_max_dbits(bits);
     const size_t nc = std::max<size_t>(((size_t)1 << dmax) * units, 1);
@@ -362,18 +364,18 @@ SortLayout sort_layout(void* buf, size_t n, int bits) {
 }  // namespace
 
 template <typename K>
-size_t radix_sort_temp_bytes(size_t n, int bits) {
-    return sort_layout<K>(nullptr, n, bits).total;
+size_t radix_sort_temp_bytes(size_t n, int bits, size_t n_hint) {
+    return sort_layout<K>(nullptr, n, bits, n_hint).total;
 }
 
 template <typename K>
-RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit) {
+RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit, size_t n_hint) {
     RadixPlan p{};
     const int bits = end_bit - begin_bit;
     if (n == 0 || bits <= 0) return p;
-    const SortLayout s = sort_layout<K>(temp, n, bits);
+    const SortLayout s = sort_layout<K>(temp, n, bits, n_hint);
     const int passes = sort_passes(bits);
-    p.rounds = rounds_for(n, bits);
+    p.rounds = rounds_for(n_hint ? n_hint : n, bits);
     p.unit_items = 64 * kWaves * p.rounds;
     p.units = (int)((n + p.unit_items - 1) / p.unit_items);
     p.dbits0 = (bits + passes - 1) / passes;
@@ -391,16 +393,16 @@ const char* radix_sort_last_error() { return g_why; }
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
-                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev) {
+                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev, size_t n_hint) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
     g_why = "";
     if (n > 0xffffffffull || bits <= 0 || bits > (int)(8 * sizeof(K))) return g_why = "bad size/bits", hipErrorInvalidValue;
     if (unit_len && !n_dev) return g_why = "sparse units without n_dev", hipErrorInvalidValue;
-    const SortLayout s = sort_layout<K>(temp, n, bits);
+    const SortLayout s = sort_layout<K>(temp, n, bits, n_hint);
     if (temp_bytes < s.total) return g_why = "temp too small", hipErrorInvalidValue;
     const int passes = sort_passes(bits);
-    const int rounds = rounds_for(n, bits);
+    const int rounds = rounds_for(n_hint ? n_hint : n, bits);
     const int units = (int)((n + (size_t)64 * kWaves * rounds - 1) / ((size_t)64 * kWaves * rounds));
     const K* ksrc = keys_in;
     const uint32_t* vsrc = vals_in;
@@ -455,15 +457,15 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
     return e;
 }
 
-template size_t radix_sort_temp_bytes<uint16_t>(size_t, int);
-template size_t radix_sort_temp_bytes<uint32_t>(size_t, int);
+template size_t radix_sort_temp_bytes<uint16_t>(size_t, int, size_t);
+template size_t radix_sort_temp_bytes<uint32_t>(size_t, int, size_t);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*);
+                                               const uint32_t*, size_t);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*);
-template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int);
-template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int);
+                                               const uint32_t*, size_t);
+template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int, size_t);
+template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int, size_t);
 
 }  // namespace rr

@@ -190,8 +190,9 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 
 
 def debug_views(geomBuffer, binningBuffer, imageBuffer, num_rendered, P, W, H):
-    """Copies of the forward's private binning/image state (tests only): point_list [4 num_pairs]
-    (tile t's list is point_list[ranges[t, 0]:ranges[t, 1]]),
+    """Copies of the forward's private binning/image state (tests only): point_list [8 num_pairs]
+    (4 slots per pair in the phase-A region [0, 4L) and the phase-B region [4L, 8L); tile t's list
+    is point_list[ranges[t, 0]:ranges[t, 1]]),
     ranges [T,2], tile_max [T], final_T [H,W], n_contrib [H,W], splats [P,12]."""
     f = _frame(P, 0, 0, W, H, 1.0, 1.0, 1.0, 0.3, False, False)
     num_rendered = frame_stats(geomBuffer, imageBuffer, P, W, H)["num_pairs"]
@@ -214,7 +215,7 @@ def debug_views(geomBuffer, binningBuffer, imageBuffer, num_rendered, P, W, H):
 
     return dict(
         # per-tile lists live at the ranges' absolute positions: 4 slots per (bin, Gaussian) pair
-        point_list=grab(v.point_list, 4 * num_rendered, torch.int32, binningBuffer) if num_rendered else
+        point_list=grab(v.point_list, 8 * num_rendered, torch.int32, binningBuffer) if num_rendered else
         torch.empty((0,), dtype=torch.int32, device=dev),
         ranges=grab(v.ranges, 2 * T, torch.int32, imageBuffer).view(T, 2),
         tile_max=grab(v.tile_max, T, torch.int32, imageBuffer),
