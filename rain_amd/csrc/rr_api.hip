@@ -306,7 +306,7 @@ int check(const rr_frame* f, hipStream_t st, const char* what) {
 // wait has outlasted any frame the stream is queried: a launch / kernel error is reported, and a
 // stream that went idle without the sequence number becoming visible falls back to the plain copy.
 struct Mailbox {
-    uint32_t* host = nullptr;  // [L, rect, seq, wide], coherent pinned
+    uint32_t* host = nullptr;  // [L, rect, seq, wide, -, phase-B pairs of the last frame], coherent pinned
     uint32_t* dev = nullptr;   // device alias of host
     uint32_t seq = 0;
     bool failed = false;       // allocation failed: always use the copy
@@ -511,6 +511,20 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
 
 namespace {
 
+// Phase B's binning: the gather path (k_duplicate_b_gather: one thread per phase-B Gaussian;
+// k_bsort_small: one workgroup counts the pairs into their bins; k_sortexpand with index passes — 3
+// launches) while phase B is small, the windowed duplicate + bin sort + bounds + sort-expand (8
+// launches) otherwise.  Both give the same lists; the choice is a
+// prediction from the last frame's phase-B pair count, which the phase-B sort-expand leaves in the
+// mailbox (word 5).  rr_set_tuning "phase_b_gather": 1 always, 0 never, -1 (default) predicted.
+int g_b_gather = -1;
+constexpr uint32_t kBGatherMax = 1u << 16;
+bool phase_b_gather() {
+    if (g_b_gather >= 0) return g_b_gather != 0;
+    const Mailbox& mb = g_mailbox;
+    return mb.host && !mb.failed && __atomic_load_n(mb.host + 5, __ATOMIC_RELAXED) <= kBGatherMax;
+}
+
 // Tile lists for one frame: duplicate -> bin sort -> per-bin depth order + tile lists -> blend,
 // once (single phase) or as the two phases of early-stop binning (rr_kernels.hpp BlendPhase).
 // The host knows the frame's total L only: phase A's pairs (split-scan offsets .x, [0, LA)) go to
@@ -527,6 +541,9 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     d.P = P; d.splats = gm.splats; d.radii = radii;
     d.gx = gx; d.gy = gy; d.cull = cull;
     const PhaseHints h = phase_hints(L, early);
+    // (the one-workgroup bin count holds up to 16384 bins: 4K frames have 8160)
+    const bool gather = early && bins_x(gx) * bins_y(gy) <= 16384 && phase_b_gather();
+    uint32_t* report = g_mailbox.failed ? nullptr : g_mailbox.dev;
     // phase A (or the only phase): its pairs for every tile
     const RadixPlan pa = tile_plan<K>(bn.temp, L, bn.bits, h.a);
     const RadixPlan pb = tile_plan<K>(bn.temp, L, bn.bits, h.b);  // phase B (early-stop binning)
@@ -537,7 +554,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L_dev = &gm.ft->LA;
         d.zero = reinterpret_cast<uint32_t*>(im.ranges); d.nzero = (int)(im.zero_bytes / sizeof(uint32_t));
         d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
-        if (early) {
+        if (early && !gather) {
             d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
             d.n_list_b = &gm.ft->GB; d.off_b = gm.lists.off_b;
         }
@@ -555,7 +572,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_sortexpand<K>(L, &gm.ft->LA, keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u,
-                             bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, im.bounds_a, st);
+                             bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, im.bounds_a, nullptr, st);
     }
     RR_STAGE_CHECK("sort-expand");
     {
@@ -568,6 +585,26 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     RR_STAGE_CHECK("blend forward");
     if (!early) return RR_OK;
     // phase B: its pairs, only for tiles phase A left open; region [L, 2L) of the pair arrays
+    if (gather) {
+        {
+            StageTimer tm(RR_STAGE_DUPLICATE, st);
+            d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b;
+            d.keys = keys + L; d.vals = bn.vals + L;
+            d.open_bits = im.open_bits; d.n_total = im.counters;
+            if (bwd_tile_order() && !fwd_tile_order() && dup_tile_order()) {
+                d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
+            }
+            launch_duplicate_b_gather<K>(d, st);
+        }
+        RR_STAGE_CHECK("duplicate (phase B gather)");
+        {
+            StageTimer tm(RR_STAGE_RANGES, st);
+            launch_sortexpand_small<K>(P, keys + L, bn.vals + L, im.counters, bn.vals_sorted + L, gm.depth_keys, gm.ft,
+                                       gx, gy, 4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + L,
+                                       bn.scr1 + L, im.bounds_b, report, st);
+        }
+        RR_STAGE_CHECK("sort-expand (phase B gather)");
+    } else {
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
         d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b; d.off = gm.lists.off_b;
@@ -596,9 +633,10 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_sortexpand<K>(L, im.counters, keys_sorted + L, bn.vals_sorted + L, gm.depth_keys, gm.ft, gx, gy,
                              4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + L, bn.scr1 + L, im.bounds_b,
-                             st);
+                             report, st);
     }
     RR_STAGE_CHECK("sort-expand (phase B)");
+    }
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = kBlendPhaseB;
@@ -1125,6 +1163,14 @@ int rr_debug_set_fwd_trace(void* dev_buf) {
 }
 
 int rr_set_tuning(const char* key, int value) {
+    if (key && std::string(key) == "early_den") {  // early-stop split: phase A ~1/den of the pairs
+        g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
+        return RR_OK;
+    }
+    if (key && std::string(key) == "phase_b_gather") {
+        g_b_gather = value < 0 ? -1 : (value != 0);
+        return RR_OK;
+    }
     if (set_tuning(key, value) != 0) return fail(RR_ERR_ARG, std::string("unknown tuning key: ") + (key ? key : "(null)"));
     return RR_OK;
 }

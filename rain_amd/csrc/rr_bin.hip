@@ -448,38 +448,23 @@ __global__ __launch_bounds__(256) void k_bin_bounds(uint32_t n_host, const uint3
     if (i + 1 == n || (uint32_t)keys[i + 1] != k) bounds[k].y = i + 1;
 }
 
-template <typename K>
-__global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bounds,
-                                                    const K* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                    const uint32_t* __restrict__ depth_keys,
-                                                    const FrameTotals* __restrict__ ft, int gx, int gy,
-                                                    uint32_t out_base, uint32_t* __restrict__ point_list,
-                                                    uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits,
-                                                    uint2* __restrict__ scr0, uint2* __restrict__ scr1) {
-    __shared__ SxShared sh;
-    const int bgx = bins_x(gx);
-    const int bin = blockIdx.x;
-    const int X = bin % bgx, Y = bin / bgx;
-    if (open_bits) {  // phase B: a bin whose tiles all closed in phase A holds no pair, and its
-                      // tiles' ranges were cleared with the frame's: nothing to search or write
-        bool any = false;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int tx = 2 * X + (b & 1), ty = 2 * Y + (b >> 1);
-            if (tx < gx && ty < gy) {
-                const uint32_t tile = (uint32_t)(ty * gx + tx);
-                any = any || ((open_bits[tile >> 5] >> (tile & 31)) & 1u);
-            }
-        }
-        if (!any) return;  // block-uniform
-    }
+// One bin's run of `len` (bin, Gaussian) pairs in index order -> depth order -> its four tiles'
+// lists at out_base + 4 lo + b len, and the tiles' ranges.  The run is vals[lo, lo + len) or, with
+// lds_vals (len <= kSxCap), already in sh.v.  Longer runs use scr0 / scr1 at [lo, lo + len).
+__device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int gx, int gy, uint32_t lo, uint32_t len,
+                                               const uint32_t* __restrict__ vals, bool lds_vals,
+                                               const uint32_t* __restrict__ depth_keys, bool wide, int ipasses,
+                                               uint32_t out_base, uint32_t* __restrict__ point_list,
+                                               uint2* __restrict__ ranges, uint2* __restrict__ scr0,
+                                               uint2* __restrict__ scr1) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint2 run = bounds[bin];  // the bin's run [lo, hi) of the bin-sorted pairs
-    const uint32_t lo = run.x, hi = run.y;
-    const uint32_t len = hi - lo;
-    // 27-bit keys in 3 passes of 9 bits, wider frames in 4 of 8
-    const bool wide = ft->wide != 0u;
-    const int passes = wide ? 4 : 3, db = wide ? 8 : 9;
+    // ipasses 9-bit passes on the Gaussian index first (a run gathered in no particular order: they
+    // restore index order), then the depth key: 27 bits in 3 passes of 9, wider frames in 4 of 8
+    const int dbd = wide ? 8 : 9;
+    const int passes = ipasses + (wide ? 4 : 3);
+    auto shift_of = [&](int p) { return p < ipasses ? 9 * p : (p - ipasses) * dbd; };
+    auto db_of = [&](int p) { return p < ipasses ? 9 : dbd; };
+    auto key_of = [&](int p, uint32_t v) { return p < ipasses ? (v & BIN_ID_MASK) : depth_keys[v & BIN_ID_MASK]; };
     const uint2* sorted_g = nullptr;  // global path: the sorted run
     if (len > 1 && len <= (uint32_t)kSxCap) {
         const int R = (int)((len + 255) / 256);
@@ -488,13 +473,20 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
         // every round's loads unconditional, the index clamped into the run: a condition (per lane or
         // on R) made the compiler branch and wait around each load; the clamped extra loads hit the
         // cache line of the run's last item and are never used (items past len are not ranked)
+        if (lds_vals) {  // gathered into sh.v by the caller
 #pragma unroll
-        for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + min(wl + (uint32_t)r * 64 + lane, len - 1)];
+            for (int r = 0; r < kSxMaxR; r++) vr[r] = sh.v[min(wl + (uint32_t)r * 64 + lane, len - 1)];
+            __syncthreads();  // every read of the gathered run before the first pass writes sh.v
+        } else {
 #pragma unroll
-        for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
+            for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + min(wl + (uint32_t)r * 64 + lane, len - 1)];
+        }
+#pragma unroll
+        for (int r = 0; r < kSxMaxR; r++) kr[r] = key_of(0, vr[r]);  // all gathers in flight
         for (int p = 0; p < passes; p++) {
-            sx_rank_chunk(sh, kr, vr, R, len, p * db, db, false, nullptr);
+            sx_rank_chunk(sh, kr, vr, R, len, shift_of(p), db_of(p), false, nullptr);
             if (p + 1 < passes) {
+                const bool rekey = p + 1 == ipasses;  // index order done: the depth keys from here on
 #pragma unroll
                 for (int r = 0; r < kSxMaxR; r++) {
                     const uint32_t i = wl + (uint32_t)r * 64 + lane;
@@ -503,23 +495,27 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
                         vr[r] = sh.v[i];
                     }
                 }
+                if (rekey)
+#pragma unroll
+                    for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];
                 __syncthreads();  // every read of this pass's order before the next pass's writes
             }
         }
     } else if (RR_SX_GLOBAL && len > (uint32_t)kSxCap) {
-        // chunks of kSxCap in order; pass p reads run p - 1 (pass 0: the bin-sorted values with their
-        // gathered depth keys) and writes the run at lo of scratch p % 2
-        const int ndig = 1 << db;
-        const uint32_t mask = (uint32_t)ndig - 1u;
+        // chunks of kSxCap in order; pass p reads run p - 1 (pass 0: the run's values with their
+        // keys) and writes the run at lo of scratch p % 2
         for (int p = 0; p < passes; p++) {
+            const int db = db_of(p), shift = shift_of(p);
+            const int ndig = 1 << db;
+            const uint32_t mask = (uint32_t)ndig - 1u;
             const uint2* src = p == 0 ? nullptr : ((p & 1) ? scr0 : scr1) + lo;
             uint2* dst = ((p & 1) ? scr1 : scr0) + lo;
-            const int shift = p * db;
+            const bool fresh = src == nullptr || p == ipasses;  // keys recomputed from the values
             // digit totals of the whole run -> each digit's first slot
             for (int d = t; d < ndig; d += 256) sh.cursor[d] = 0;
             __syncthreads();
             for (uint32_t i = t; i < len; i += 256) {
-                const uint32_t k = src ? src[i].x : depth_keys[vals[lo + i] & BIN_ID_MASK];
+                const uint32_t k = fresh ? key_of(p, src ? src[i].y : vals[lo + i]) : src[i].x;
                 atomicAdd(&sh.cursor[(k >> shift) & mask], 1u);
             }
             __syncthreads();
@@ -556,9 +552,10 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
                 } else {
 #pragma unroll
                     for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + c0 + min(wl + (uint32_t)r * 64 + lane, clen - 1)];
-#pragma unroll
-                    for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];
                 }
+                if (fresh)
+#pragma unroll
+                    for (int r = 0; r < kSxMaxR; r++) kr[r] = key_of(p, vr[r]);
                 sx_rank_chunk(sh, kr, vr, R, clen, shift, db, true, dst);
             }
             __syncthreads();
@@ -573,7 +570,7 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
     for (uint32_t r0 = 0; r0 < len; r0 += 256) {
         const uint32_t j = r0 + (uint32_t)t;
         uint32_t v = 0u;
-        if (j < len) v = len <= 1 ? vals[lo + j] : sorted_g ? sorted_g[j].y : sh.v[j];
+        if (j < len) v = (len <= 1 && !lds_vals) ? vals[lo + j] : sorted_g ? sorted_g[j].y : sh.v[j];
         const uint32_t m = j < len ? v >> BIN_SHIFT : 0u;
         uint32_t rank[4];
 #pragma unroll
@@ -603,22 +600,155 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
     }
 }
 
+// Phase B's pair count to the host mailbox (word 5; rr_api.hip): the next frame chooses its phase-B
+// binning from it (a prediction only: both ways give the same lists).
+__device__ __forceinline__ void report_phase_b(uint32_t* box, uint32_t n) {
+    __hip_atomic_store(box + 5, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Phase B of few pairs (k_duplicate_b_gather emitted them densely, [0, n), in no particular order):
+// one workgroup counts them per bin in LDS, writes every bin's run into bounds and scatters the values
+// into their bins (order inside a bin arbitrary: k_sortexpand restores index order with its index
+// passes).  One launch instead of the bin sort's five and the bounds launch.  Correct for any n,
+// fast while n is small (one workgroup walks all n pairs twice): the host takes this path when the
+// previous frame's phase B was small (rr_api.hip phase_b_gather).
+constexpr int kSmallSortMaxBins = 16384;
+template <typename K>
+__global__ __launch_bounds__(1024) void k_bsort_small(const K* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                      const uint32_t* __restrict__ n_dev, int nb,
+                                                      uint32_t* __restrict__ vals_out, uint2* __restrict__ bounds) {
+    __shared__ uint32_t cnt[kSmallSortMaxBins];
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t n = *n_dev;
+    for (int b = t; b < nb; b += 1024) cnt[b] = 0u;
+    __syncthreads();
+    constexpr int kG = 8;  // loads in flight per thread
+    for (uint32_t b0 = 0; b0 < n; b0 += 1024u * kG) {
+        K kk[kG];
+#pragma unroll
+        for (int q = 0; q < kG; q++) kk[q] = keys[min(b0 + (uint32_t)(q * 1024 + t), n - 1)];
+#pragma unroll
+        for (int q = 0; q < kG; q++)
+            if (b0 + (uint32_t)(q * 1024 + t) < n) atomicAdd(&cnt[(uint32_t)kk[q]], 1u);
+    }
+    __syncthreads();
+    // exclusive scan over the bins: a contiguous run of bins per thread, then the waves
+    const int per = (nb + 1023) / 1024;
+    const int b0 = t * per;
+    uint32_t sum = 0;
+    for (int k = 0; k < per; k++)
+        if (b0 + k < nb) sum += cnt[b0 + k];
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int i = 0; i < w; i++) run += wsum[i];
+    for (int k = 0; k < per; k++) {
+        const int b = b0 + k;
+        if (b < nb) {
+            const uint32_t c = cnt[b];
+            bounds[b] = make_uint2(run, run + c);
+            cnt[b] = run;  // the bin's next free slot
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024u * kG) {
+        K kk[kG];
+        uint32_t vv[kG];
+#pragma unroll
+        for (int q = 0; q < kG; q++) {
+            const uint32_t i = min(i0 + (uint32_t)(q * 1024 + t), n - 1);
+            kk[q] = keys[i];
+            vv[q] = vals[i];
+        }
+#pragma unroll
+        for (int q = 0; q < kG; q++)
+            if (i0 + (uint32_t)(q * 1024 + t) < n) vals_out[atomicAdd(&cnt[(uint32_t)kk[q]], 1u)] = vv[q];
+    }
+}
+
+// per bin: open test (phase B), the bin's run from k_bin_bounds, then sortexpand_run
+template <typename K>
+__global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bounds,
+                                                    const K* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ depth_keys,
+                                                    const FrameTotals* __restrict__ ft, int gx, int gy,
+                                                    uint32_t out_base, uint32_t* __restrict__ point_list,
+                                                    uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits,
+                                                    uint2* __restrict__ scr0, uint2* __restrict__ scr1,
+                                                    const uint32_t* __restrict__ n_dev, uint32_t* report,
+                                                    int ipasses) {
+    __shared__ SxShared sh;
+    const int bgx = bins_x(gx);
+    const int bin = blockIdx.x;
+    const int X = bin % bgx, Y = bin / bgx;
+    if (report && bin == 0 && threadIdx.x == 0) report_phase_b(report, *n_dev);
+    if (open_bits) {  // phase B: a bin whose tiles all closed in phase A holds no pair, and its
+                      // tiles' ranges were cleared with the frame's: nothing to search or write
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int tx = 2 * X + (b & 1), ty = 2 * Y + (b >> 1);
+            if (tx < gx && ty < gy) {
+                const uint32_t tile = (uint32_t)(ty * gx + tx);
+                any = any || ((open_bits[tile >> 5] >> (tile & 31)) & 1u);
+            }
+        }
+        if (!any) return;  // block-uniform
+    }
+    const uint2 run = bounds[bin];  // the bin's run [lo, hi) of the bin-sorted pairs
+    sortexpand_run(sh, X, Y, gx, gy, run.x, run.y - run.x, vals, false, depth_keys, ft->wide != 0u, ipasses,
+                   out_base, point_list, ranges, scr0, scr1);
+}
+
 template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
                        uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                       uint2* bounds, hipStream_t st) {
+                       uint2* bounds, uint32_t* report, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0) return;
     if (L > 0) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
-                                        open_bits, scr0, scr1);
+                                        open_bits, scr0, scr1, n_dev, n_dev ? report : nullptr, 0);
 }
 template void launch_sortexpand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, uint2*, uint2*, hipStream_t);
+                                          uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
 template void launch_sortexpand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, uint2*, uint2*, hipStream_t);
+                                          uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
+
+int index_passes(int P) {  // 9-bit passes covering the Gaussian indices [0, P)
+    int b = 1;
+    while (b < 28 && (1u << b) < (uint32_t)P) b++;
+    return (b + 8) / 9;
+}
+
+template <typename K>
+bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* vals_sorted,
+                             const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
+                             uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
+                             uint2* bounds, uint32_t* report, hipStream_t st) {
+    const int nb = bins_x(gx) * bins_y(gy);
+    if (nb <= 0 || nb > kSmallSortMaxBins) return false;
+    k_bsort_small<K><<<1, 1024, 0, st>>>(keys, vals, n_dev, nb, vals_sorted, bounds);
+    k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
+                                        open_bits, scr0, scr1, n_dev, report, index_passes(P));
+    return true;
+}
+template bool launch_sortexpand_small<uint16_t>(int, const uint16_t*, const uint32_t*, const uint32_t*, uint32_t*,
+                                                const uint32_t*, const FrameTotals*, int, int, uint32_t, uint32_t*,
+                                                uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
+template bool launch_sortexpand_small<uint32_t>(int, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t*,
+                                                const uint32_t*, const FrameTotals*, int, int, uint32_t, uint32_t*,
+                                                uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
 
 }  // namespace rr

@@ -370,6 +370,125 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
     for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + wb] = hist[d];
 }
 
+// Phase B of few pairs (rr_bin.hip k_sortexpand_gather): one thread per phase-B Gaussian instead of
+// output-driven windows over all of phase B's ~2/3 of the pairs, most of which land on tiles phase A
+// closed.  A Gaussian whose rectangle holds no open tile is done after one record load; the others
+// count their kept (bin, Gaussian) pairs, the workgroup reserves its total with one atomic on
+// *n_total and writes them densely — in no particular order, which the gather's index passes
+// restore.  The extra workgroup 0 computes the backward's tile order as k_duplicate's does.
+template <typename K>
+__global__ __launch_bounds__(256) void k_duplicate_b_gather(const uint32_t* __restrict__ n_dev,
+                                                            const uint32_t* __restrict__ idx,
+                                                            const Splat* __restrict__ splats,
+                                                            const int* __restrict__ radii, int gx, int gy, int cull,
+                                                            K* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                            const uint32_t* __restrict__ open_bits,
+                                                            uint32_t* __restrict__ n_total,
+                                                            const uint32_t* __restrict__ order_cost,
+                                                            uint32_t* __restrict__ order_out,
+                                                            uint32_t* __restrict__ order_flag, int order_T) {
+    if (order_out && blockIdx.x == 0) {
+        tile_order_body256(order_T, order_cost, open_bits, order_out);
+        if (threadIdx.x == 0) *order_flag = (uint32_t)order_T;
+        return;
+    }
+    const int wb = order_out ? (int)blockIdx.x - 1 : (int)blockIdx.x;
+    const bool mask_lds = gx * gy <= 65536;
+    __shared__ uint32_t s_open[2048];
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t s_base;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (mask_lds)
+        for (int i = t; i < (gx * gy + 31) / 32; i += 256) s_open[i] = open_bits[i];
+    __syncthreads();
+    auto is_open = [&](uint32_t tile) -> bool {
+        const uint32_t word = mask_lds ? s_open[tile >> 5] : open_bits[tile >> 5];
+        return ((word >> (tile & 31)) & 1u) != 0;
+    };
+    auto open4 = [&](int X, int Y) -> uint32_t {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int tx = 2 * X + (b & 1), ty = 2 * Y + (b >> 1);
+            if (tx < gx && ty < gy && is_open((uint32_t)(ty * gx + tx))) m |= 1u << b;
+        }
+        return m;
+    };
+    auto rect_open = [&](int x0, int y0, int x1, int y1) -> bool {
+        for (int y = y0; y < y1; y++) {
+            const uint32_t lo = (uint32_t)(y * gx + x0), hi = (uint32_t)(y * gx + x1);  // bits [lo, hi)
+            for (uint32_t wd = lo >> 5; wd <= (hi - 1) >> 5; wd++) {
+                uint32_t m = mask_lds ? s_open[wd] : open_bits[wd];
+                if (wd == lo >> 5) m &= ~0u << (lo & 31);
+                if (wd == (hi - 1) >> 5) m &= ~0u >> (31 - ((hi - 1) & 31));
+                if (m) return true;
+            }
+        }
+        return false;
+    };
+    const int bgx = bins_x(gx);
+    const int s = wb * 256 + t;
+    const int P = (int)*n_dev;  // entries of the phase-B list
+    uint32_t g = 0, cnt = 0;
+    CullEll ell{};
+    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    bool live = false;
+    if (s < P) {
+        g = idx[s];
+        const int r = radii[g];
+        const float4 A = splats[g].a;
+        const float4 Bv = splats[g].b;
+        asm volatile("" ::"v"(r), "v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(Bv.x), "v"(Bv.w));
+        tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
+        if (x0 < x1 && y0 < y1 && rect_open(x0, y0, x1, y1)) {
+            float ccx, ccy, ccz;
+            splat_conic(A, Bv, ccx, ccy, ccz);
+            ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
+            live = true;
+        }
+    }
+    // the kept pairs, in the duplicate's enumeration (bin rows, then bin columns); pass 0 counts,
+    // pass 1 writes
+    auto walk = [&](bool emit, uint32_t pos) {
+        uint32_t c = 0;
+        for (int Y = y0 >> 1; Y < (y1 + 1) >> 1; Y++) {
+            int l0, h0, l1, h1, Xa, Xb;
+            bin_row_spans(ell, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
+            bin_cols(l0, h0, l1, h1, Xa, Xb);
+            for (int X = Xa; X < Xb; X++) {
+                const uint32_t m = bin_mask(X, l0, h0, l1, h1) & open4(X, Y);
+                if (!m) continue;
+                if (emit) {
+                    keys[pos + c] = (K)(Y * bgx + X);
+                    vals[pos + c] = g | (m << BIN_SHIFT);
+                }
+                c++;
+            }
+        }
+        return c;
+    };
+    if (live) cnt = walk(false, 0u);
+    // the workgroup's kept pairs: wave prefix sums, one reservation
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        pre += i < w ? wsum[i] : 0u;
+        tot += wsum[i];
+    }
+    if (tot == 0) return;  // block-uniform
+    if (t == 0) s_base = atomicAdd(n_total, tot);
+    __syncthreads();
+    if (cnt) walk(true, s_base + pre + incl - cnt);
+}
+
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
                                                       const float* __restrict__ view, uint8_t* __restrict__ present) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -429,6 +548,17 @@ bool launch_duplicate(const DupArgs<K>& d, hipStream_t st) {
 }
 template bool launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
 template bool launch_duplicate<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
+
+template <typename K>
+void launch_duplicate_b_gather(const DupArgs<K>& d, hipStream_t st) {
+    if (d.P == 0) return;
+    const bool ord = d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
+    k_duplicate_b_gather<K><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
+        d.n_list, d.idx, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits, d.n_total,
+        ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T);
+}
+template void launch_duplicate_b_gather<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
+template void launch_duplicate_b_gather<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;

@@ -200,7 +200,16 @@ template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
                        uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                       uint2* bounds, hipStream_t st);  // bounds: [bins], zero on entry (the bins' runs)
+                       uint2* bounds, uint32_t* report, hipStream_t st);  // bounds: [bins], zero on entry
+// Phase B of few pairs (rr_bin.hip k_bsort_small + k_sortexpand with index passes): the densely
+// emitted, unordered phase-B pairs (k_duplicate_b_gather) counted and scattered into their bins by
+// one workgroup — no bin sort.  report: optional host-mapped mailbox; word 5 receives the phase's
+// pair count.  false: more bins than the one-workgroup count holds (nothing launched).
+template <typename K>
+bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* vals_sorted,
+                             const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
+                             uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
+                             uint2* bounds, uint32_t* report, hipStream_t st);
 template <typename K>
 struct DupArgs {
     int P;                       // capacity of the lists (the frame's Gaussians)
@@ -248,6 +257,10 @@ struct DupArgs {
 // returns whether the window starts (both sets) were computed
 template <typename K>
 bool launch_duplicate(const DupArgs<K>& d, hipStream_t st);
+// phase B of few pairs: one thread per phase-B Gaussian (d.n_list / d.idx), kept pairs written densely
+// and unordered at d.keys / d.vals, their count in *d.n_total (rr_forward.hip k_duplicate_b_gather)
+template <typename K>
+void launch_duplicate_b_gather(const DupArgs<K>& d, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 

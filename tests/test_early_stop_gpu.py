@@ -12,16 +12,20 @@ from tests.test_parity_gpu import _check_forward, _check_grads, _dpix
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def split(monkeypatch):
-    """Force the two-phase path onto small frames: phase A = L/den pairs, any frame size."""
+@pytest.fixture(params=["gather", "windows"])
+def split(request, monkeypatch):
+    """Force the two-phase path onto small frames: phase A = L/den pairs, any frame size; phase B
+    binned by each of its two paths (rr_api.hip phase_b_gather: few pairs gathered per bin, or the
+    windowed duplicate + bin sort)."""
     from rain_amd import _native as N
     from rain_amd.diff_gaussian_rasterization import _C
 
     def set_split(den):
         N.check(N.raster().rr_set_binning_config(den, 1), "binning config")
 
+    N.check(N.raster().rr_set_tuning(b"phase_b_gather", 1 if request.param == "gather" else 0), "tuning")
     yield set_split
+    N.check(N.raster().rr_set_tuning(b"phase_b_gather", -1), "tuning")
     N.check(N.raster().rr_set_binning_config(0, 0), "binning config")
     monkeypatch.setattr(_C, "EARLY_STOP", True)
 
