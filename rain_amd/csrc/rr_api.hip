@@ -113,6 +113,7 @@ struct Img {
     uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask (in the zeroed block; the phase-A blend sets it)
     uint2* bounds_a;      // [bins] phase A's (or the single phase's) bin runs (zeroed block; k_bin_bounds)
     uint2* bounds_b;      // [bins] phase B's
+    uint32_t* bin_cnt;    // [bins] phase B's pair count per bin (the gather path)
     uint32_t* order;      // [T] backward blend dispatch order (heaviest tiles first)
     size_t total;
 };
@@ -124,16 +125,17 @@ Img carve_img(void* buf, int W, int H) {
     m.final_T = c.take<float>(N);
     m.n_contrib = c.take<uint32_t>(N);
     // one block, cleared before every render: ranges [T], ranges_b [T], counters [4],
-    // open_bits [ceil(T/32)], bounds_a [bins], bounds_b [bins]
+    // open_bits [ceil(T/32)], bounds_a [bins], bounds_b [bins], bin_cnt [bins]
     const size_t nbits = ((size_t)T + 31) / 32;
     const size_t NB = (size_t)std::max(bins_x(grid_x(W)) * bins_y(grid_y(H)), 1);
-    const size_t nz = 2 * (size_t)T + 2 + (nbits + 1) / 2 + 2 * NB;
+    const size_t nz = 2 * (size_t)T + 2 + (nbits + 1) / 2 + 2 * NB + (NB + 1) / 2;
     m.ranges = c.take<uint2>(nz);
     m.ranges_b = m.ranges ? m.ranges + T : nullptr;
     m.counters = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T) : nullptr;
     m.open_bits = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T + 2) : nullptr;
     m.bounds_a = m.ranges ? m.ranges + 2 * T + 2 + (nbits + 1) / 2 : nullptr;
     m.bounds_b = m.ranges ? m.bounds_a + NB : nullptr;
+    m.bin_cnt = m.ranges ? reinterpret_cast<uint32_t*>(m.bounds_b + NB) : nullptr;
     m.zero_bytes = nz * sizeof(uint2);
     m.tile_max = c.take<uint32_t>(T);
     m.open = c.take<uint8_t>(T);
@@ -512,12 +514,12 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
 namespace {
 
 // Phase B's binning: the gather path (k_duplicate_b_gather: one thread per phase-B Gaussian;
-// k_bsort_small: one workgroup counts the pairs into their bins; k_sortexpand with index passes — 3
-// launches) while phase B is small, the windowed duplicate + bin sort + bounds + sort-expand (8
-// launches) otherwise.  Both give the same lists; the choice is a
-// prediction from the last frame's phase-B pair count, which the phase-B sort-expand leaves in the
-// mailbox (word 5).  rr_set_tuning "phase_b_gather": 1 always, 0 never, -1 (default) predicted.
-int g_b_gather = -1;
+// k_bin_count + k_bin_scan + k_bin_scatter: the pairs into their bins; k_sortexpand restoring
+// (depth, index) order — 5 launches) or the windowed duplicate + bin sort + bounds + sort-expand (8
+// launches).  Both give the same lists.  rr_set_tuning "phase_b_gather": 1 (default) the gather
+// path, 0 the windowed one, -1 the gather path when the last frame's phase B held at most
+// kBGatherMax pairs (the phase-B sort-expand leaves its count in mailbox word 5).
+int g_b_gather = 1;
 constexpr uint32_t kBGatherMax = 1u << 16;
 bool phase_b_gather() {
     if (g_b_gather >= 0) return g_b_gather != 0;
@@ -599,9 +601,9 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         RR_STAGE_CHECK("duplicate (phase B gather)");
         {
             StageTimer tm(RR_STAGE_RANGES, st);
-            launch_sortexpand_small<K>(P, keys + L, bn.vals + L, im.counters, bn.vals_sorted + L, gm.depth_keys, gm.ft,
-                                       gx, gy, 4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + L,
-                                       bn.scr1 + L, im.bounds_b, report, st);
+            launch_sortexpand_small<K>(P, keys + L, bn.vals + L, im.counters, im.bin_cnt, bn.vals_sorted + L,
+                                       gm.depth_keys, gm.ft, gx, gy, 4u * L, bn.point_list, im.ranges_b, im.open_bits,
+                                       bn.scr0 + L, bn.scr1 + L, im.bounds_b, report, st);
         }
         RR_STAGE_CHECK("sort-expand (phase B gather)");
     } else {

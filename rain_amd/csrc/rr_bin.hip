@@ -448,6 +448,35 @@ __global__ __launch_bounds__(256) void k_bin_bounds(uint32_t n_host, const uint3
     if (i + 1 == n || (uint32_t)keys[i + 1] != k) bounds[k].y = i + 1;
 }
 
+// After a depth-only sort of a run in no particular order: every group of equal depth keys put in
+// Gaussian-index order in place, one thread per group (groups are clones at one position: a few
+// items).  Returns true when a group longer than kTieMax was left for a full index-pass sort.
+constexpr uint32_t kTieMax = 32;
+template <typename KeyAt, typename ValAt, typename SetVal>
+__device__ __forceinline__ bool fix_ties(uint32_t len, KeyAt key_at, ValAt val_at, SetVal set_val) {
+    bool big = false;
+    for (uint32_t i = threadIdx.x; i + 1 < len; i += 256) {
+        const uint32_t k = key_at(i);
+        if (key_at(i + 1) != k || (i > 0 && key_at(i - 1) == k)) continue;  // not a group's first item
+        uint32_t j = i + 2;
+        while (j < len && j - i <= kTieMax && key_at(j) == k) j++;
+        if (j - i > kTieMax) {
+            big = true;
+            continue;
+        }
+        for (uint32_t a = i + 1; a < j; a++) {  // insertion sort on the index
+            const uint32_t v = val_at(a);
+            uint32_t b = a;
+            while (b > i && (val_at(b - 1) & BIN_ID_MASK) > (v & BIN_ID_MASK)) {
+                set_val(b, val_at(b - 1));
+                b--;
+            }
+            set_val(b, v);
+        }
+    }
+    return __syncthreads_or(big);
+}
+
 // One bin's run of `len` (bin, Gaussian) pairs in index order -> depth order -> its four tiles'
 // lists at out_base + 4 lo + b len, and the tiles' ranges.  The run is vals[lo, lo + len) or, with
 // lds_vals (len <= kSxCap), already in sh.v.  Longer runs use scr0 / scr1 at [lo, lo + len).
@@ -458,13 +487,15 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
                                                uint2* __restrict__ ranges, uint2* __restrict__ scr0,
                                                uint2* __restrict__ scr1) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    // ipasses 9-bit passes on the Gaussian index first (a run gathered in no particular order: they
-    // restore index order), then the depth key: 27 bits in 3 passes of 9, wider frames in 4 of 8
+    // The depth key: 27 bits in 3 passes of 9, wider frames in 4 of 8.  A run in no particular order
+    // (ipasses > 0: the phase-B pairs of the gather path) needs index order among equal depth keys:
+    // its LDS path sorts by depth alone and, only if two neighbours then share a key, sorts again
+    // with ipasses 9-bit passes on the Gaussian index first; its global path always does.
     const int dbd = wide ? 8 : 9;
-    const int passes = ipasses + (wide ? 4 : 3);
-    auto shift_of = [&](int p) { return p < ipasses ? 9 * p : (p - ipasses) * dbd; };
-    auto db_of = [&](int p) { return p < ipasses ? 9 : dbd; };
-    auto key_of = [&](int p, uint32_t v) { return p < ipasses ? (v & BIN_ID_MASK) : depth_keys[v & BIN_ID_MASK]; };
+    int ip = 0;  // index passes of the current attempt
+    auto shift_of = [&](int p) { return p < ip ? 9 * p : (p - ip) * dbd; };
+    auto db_of = [&](int p) { return p < ip ? 9 : dbd; };
+    auto key_of = [&](int p, uint32_t v) { return p < ip ? (v & BIN_ID_MASK) : depth_keys[v & BIN_ID_MASK]; };
     const uint2* sorted_g = nullptr;  // global path: the sorted run
     if (len > 1 && len <= (uint32_t)kSxCap) {
         const int R = (int)((len + 255) / 256);
@@ -481,36 +512,52 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
 #pragma unroll
             for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + min(wl + (uint32_t)r * 64 + lane, len - 1)];
         }
+        for (int attempt = 0;; attempt++) {
+            const int passes = ip + (wide ? 4 : 3);
 #pragma unroll
-        for (int r = 0; r < kSxMaxR; r++) kr[r] = key_of(0, vr[r]);  // all gathers in flight
-        for (int p = 0; p < passes; p++) {
-            sx_rank_chunk(sh, kr, vr, R, len, shift_of(p), db_of(p), false, nullptr);
-            if (p + 1 < passes) {
-                const bool rekey = p + 1 == ipasses;  // index order done: the depth keys from here on
+            for (int r = 0; r < kSxMaxR; r++) kr[r] = key_of(0, vr[r]);  // all gathers in flight
+            for (int p = 0; p < passes; p++) {
+                sx_rank_chunk(sh, kr, vr, R, len, shift_of(p), db_of(p), false, nullptr);
+                if (p + 1 < passes) {
+                    const bool rekey = p + 1 == ip;  // index order done: the depth keys from here on
 #pragma unroll
-                for (int r = 0; r < kSxMaxR; r++) {
-                    const uint32_t i = wl + (uint32_t)r * 64 + lane;
-                    if (r < R && i < len) {
-                        kr[r] = sh.k[i];
-                        vr[r] = sh.v[i];
+                    for (int r = 0; r < kSxMaxR; r++) {
+                        const uint32_t i = wl + (uint32_t)r * 64 + lane;
+                        if (r < R && i < len) {
+                            kr[r] = sh.k[i];
+                            vr[r] = sh.v[i];
+                        }
                     }
-                }
-                if (rekey)
+                    if (rekey)
 #pragma unroll
-                    for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];
-                __syncthreads();  // every read of this pass's order before the next pass's writes
+                        for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];
+                    __syncthreads();  // every read of this pass's order before the next pass's writes
+                }
             }
+            if (ipasses == 0 || attempt > 0) break;
+            // unordered run sorted by depth alone: equal keys put in index order in place, or (a long
+            // group) the full sort with the index passes first
+            if (!fix_ties(
+                    len, [&](uint32_t i) { return sh.k[i]; }, [&](uint32_t i) { return sh.v[i]; },
+                    [&](uint32_t i, uint32_t v) { sh.v[i] = v; }))
+                break;  // block-uniform
+            ip = ipasses;
+#pragma unroll
+            for (int r = 0; r < kSxMaxR; r++) vr[r] = sh.v[min(wl + (uint32_t)r * 64 + lane, len - 1)];
+            __syncthreads();  // every read of the depth order before the index passes write sh.v
         }
     } else if (RR_SX_GLOBAL && len > (uint32_t)kSxCap) {
         // chunks of kSxCap in order; pass p reads run p - 1 (pass 0: the run's values with their
         // keys) and writes the run at lo of scratch p % 2
+      for (int attempt = 0;; attempt++) {
+        const int passes = ip + (wide ? 4 : 3);
         for (int p = 0; p < passes; p++) {
             const int db = db_of(p), shift = shift_of(p);
             const int ndig = 1 << db;
             const uint32_t mask = (uint32_t)ndig - 1u;
             const uint2* src = p == 0 ? nullptr : ((p & 1) ? scr0 : scr1) + lo;
             uint2* dst = ((p & 1) ? scr1 : scr0) + lo;
-            const bool fresh = src == nullptr || p == ipasses;  // keys recomputed from the values
+            const bool fresh = src == nullptr || p == ip;  // keys recomputed from the values
             // digit totals of the whole run -> each digit's first slot
             for (int d = t; d < ndig; d += 256) sh.cursor[d] = 0;
             __syncthreads();
@@ -561,6 +608,16 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
             __syncthreads();
         }
         sorted_g = (((passes - 1) & 1) ? scr1 : scr0) + lo;
+        if (ipasses == 0 || attempt > 0) break;
+        uint2* sg = const_cast<uint2*>(sorted_g);
+        __threadfence_block();
+        if (!fix_ties(
+                len, [&](uint32_t i) { return sg[i].x; }, [&](uint32_t i) { return sg[i].y; },
+                [&](uint32_t i, uint32_t v) { sg[i].y = v; }))
+            break;
+        // a long group: the full sort, index passes first, from the run's original values
+        ip = ipasses;
+      }
     }
     // the four tile lists, stable, from the depth-ordered run (LDS, global scratch, or the single /
     // empty run straight from vals)
@@ -606,39 +663,46 @@ __device__ __forceinline__ void report_phase_b(uint32_t* box, uint32_t n) {
     __hip_atomic_store(box + 5, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Phase B of few pairs (k_duplicate_b_gather emitted them densely, [0, n), in no particular order):
-// one workgroup counts them per bin in LDS, writes every bin's run into bounds and scatters the values
-// into their bins (order inside a bin arbitrary: k_sortexpand restores index order with its index
-// passes).  One launch instead of the bin sort's five and the bounds launch.  Correct for any n,
-// fast while n is small (one workgroup walks all n pairs twice): the host takes this path when the
-// previous frame's phase B was small (rr_api.hip phase_b_gather).
-constexpr int kSmallSortMaxBins = 16384;
-template <typename K>
-__global__ __launch_bounds__(1024) void k_bsort_small(const K* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                      const uint32_t* __restrict__ n_dev, int nb,
-                                                      uint32_t* __restrict__ vals_out, uint2* __restrict__ bounds) {
-    __shared__ uint32_t cnt[kSmallSortMaxBins];
-    __shared__ uint32_t wsum[16];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+// Phase B of the gather path (k_duplicate_b_gather emitted its pairs densely, [0, n), in no
+// particular order): k_bin_count counts them per bin, k_bin_scan turns the counts into every bin's
+// run (bounds) and a cursor, k_bin_scatter drops each pair's value into its bin's run (order inside a
+// bin arbitrary: k_sortexpand restores (depth, index) order).  Three launches instead of the bin
+// sort's five and the bounds launch.  Count and scatter run kBinGroups workgroups over the same
+// strided item sets; each aggregates its items per bin in LDS, so a global atomic is paid per
+// (workgroup, bin) and not per pair (per-pair atomics on a few hot bins serialise: +40 us).
+constexpr int kBinScanMax = 16384;  // bins one workgroup holds (4K frames: 8160)
+constexpr int kBinGroups = 64;
+__global__ __launch_bounds__(1024) void k_bin_count(const void* __restrict__ keys_v, int wide_keys,
+                                                    const uint32_t* __restrict__ n_dev, int nb,
+                                                    uint32_t* __restrict__ bin_cnt) {
+    __shared__ uint32_t h[kBinScanMax];
+    const int t = threadIdx.x;
     const uint32_t n = *n_dev;
-    for (int b = t; b < nb; b += 1024) cnt[b] = 0u;
+    const uint32_t per = (n + kBinGroups - 1) / kBinGroups;
+    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    if (i0 >= i1) return;
+    for (int b = t; b < nb; b += 1024) h[b] = 0u;
     __syncthreads();
-    constexpr int kG = 8;  // loads in flight per thread
-    for (uint32_t b0 = 0; b0 < n; b0 += 1024u * kG) {
-        K kk[kG];
-#pragma unroll
-        for (int q = 0; q < kG; q++) kk[q] = keys[min(b0 + (uint32_t)(q * 1024 + t), n - 1)];
-#pragma unroll
-        for (int q = 0; q < kG; q++)
-            if (b0 + (uint32_t)(q * 1024 + t) < n) atomicAdd(&cnt[(uint32_t)kk[q]], 1u);
+    for (uint32_t i = i0 + t; i < i1; i += 1024) {
+        const uint32_t k = wide_keys ? static_cast<const uint32_t*>(keys_v)[i] : static_cast<const uint16_t*>(keys_v)[i];
+        atomicAdd(&h[k], 1u);
     }
     __syncthreads();
-    // exclusive scan over the bins: a contiguous run of bins per thread, then the waves
-    const int per = (nb + 1023) / 1024;
-    const int b0 = t * per;
-    uint32_t sum = 0;
-    for (int k = 0; k < per; k++)
-        if (b0 + k < nb) sum += cnt[b0 + k];
+    for (int b = t; b < nb; b += 1024)
+        if (h[b]) atomicAdd(&bin_cnt[b], h[b]);
+}
+
+__global__ __launch_bounds__(1024) void k_bin_scan(int nb, uint32_t* __restrict__ bin_cnt, uint2* __restrict__ bounds) {
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    constexpr int kPer = kBinScanMax / 1024;
+    const int b0 = t * kPer;
+    uint32_t c[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        c[k] = b0 + k < nb ? bin_cnt[b0 + k] : 0u;
+        sum += c[k];
+    }
     uint32_t incl = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -649,28 +713,39 @@ __global__ __launch_bounds__(1024) void k_bsort_small(const K* __restrict__ keys
     __syncthreads();
     uint32_t run = incl - sum;
     for (int i = 0; i < w; i++) run += wsum[i];
-    for (int k = 0; k < per; k++) {
-        const int b = b0 + k;
-        if (b < nb) {
-            const uint32_t c = cnt[b];
-            bounds[b] = make_uint2(run, run + c);
-            cnt[b] = run;  // the bin's next free slot
-            run += c;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        if (b0 + k < nb) {
+            bounds[b0 + k] = make_uint2(run, run + c[k]);
+            bin_cnt[b0 + k] = run;  // the bin's next free slot
         }
+        run += c[k];
     }
+}
+
+__global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ keys_v, int wide_keys,
+                                                      const uint32_t* __restrict__ vals,
+                                                      const uint32_t* __restrict__ n_dev, int nb,
+                                                      uint32_t* __restrict__ bin_cur, uint32_t* __restrict__ vals_out) {
+    __shared__ uint32_t h[kBinScanMax];
+    const int t = threadIdx.x;
+    const uint32_t n = *n_dev;
+    const uint32_t per = (n + kBinGroups - 1) / kBinGroups;
+    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    if (i0 >= i1) return;
+    auto key = [&](uint32_t i) -> uint32_t {
+        return wide_keys ? static_cast<const uint32_t*>(keys_v)[i] : static_cast<const uint16_t*>(keys_v)[i];
+    };
+    for (int b = t; b < nb; b += 1024) h[b] = 0u;
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < n; i0 += 1024u * kG) {
-        K kk[kG];
-        uint32_t vv[kG];
-#pragma unroll
-        for (int q = 0; q < kG; q++) {
-            const uint32_t i = min(i0 + (uint32_t)(q * 1024 + t), n - 1);
-            kk[q] = keys[i];
-            vv[q] = vals[i];
-        }
-#pragma unroll
-        for (int q = 0; q < kG; q++)
-            if (i0 + (uint32_t)(q * 1024 + t) < n) vals_out[atomicAdd(&cnt[(uint32_t)kk[q]], 1u)] = vv[q];
+    for (uint32_t i = i0 + t; i < i1; i += 1024) atomicAdd(&h[key(i)], 1u);
+    __syncthreads();
+    for (int b = t; b < nb; b += 1024)  // this workgroup's slots of each bin
+        if (h[b]) h[b] = atomicAdd(&bin_cur[b], h[b]);
+    __syncthreads();
+    for (uint32_t i = i0 + t; i < i1; i += 1024) {
+        const uint32_t k = key(i), v = vals[i];
+        vals_out[atomicAdd(&h[k], 1u)] = v;
     }
 }
 
@@ -733,22 +808,27 @@ int index_passes(int P) {  // 9-bit passes covering the Gaussian indices [0, P)
 }
 
 template <typename K>
-bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* vals_sorted,
-                             const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
-                             uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                             uint2* bounds, uint32_t* report, hipStream_t st) {
+bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
+                             uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
+                             uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
+                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
-    if (nb <= 0 || nb > kSmallSortMaxBins) return false;
-    k_bsort_small<K><<<1, 1024, 0, st>>>(keys, vals, n_dev, nb, vals_sorted, bounds);
+    if (nb <= 0 || nb > kBinScanMax) return false;
+    const int wk = sizeof(K) == 4;
+    k_bin_count<<<kBinGroups, 1024, 0, st>>>(keys, wk, n_dev, nb, bin_cnt);
+    k_bin_scan<<<1, 1024, 0, st>>>(nb, bin_cnt, bounds);
+    k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, vals_sorted);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
                                         open_bits, scr0, scr1, n_dev, report, index_passes(P));
     return true;
 }
 template bool launch_sortexpand_small<uint16_t>(int, const uint16_t*, const uint32_t*, const uint32_t*, uint32_t*,
-                                                const uint32_t*, const FrameTotals*, int, int, uint32_t, uint32_t*,
-                                                uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
+                                                uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
+                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*,
+                                                hipStream_t);
 template bool launch_sortexpand_small<uint32_t>(int, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t*,
-                                                const uint32_t*, const FrameTotals*, int, int, uint32_t, uint32_t*,
-                                                uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
+                                                uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
+                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*,
+                                                hipStream_t);
 
 }  // namespace rr

@@ -374,8 +374,7 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
 // output-driven windows over all of phase B's ~2/3 of the pairs, most of which land on tiles phase A
 // closed.  A Gaussian whose rectangle holds no open tile is done after one record load; the others
 // count their kept (bin, Gaussian) pairs, the workgroup reserves its total with one atomic on
-// *n_total and writes them densely — in no particular order, which the gather's index passes
-// restore.  The extra workgroup 0 computes the backward's tile order as k_duplicate's does.
+// *n_total and writes them densely — in no particular order, which the per-bin sort restores.  The extra workgroup 0 computes the backward's tile order as k_duplicate's does.
 template <typename K>
 __global__ __launch_bounds__(256) void k_duplicate_b_gather(const uint32_t* __restrict__ n_dev,
                                                             const uint32_t* __restrict__ idx,

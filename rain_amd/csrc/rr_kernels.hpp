@@ -201,15 +201,16 @@ void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const u
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
                        uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
                        uint2* bounds, uint32_t* report, hipStream_t st);  // bounds: [bins], zero on entry
-// Phase B of few pairs (rr_bin.hip k_bsort_small + k_sortexpand with index passes): the densely
-// emitted, unordered phase-B pairs (k_duplicate_b_gather) counted and scattered into their bins by
-// one workgroup — no bin sort.  report: optional host-mapped mailbox; word 5 receives the phase's
-// pair count.  false: more bins than the one-workgroup count holds (nothing launched).
+// Phase B of the gather path (rr_bin.hip k_bin_count + k_bin_scan + k_bin_scatter + k_sortexpand):
+// the densely emitted, unordered phase-B pairs (k_duplicate_b_gather) counted per bin (bin_cnt, zero
+// on entry) and dropped into their bins' runs — no bin sort, no bounds launch.  report:
+// optional host-mapped mailbox; word 5 receives the phase's pair count.  false: more bins than one
+// workgroup scans (nothing launched).
 template <typename K>
-bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* vals_sorted,
-                             const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
-                             uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                             uint2* bounds, uint32_t* report, hipStream_t st);
+bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
+                             uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
+                             uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
+                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st);
 template <typename K>
 struct DupArgs {
     int P;                       // capacity of the lists (the frame's Gaussians)

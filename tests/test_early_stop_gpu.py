@@ -114,3 +114,31 @@ def test_fused_raw_path_two_phase(gpu, split):
     assert torch.equal(r, r_full)
     assert torch.equal(c, c_full)
     assert torch.equal(d, d_full)
+
+
+@pytest.mark.parametrize("copies", [2, 48])
+def test_two_phase_equal_depths(gpu, split, monkeypatch, copies):
+    """Gaussians at one depth (densify clones: exact copies) must keep index order inside every tile
+    list — the gather path's per-bin sort sees its phase-B pairs in no particular order and resolves
+    equal depth keys by index (groups of up to 32 in place, longer ones by a full index-pass sort)."""
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    inp, st = make_scene(P=1500, W=160, H=128, sh_degree=2, scale_mult=2.0)
+    n = 1500 // copies
+    src = torch.randint(0, 1500, (n,), generator=torch.Generator().manual_seed(7))
+    for k, v in inp.items():  # the first n * copies rows: `copies` copies of n source rows each
+        if isinstance(v, torch.Tensor) and v.dim() > 0 and v.shape[0] == 1500:
+            rows = v[src.to(v.device)].repeat_interleave(copies, dim=0)
+            v[: rows.shape[0]] = rows
+    # low opacity keeps tiles open, so that phase B holds the copies too
+    inp["opacities"] = inp["opacities"] * 0.2
+    dpix = _dpix(st)
+    monkeypatch.setattr(_C, "EARLY_STOP", False)
+    full = gpu_run(inp, st, gpu, dL_dpix=dpix)
+    monkeypatch.setattr(_C, "EARLY_STOP", True)
+    split(4)
+    early = gpu_run(inp, st, gpu, dL_dpix=dpix)
+    s = _stats(early, 1500, st)
+    assert s["num_binned"] > s["num_pairs"] // 4, s  # phase B binned pairs
+    np.testing.assert_array_equal(early["color"], full["color"])
+    np.testing.assert_array_equal(early["depth"], full["depth"])

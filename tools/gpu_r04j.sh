@@ -11,7 +11,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
   > gpurun_out/${TAG}_gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/${TAG}_gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
-  for o in phase_b_gather=-1 phase_b_gather=0; do
+  for o in phase_b_gather=1 phase_b_gather=0; do
     timeout -k 10 300 python -u tools/variant_step.py --tag $o --tune $o \
       >> gpurun_out/${TAG}_ab.jsonl 2>> gpurun_out/${TAG}_ab.err || { tail -20 gpurun_out/${TAG}_ab.err; exit 1; }
   done
