@@ -124,6 +124,14 @@ int rt_stream_copy(void* dst, const void* src, size_t n_bytes, void* stream);
  * bench.py prices the fused-Adam backward kernel against. */
 int rt_stream_rmw(float* p, float* m, float* v, size_t n_floats, void* stream);
 
+/* Densification statistics of the reference-API step (gaussian_model.py:419-421,
+ * add_densification_stats; train.py:133), one launch each, for the rows with vis[i] != 0:
+ * xyz_gradient_accum[i] += ||grad2d[i, 0:2]|| (torch.norm's rounding), denom[i] += 1;
+ * max_radii2D[i] = max(max_radii2D[i], radii[i]).  grad2d rows are grad_stride floats apart. */
+int rt_densify_stats(int P, const float* grad2d, int grad_stride, const uint8_t* vis, float* xyz_gradient_accum,
+                     float* denom, void* stream);
+int rt_max_radii(int P, const int* radii, const uint8_t* vis, float* max_radii2D, void* stream);
+
 /* Trace markers (not on the training path): launches an empty one-wave kernel named
  * k_trace_mark_begin (which == 0) or k_trace_mark_end (which != 0) on `stream`, so that a
  * rocprofv3 kernel trace can be cut to the launches between them (bench.py's timed loop). */

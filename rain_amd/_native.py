@@ -215,7 +215,8 @@ def loss_lib():
 
 TRAIN_LIB = os.path.join(LIB_DIR, "librain_train.so")
 TRAIN_SYMBOLS = ["rt_adam_step", "rt_adam_step_scaled", "rt_densify_workspace_bytes", "rt_densify_plan",
-                 "rt_densify_apply", "rt_stream_copy", "rt_stream_rmw", "rt_trace_marker", "rt_last_error"]
+                 "rt_densify_apply", "rt_stream_copy", "rt_stream_rmw", "rt_trace_marker", "rt_densify_stats",
+                 "rt_max_radii", "rt_last_error"]
 RT_MAX_GROUPS = 8
 _train = None
 
@@ -268,6 +269,10 @@ def train_lib():
         L.rt_stream_rmw.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
         L.rt_trace_marker.restype = ctypes.c_int
         L.rt_trace_marker.argtypes = [ctypes.c_int, ctypes.c_int, vp]
+        L.rt_densify_stats.restype = ctypes.c_int
+        L.rt_densify_stats.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, vp]
+        L.rt_max_radii.restype = ctypes.c_int
+        L.rt_max_radii.argtypes = [ctypes.c_int, vp, vp, vp, vp]
         L.rt_last_error.restype = ctypes.c_char_p
         _train = L
     return _train

@@ -185,6 +185,49 @@ int rt_trace_marker(int which, int tag, void* stream) {
     return 0;
 }
 
+// Densification statistics of the reference-API step in one launch each (the torch expressions
+// gaussian_model.py:419-421 / train.py:133 take 8 elementwise and reduction launches, ~45 us per
+// step at 1M Gaussians): rows the visibility mask selects gain the screen-gradient norm and a count,
+// or the larger radius.  The norm is torch.norm's: the two squares, each rounded, summed, sqrt.
+__global__ __launch_bounds__(256) void k_densify_stats(int P, const float* __restrict__ grad, int stride,
+                                                       const uint8_t* __restrict__ vis, float* __restrict__ accum,
+                                                       float* __restrict__ denom) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P || !vis[i]) return;
+    const float x = grad[(size_t)i * stride], y = grad[(size_t)i * stride + 1];
+    accum[i] += __fsqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)));
+    denom[i] += 1.0f;
+}
+
+__global__ __launch_bounds__(256) void k_max_radii(int P, const int* __restrict__ radii, const uint8_t* __restrict__ vis,
+                                                   float* __restrict__ max_radii) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P || !vis[i]) return;
+    max_radii[i] = fmaxf(max_radii[i], (float)radii[i]);
+}
+
+int rt_densify_stats(int P, const float* grad2d, int grad_stride, const uint8_t* vis, float* xyz_gradient_accum,
+                     float* denom, void* stream) {
+    if (P < 0 || grad_stride < 2) return fail("densify stats: bad P / stride");
+    if (P == 0) return 0;
+    if (!grad2d || !vis || !xyz_gradient_accum || !denom) return fail("densify stats: null array");
+    k_densify_stats<<<(P + 255) / 256, 256, 0, (hipStream_t)stream>>>(P, grad2d, grad_stride, vis, xyz_gradient_accum,
+                                                                       denom);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(std::string("densify stats launch: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int rt_max_radii(int P, const int* radii, const uint8_t* vis, float* max_radii2D, void* stream) {
+    if (P < 0) return fail("max radii: bad P");
+    if (P == 0) return 0;
+    if (!radii || !vis || !max_radii2D) return fail("max radii: null array");
+    k_max_radii<<<(P + 255) / 256, 256, 0, (hipStream_t)stream>>>(P, radii, vis, max_radii2D);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(std::string("max radii launch: ") + hipGetErrorString(e));
+    return 0;
+}
+
 int rt_stream_rmw(float* p, float* m, float* v, size_t n_floats, void* stream) {
     if ((n_floats & 3u) || !aligned16(p) || !aligned16(m) || !aligned16(v))
         return fail("stream rmw: 4-float multiples, 16-B aligned arrays only");

@@ -267,11 +267,15 @@ class RasterizeRawParams(torch.autograd.Function):
                                                  scale_modifier)
         ctx.st = st
         ctx.mark_non_differentiable(radii, depth)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for radii / depth (two fills)
         return color, radii, depth
 
     @staticmethod
     def backward(ctx, grad_color, _grad_radii, _grad_depth):
         st = ctx.st
+        if grad_color is None:  # the image unused by the loss (materialize_grads off)
+            grad_color = torch.zeros((3, st.frame.height, st.frame.width), dtype=torch.float32,
+                                     device=st.keep[1][0].device)
         ctx.st = None
         _keep, p = st.keep  # kernel order: xyz, f_dc, opacity, scaling, rotation, f_rest
         grads = dict(xyz=torch.empty_like(p[0]), f_dc=torch.empty_like(p[1]), opacity=torch.empty_like(p[2]),

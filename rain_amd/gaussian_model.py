@@ -585,14 +585,35 @@ class GaussianModel:
         The reference's boolean-mask indexing makes the host wait for the device (the mask's count
         sizes the gather); the same update as a select keeps the step free of host syncs: masked
         rows gain exactly the reference's norm, the others exactly 0."""
-        m = update_filter.reshape(-1, 1)
         g = viewspace_point_tensor.grad
+        if g.is_cuda and self._stats_native(g, update_filter):  # one launch (rain_train.h rt_densify_stats)
+            from . import _native
+            _native.check_rt(_native.train_lib().rt_densify_stats(
+                g.shape[0], g.data_ptr(), g.stride(0), update_filter.data_ptr(), self.xyz_gradient_accum.data_ptr(),
+                self.denom.data_ptr(), _native.stream_of(g)), "densify stats")
+            return
+        m = update_filter.reshape(-1, 1)
         self.xyz_gradient_accum += torch.where(m, torch.norm(g[:, :2], dim=-1, keepdim=True), 0.0)
         self.denom += m.to(self.denom.dtype)
+
+    def _stats_native(self, g, mask):
+        """The statistics arrays and inputs in the layout the native kernels take."""
+        P = g.shape[0]
+        return (g.dtype == torch.float32 and g.dim() == 2 and g.shape[1] >= 2 and g.stride(1) == 1
+                and mask.dtype == torch.bool and mask.is_contiguous() and mask.numel() == P
+                and all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == P
+                        for t in (self.xyz_gradient_accum, self.denom, self.max_radii2D)))
 
     def update_max_radii(self, radii, visibility_filter):
         """train.py:133, max_radii2D[vis] = max(max_radii2D[vis], radii[vis]), without the host sync of
         boolean-mask indexing (the same values)."""
+        if radii.is_cuda and radii.dtype == torch.int32 and radii.is_contiguous() \
+                and self._stats_native(radii.view(-1, 1).expand(-1, 2), visibility_filter):
+            from . import _native
+            _native.check_rt(_native.train_lib().rt_max_radii(
+                radii.numel(), radii.data_ptr(), visibility_filter.data_ptr(), self.max_radii2D.data_ptr(),
+                _native.stream_of(radii)), "max radii")
+            return
         self.max_radii2D = torch.where(visibility_filter, torch.maximum(self.max_radii2D, radii.float()),
                                        self.max_radii2D)
 

@@ -129,3 +129,30 @@ def test_native_densify_without_optimizer_state():
         else:
             assert torch.equal(pa.detach(), pb.detach()), name
         assert len(b.optimizer.state.get(pb, {})) == len(a.optimizer.state.get(pa, {}))
+
+
+def test_native_densification_stats_equal_torch(gpu):
+    """GaussianModel.add_densification_stats / update_max_radii on HIP tensors (rain_train.h
+    rt_densify_stats / rt_max_radii, one launch each) give the torch expressions' values
+    (gaussian_model.py:419-421, train.py:133): counts and radii bitwise, the norm sums to the last
+    ulp (torch's reduction may contract x*x + y*y into an fma)."""
+    P = 50_000
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    g = GaussianModel(3, device="cuda")
+    g.set_params(synthetic.random_gaussians(P, sh_degree=3, seed=2, bench=True, device="cuda"))
+    g.xyz_gradient_accum = torch.rand((P, 1), device="cuda", generator=gen)
+    g.denom = torch.randint(0, 5, (P, 1), device="cuda", generator=gen).float()
+    g.max_radii2D = torch.randint(0, 40, (P,), device="cuda", generator=gen).float()
+    vsp = torch.zeros((P, 3), device="cuda", requires_grad=True)
+    vsp.grad = torch.randn((P, 3), device="cuda", generator=gen) * 1e-3
+    vis = torch.rand((P,), device="cuda", generator=gen) > 0.3
+    radii = torch.randint(0, 60, (P,), device="cuda", generator=gen, dtype=torch.int32)
+    m = vis.reshape(-1, 1)
+    want_acc = g.xyz_gradient_accum + torch.where(m, torch.norm(vsp.grad[:, :2], dim=-1, keepdim=True), 0.0)
+    want_den = g.denom + m.float()
+    want_rad = torch.where(vis, torch.maximum(g.max_radii2D, radii.float()), g.max_radii2D)
+    g.add_densification_stats(vsp, vis)
+    g.update_max_radii(radii, vis)
+    assert float(((g.xyz_gradient_accum - want_acc).abs() / want_acc.abs().clamp_min(1e-30)).max()) <= 2.5e-7
+    assert torch.equal(g.denom, want_den)
+    assert torch.equal(g.max_radii2D, want_rad)
