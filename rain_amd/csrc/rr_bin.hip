@@ -35,10 +35,10 @@ namespace rr {
 // den <= 1, a frame below min_pairs pairs or no sampled pair: cut = all ones (one phase).
 constexpr int kCutBuckets = 4096;
 constexpr int kCutShift = kDepthKeyBits - 12;
-// evenly spaced Gaussians: every one up to 8192, ~1 in 123 at 1M (the cut only steers the split's
-// balance; any cut gives the same lists).  Per-bucket sums fit 32 bits: <= 8192 samples of at most
+// evenly spaced Gaussians: every one up to 4096, ~1 in 245 at 1M (the cut only steers the split's
+// balance; any cut gives the same lists).  Per-bucket sums fit 32 bits: <= 4096 samples of at most
 // 2^18 bins each.
-constexpr int kCutSamples = 8192;
+constexpr int kCutSamples = 4096;
 constexpr int kCutSamplesPerThread = kCutSamples / 1024;
 
 // The samples {depth key, pairs} gathered by many workgroups into a dense array (one workgroup
@@ -75,11 +75,22 @@ __global__ __launch_bounds__(1024) void k_early_cut(int ns, const uint2* __restr
     }
     unsigned long long L = 0, rect = 0, S = 0;
     uint32_t wide = 0;
-    for (int i = t; i < nb; i += 1024) {
-        const uint2 v = block_sums[i];
-        L += v.x;
-        rect += v.y;
-        wide |= block_wide[i];
+    for (int i0 = 0; i0 < nb; i0 += 4 * 1024) {  // 4 block records per thread in flight at once
+        uint2 v[4];
+        uint32_t wd[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = min(i0 + q * 1024 + t, nb - 1);
+            v[q] = block_sums[i];
+            wd[q] = block_wide[i];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i0 + q * 1024 + t < nb) {
+                L += v[q].x;
+                rect += v[q].y;
+                wide |= wd[q];
+            }
     }
     __syncthreads();
 #pragma unroll
