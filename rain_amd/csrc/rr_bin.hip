@@ -703,9 +703,11 @@ __global__ __launch_bounds__(1024) void k_bin_count(const void* __restrict__ key
         if (h[b]) atomicAdd(&bin_cnt[b], h[b]);
 }
 
-__global__ __launch_bounds__(1024) void k_bin_scan(int nb, uint32_t* __restrict__ bin_cnt, uint2* __restrict__ bounds) {
+__global__ __launch_bounds__(1024) void k_bin_scan(int nb, const uint32_t* __restrict__ n_dev,
+                                                   uint32_t* __restrict__ bin_cnt, uint2* __restrict__ bounds) {
     __shared__ uint32_t wsum[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (*n_dev == 0) return;  // no pairs: the zeroed bounds already say so
     constexpr int kPer = kBinScanMax / 1024;
     const int b0 = t * kPer;
     uint32_t c[kPer], sum = 0;
@@ -827,7 +829,7 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
     if (nb <= 0 || nb > kBinScanMax) return false;
     const int wk = sizeof(K) == 4;
     k_bin_count<<<kBinGroups, 1024, 0, st>>>(keys, wk, n_dev, nb, bin_cnt);
-    k_bin_scan<<<1, 1024, 0, st>>>(nb, bin_cnt, bounds);
+    k_bin_scan<<<1, 1024, 0, st>>>(nb, n_dev, bin_cnt, bounds);
     k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, vals_sorted);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
                                         open_bits, scr0, scr1, n_dev, report, index_passes(P));

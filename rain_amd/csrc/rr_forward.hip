@@ -397,9 +397,14 @@ __global__ __launch_bounds__(256) void k_duplicate_b_gather(const uint32_t* __re
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t s_base;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (mask_lds)
-        for (int i = t; i < (gx * gy + 31) / 32; i += 256) s_open[i] = open_bits[i];
-    __syncthreads();
+    bool any_open = false;
+    for (int i = t; i < (gx * gy + 31) / 32; i += 256) {
+        const uint32_t word = open_bits[i];
+        if (mask_lds) s_open[i] = word;
+        any_open = any_open || word != 0u;
+    }
+    // phase A closed every tile (about half the bench frames): nothing to emit, no record loads
+    if (!__syncthreads_or(any_open)) return;
     auto is_open = [&](uint32_t tile) -> bool {
         const uint32_t word = mask_lds ? s_open[tile >> 5] : open_bits[tile >> 5];
         return ((word >> (tile & 31)) & 1u) != 0;
