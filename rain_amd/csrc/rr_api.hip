@@ -520,6 +520,9 @@ namespace {
 // path, 0 the windowed one, -1 the gather path when the last frame's phase B held at most
 // kBGatherMax pairs (the phase-B sort-expand leaves its count in mailbox word 5).
 int g_b_gather = 1;
+// The bins' runs from the bin sort's last scatter (default) or from a k_bin_bounds launch over the
+// sorted keys (rr_set_tuning "bounds_in_sort" 0).
+int g_bounds_in_sort = 1;
 constexpr uint32_t kBGatherMax = 1u << 16;
 bool phase_b_gather() {
     if (g_b_gather >= 0) return g_b_gather != 0;
@@ -567,14 +570,15 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_TILE_SORT, st);
         RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.vals_sorted, L, 0, bn.bits,
-                                     st, true, nullptr, &gm.ft->LA, h.a),
+                                     st, true, nullptr, &gm.ft->LA, h.a, g_bounds_in_sort ? im.bounds_a : nullptr),
                  std::string("bin sort (") + radix_sort_last_error() + ")");
     }
     RR_STAGE_CHECK("bin sort");
     {
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_sortexpand<K>(L, &gm.ft->LA, keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u,
-                             bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, im.bounds_a, nullptr, st);
+                             bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, im.bounds_a, g_bounds_in_sort != 0,
+                             nullptr, st);
     }
     RR_STAGE_CHECK("sort-expand");
     {
@@ -627,7 +631,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_TILE_SORT, st);
         RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys + L, keys_sorted + L, bn.vals + L,
-                                     bn.vals_sorted + L, L, 0, bn.bits, st, true, bn.unit_len, im.counters, h.b),
+                                     bn.vals_sorted + L, L, 0, bn.bits, st, true, bn.unit_len, im.counters, h.b,
+                                     g_bounds_in_sort ? im.bounds_b : nullptr),
                  std::string("bin sort, phase B (") + radix_sort_last_error() + ")");
     }
     RR_STAGE_CHECK("bin sort (phase B)");
@@ -635,7 +640,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_sortexpand<K>(L, im.counters, keys_sorted + L, bn.vals_sorted + L, gm.depth_keys, gm.ft, gx, gy,
                              4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + L, bn.scr1 + L, im.bounds_b,
-                             report, st);
+                             g_bounds_in_sort != 0, report, st);
     }
     RR_STAGE_CHECK("sort-expand (phase B)");
     }
@@ -1167,6 +1172,10 @@ int rr_debug_set_fwd_trace(void* dev_buf) {
 int rr_set_tuning(const char* key, int value) {
     if (key && std::string(key) == "early_den") {  // early-stop split: phase A ~1/den of the pairs
         g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
+        return RR_OK;
+    }
+    if (key && std::string(key) == "bounds_in_sort") {
+        g_bounds_in_sort = value != 0;
         return RR_OK;
     }
     if (key && std::string(key) == "phase_b_gather") {

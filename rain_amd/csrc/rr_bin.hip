@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256) void k_bin_bounds(uint32_t n_host, const uint3
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = (uint32_t)keys[i];
-    if (i == 0 || (uint32_t)keys[i - 1] != k) bounds[k].x = i;
+    if (i == 0 || (uint32_t)keys[i - 1] != k) bounds[k].x = ~i;  // {~start, end}: rr_kernels.hpp
     if (i + 1 == n || (uint32_t)keys[i + 1] != k) bounds[k].y = i + 1;
 }
 
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int nb, const uint32_t* __res
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
         if (b0 + k < nb) {
-            bounds[b0 + k] = make_uint2(run, run + c[k]);
+            bounds[b0 + k] = make_uint2(~run, run + c[k]);  // {~start, end}
             bin_cnt[b0 + k] = run;  // the bin's next free slot
         }
         run += c[k];
@@ -791,8 +791,9 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
         }
         if (!any) return;  // block-uniform
     }
-    const uint2 run = bounds[bin];  // the bin's run [lo, hi) of the bin-sorted pairs
-    sortexpand_run(sh, X, Y, gx, gy, run.x, run.y - run.x, vals, false, depth_keys, ft->wide != 0u, ipasses,
+    const uint2 run = bounds[bin];  // the bin's run [lo, hi) of the bin-sorted pairs, {~lo, hi}
+    const uint32_t lo = run.y ? ~run.x : 0u;
+    sortexpand_run(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
                    out_base, point_list, ranges, scr0, scr1);
 }
 
@@ -800,19 +801,19 @@ template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
                        uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                       uint2* bounds, uint32_t* report, hipStream_t st) {
+                       uint2* bounds, bool bounds_ready, uint32_t* report, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0) return;
-    if (L > 0) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
+    if (L > 0 && !bounds_ready) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
                                         open_bits, scr0, scr1, n_dev, n_dev ? report : nullptr, 0);
 }
 template void launch_sortexpand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
+                                          uint2*, uint2*, uint2*, bool, uint32_t*, hipStream_t);
 template void launch_sortexpand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, uint2*, uint2*, uint32_t*, hipStream_t);
+                                          uint2*, uint2*, uint2*, bool, uint32_t*, hipStream_t);
 
 int index_passes(int P) {  // 9-bit passes covering the Gaussian indices [0, P)
     int b = 1;

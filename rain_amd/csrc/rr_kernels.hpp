@@ -200,7 +200,8 @@ template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
                        uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                       uint2* bounds, uint32_t* report, hipStream_t st);  // bounds: [bins], zero on entry
+                       uint2* bounds, bool bounds_ready, uint32_t* report,
+                       hipStream_t st);  // bounds: [bins], zero on entry, or filled by the sort (bounds_ready)
 // Phase B of the gather path (rr_bin.hip k_bin_count + k_bin_scan + k_bin_scatter + k_sortexpand):
 // the densely emitted, unordered phase-B pairs (k_duplicate_b_gather) counted per bin (bin_cnt, zero
 // on entry) and dropped into their bins' runs — no bin sort, no bounds launch.  report:
@@ -291,7 +292,10 @@ template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
                             bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
-                            const uint32_t* n_dev = nullptr, size_t n_hint = 0);
+                            const uint32_t* n_dev = nullptr, size_t n_hint = 0, uint2* bounds = nullptr);
+// bounds (optional, [1 << (end_bit - begin_bit)], zero on entry): each key's run in the sorted output,
+// encoded {~start, end} (a key without items keeps {0, 0}; rr_bin.hip bin_run decodes), written by
+// the last pass's scatter
 const char* radix_sort_last_error();
 void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
 void set_sort_min_units_tile(int units);  // the same for the bin sorts (<= 16-bit keys; default 1024)

@@ -167,7 +167,8 @@ __global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ ke
                                                             const uint32_t* __restrict__ offsets, int units,
                                                             const uint32_t* __restrict__ totals,
                                                             const uint32_t* __restrict__ unit_len,
-                                                            const uint32_t* __restrict__ n_dev) {
+                                                            const uint32_t* __restrict__ n_dev,
+                                                            uint2* __restrict__ bounds) {
     constexpr int ND = 1 << DB;  // digits the kernel is compiled for (>= 1 << dbits)
     constexpr int DPL = ND / 64;  // digits per lane in the digit scans
     __shared__ uint32_t dbase[ND];         // first output slot of each digit
@@ -300,6 +301,14 @@ __global__ __launch_bounds__(64 * SW) void k_rs_scatter(const K* __restrict__ ke
         const uint32_t pos = goff[d] + (uint32_t)j;
         if (keys_out) keys_out[pos] = k;
         vals_out[pos] = s_val[j];
+        if (bounds) {
+            // last pass (the unit's items in final key order): a key's first and last item of this
+            // unit bound its run; the units' pieces of one run are adjacent, so the minimum start and
+            // the maximum end over them are the run (rr_kernels.hpp bounds encoding: x = ~start,
+            // y = end, atomic max on zeroed words).  A unit holds few distinct keys: ~2 atomics each.
+            if (j == 0 || s_key[j - 1] != k) atomicMax(&bounds[(uint32_t)k].x, ~pos);
+            if (j + 1 == nu || s_key[j + 1] != k) atomicMax(&bounds[(uint32_t)k].y, pos + 1u);
+        }
     }
 }
 
@@ -393,7 +402,8 @@ const char* radix_sort_last_error() { return g_why; }
 template <typename K>
 hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, size_t n, int begin_bit, int end_bit, hipStream_t st,
-                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev, size_t n_hint) {
+                            bool first_counts_ready, const uint32_t* unit_len, const uint32_t* n_dev, size_t n_hint,
+                            uint2* bounds) {
     const int bits = end_bit - begin_bit;
     if (n == 0) return hipSuccess;
     g_why = "";
@@ -447,7 +457,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                                     : rs <= 8 ? k_rs_scatter<K, 8, 8, 4>
                                               : k_rs_scatter<K, kMaxRounds, 8, 4>));
         scatter<<<units, 64 * sw, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift, dbits, rs, s.offsets, units,
-                                               s.totals, p == 0 ? unit_len : nullptr, n_dev);
+                                               s.totals, p == 0 ? unit_len : nullptr, n_dev, last ? bounds : nullptr);
         ksrc = kdst;
         vsrc = vdst;
         shift += dbits;
@@ -461,10 +471,10 @@ template size_t radix_sort_temp_bytes<uint16_t>(size_t, int, size_t);
 template size_t radix_sort_temp_bytes<uint32_t>(size_t, int, size_t);
 template hipError_t radix_sort_pairs<uint16_t>(void*, size_t, const uint16_t*, uint16_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, size_t);
+                                               const uint32_t*, size_t, uint2*);
 template hipError_t radix_sort_pairs<uint32_t>(void*, size_t, const uint32_t*, uint32_t*, const uint32_t*, uint32_t*,
                                                size_t, int, int, hipStream_t, bool, const uint32_t*,
-                                               const uint32_t*, size_t);
+                                               const uint32_t*, size_t, uint2*);
 template RadixPlan radix_sort_plan<uint16_t>(void*, size_t, int, int, size_t);
 template RadixPlan radix_sort_plan<uint32_t>(void*, size_t, int, int, size_t);
 

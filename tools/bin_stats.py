@@ -44,7 +44,8 @@ def main():
         raw = img[bounds_a:bounds_a + 2 * NB * 8].cpu().numpy().view(np.uint32).reshape(2, NB, 2).astype(np.int64)
         res = {}
         for ph, b in zip("AB", raw):
-            n = b[:, 1] - b[:, 0]
+            lo = np.where(b[:, 1] > 0, 0xFFFFFFFF - b[:, 0], 0)  # {~start, end} (rr_kernels.hpp)
+            n = b[:, 1] - lo
             q = {p: int(np.percentile(n, p)) for p in (50, 90, 99, 100)}
             res[ph] = dict(sum=int(n.sum()), nonempty=int((n > 0).sum()), pct=q,
                            over_2048=int((n > 2048).sum()), over_4096=int((n > 4096).sum()),
