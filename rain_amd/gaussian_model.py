@@ -607,8 +607,12 @@ class GaussianModel:
     def update_max_radii(self, radii, visibility_filter):
         """train.py:133, max_radii2D[vis] = max(max_radii2D[vis], radii[vis]), without the host sync of
         boolean-mask indexing (the same values)."""
+        P = radii.numel()
         if radii.is_cuda and radii.dtype == torch.int32 and radii.is_contiguous() \
-                and self._stats_native(radii.view(-1, 1).expand(-1, 2), visibility_filter):
+                and visibility_filter.dtype == torch.bool and visibility_filter.is_contiguous() \
+                and visibility_filter.numel() == P and self.max_radii2D.is_cuda \
+                and self.max_radii2D.dtype == torch.float32 and self.max_radii2D.is_contiguous() \
+                and self.max_radii2D.numel() == P:
             from . import _native
             _native.check_rt(_native.train_lib().rt_max_radii(
                 radii.numel(), radii.data_ptr(), visibility_filter.data_ptr(), self.max_radii2D.data_ptr(),
