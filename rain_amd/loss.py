@@ -124,10 +124,13 @@ class _FusedL1SSIM(torch.autograd.Function):
         ctx.save_for_backward(img, gt, ws)
         ctx.lam = float(lambda_dssim)
         ctx.mark_non_differentiable(parts)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for `parts` (a fill per step)
         return loss, parts
 
     @staticmethod
     def backward(ctx, grad_loss, _grad_parts):
+        if grad_loss is None:  # the loss itself not in the differentiated graph: zero gradient
+            return None, None, None
         img, gt, ws = ctx.saved_tensors
         return l1_ssim_backward(img, gt, ctx.lam, ws, grad_loss), None, None
 

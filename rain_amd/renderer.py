@@ -48,6 +48,16 @@ def _raw_path_ok(pc, pipe, override_color) -> bool:
         and pc._features_rest.shape[1] + 1 <= 16
 
 
+_ZERO_SINKS: dict = {}  # device -> [P, 3] fp32 zeros (render()'s means2D sink on the raw path)
+
+
+def _zero_sink(xyz: torch.Tensor) -> torch.Tensor:
+    z = _ZERO_SINKS.get(xyz.device)
+    if z is None or z.shape != xyz.shape or z.dtype != xyz.dtype:
+        z = _ZERO_SINKS[xyz.device] = torch.zeros_like(xyz, memory_format=torch.contiguous_format)
+    return z
+
+
 @dataclass
 class PipelineParams:
     """arguments/__init__.py:54-59."""
@@ -59,11 +69,18 @@ class PipelineParams:
 def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=1.0, override_color=None,
            low_pass=0.3):
     xyz = pc.get_xyz
-    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
-    try:
-        screenspace_points.retain_grad()
-    except Exception:
-        pass
+    raw = _raw_path_ok(pc, pipe, override_color)
+    if raw:
+        # the means2D gradient sink as a fresh leaf over a cached zero buffer (the rasterizer never
+        # reads its values): autograd hands it the backward's own gradient tensor, where the
+        # reference's `zeros_like + 0` with retain_grad() costs a fill, an add and a gradient clone
+        screenspace_points = _zero_sink(xyz).detach().requires_grad_()
+    else:
+        screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
+        try:
+            screenspace_points.retain_grad()
+        except Exception:
+            pass
 
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
     tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
@@ -73,7 +90,7 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=
         viewmatrix=viewpoint_camera.world_view_transform, projmatrix=viewpoint_camera.full_proj_transform,
         sh_degree=pc.active_sh_degree, campos=viewpoint_camera.camera_center, prefiltered=False, debug=pipe.debug,
         low_pass=low_pass)
-    if _raw_path_ok(pc, pipe, override_color):
+    if raw:
         from .fused import RasterizeRawParams
 
         rendered_image, radii, depth = RasterizeRawParams.apply(

@@ -134,6 +134,11 @@ def test_render_raw_fast_path_matches_getters_route(gpu, monkeypatch, sh_degree,
     assert vb.shape == va.shape == (P, 3)
     assert float(vb[:, 2].abs().max()) == 0.0
     assert rel_l1(vb, va) < 1e-4
+    # the raw path's sink: a fresh zero leaf per call (cached storage, never written)
+    sink = pb["viewspace_points"]
+    assert sink.is_leaf and float(sink.detach().abs().max()) == 0.0
+    again = render(cam, g, PipelineParams(), bg, low_pass=low_pass)["viewspace_points"]
+    assert again.grad is None and again is not sink
 
 
 @pytest.mark.parametrize("impl", ["foreach", "fused"])
