@@ -27,7 +27,8 @@ Extra objects on the JSON line:
                 bytes per launch from SURVEY §8(d) x the frame's measured L / V / L_eff / T / N;
                 the VALU-bound blends beside it (blend_fwd / blend_bwd) and the heaviest kernel
                 overall (step_dominant)
-  cpu_baseline  the CPU oracle (oracle/raster_oracle.c, "port") on the same frame, rank 0, N=1
+  cpu_baseline  the CPU oracle (oracle/raster_oracle.c, "port") on the same frame, timed on rank 0
+                at every N (--no-cpu-baseline skips it)
 """
 from __future__ import annotations
 
