@@ -114,19 +114,22 @@ size_t rr_backward_workspace_bytes(int P);
 
 /*
  * Forward, stage 1 (replaces Rasterizer::forward rasterizer_impl.cu:213-277):
- * preprocess every Gaussian, stable-sort visible Gaussians by depth, prefix-sum their tile
- * counts, and read back the pair counts (the one device->host sync the reference also has,
+ * preprocess every Gaussian, total their (bin, Gaussian) pair counts, choose the early-stop depth
+ * cut, and read back the pair counts (the one device->host sync the reference also has,
  * rasterizer_impl.cu:273).  Writes radii[P] (int32), *num_rendered = the reference's value (sum
  * of bounding-square tile counts, returned to Python unchanged) and *num_pairs = the pairs that
- * will actually be binned (after exact tile culling; size the binning buffer with it).
+ * will actually be binned (after exact tile culling; size the binning buffer with it).  The image
+ * buffer's per-frame block (tile ranges, counters) is reset here: render the frame (stage 2) into
+ * the same image buffer.
  */
 int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, int* radii,
                         void* geom_buffer, size_t geom_bytes, void* image_buffer, size_t image_bytes,
                         int* num_rendered, int* num_pairs, void* stream);
 
 /*
- * Forward, stage 2 (replaces rasterizer_impl.cu:279-329): expand (tile, Gaussian) pairs in
- * depth order, stable-sort them by tile, find per-tile ranges and alpha-blend every tile.
+ * Forward, stage 2 (replaces rasterizer_impl.cu:279-329): emit the (bin, Gaussian) pairs, put
+ * each bin's pairs in the reference's (depth, index) order, split them into the bin's tile lists
+ * and ranges, and alpha-blend every tile (two early-stop phases on large frames).
  * out_color [3,H,W], out_depth [1,H,W] are fully written.  `f` must carry the same flags as in
  * stage 1.
  */
@@ -382,7 +385,18 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *                         block sum the earlier block totals itself (2 launches); larger ones scan
  *                         the totals in one workgroup first (3 launches); default 512, <0 resets,
  *   "wide_bin_keys" 0/1   32-bit bin keys even when the bins fit 16 bits (default 0: only frames
- *                         with more than 65536 bins of 32x32 px use them).
+ *                         with more than 65536 bins of 32x32 px use them),
+ *   "phase_a_gather" 0/1/2  phase A (or a single-phase frame): 0 (default) windowed duplicate over
+ *                         the split scan's index-ordered list + stable bin sort; the gather path —
+ *                         one thread per Gaussian emitting its pairs, per-bin count / scan /
+ *                         scatter — over every Gaussian of the frame (1) or over the list (2),
+ *   "phase_b_gather" -1/0/1/2  phase B: the gather path over the list (1, default) or over every
+ *                         Gaussian (2), the windowed path (0), or by the last frame's phase-B size (-1),
+ *   "sx_bucket" 0/1       per-bin order by one bucket pass + per-bucket insertion sort (default 1)
+ *                         or by 9-bit LSD passes only,
+ *   "bounds_in_sort" 0/1  windowed paths: bin runs from the bin sort's last scatter (default 1),
+ *   "early_den" n         early-stop split: phase A holds ~1/n of the pairs (default 3).
+ * Frames of more than 16384 bins always take the windowed paths.
  * Results are identical for every setting.  Unknown keys return RR_ERR_ARG. */
 int rr_set_tuning(const char* key, int value);
 /* Diagnostics: device buffer of >= 8 * 8 * tiles u32 receiving one timing record per forward-blend

@@ -106,14 +106,15 @@ struct Img {
     uint32_t* n_contrib;
     uint2* ranges;      // phase-A (or single-phase) lists; ranges_b and counters follow it
     uint2* ranges_b;    // phase-B lists of early-stop binning (all {0,0} otherwise)
-    uint32_t* counters; // [0] = phase-B pair count (device-side)
-    size_t zero_bytes;  // ranges .. open_bits: cleared before every render
+    uint32_t* counters; // [0] phase-B pairs, [1] backward tile order done, [2] phase-A pairs (gather path)
+    size_t zero_bytes;  // ranges .. bin_cnt_a: cleared before every render
     uint32_t* tile_max;
     uint8_t* open;      // [T] tile still open after phase A
     uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask (in the zeroed block; the phase-A blend sets it)
     uint2* bounds_a;      // [bins] phase A's (or the single phase's) bin runs (zeroed block; k_bin_bounds)
     uint2* bounds_b;      // [bins] phase B's
     uint32_t* bin_cnt;    // [bins] phase B's pair count per bin (the gather path)
+    uint32_t* bin_cnt_a;  // [bins] phase A's
     uint32_t* order;      // [T] backward blend dispatch order (heaviest tiles first)
     size_t total;
 };
@@ -125,10 +126,10 @@ Img carve_img(void* buf, int W, int H) {
     m.final_T = c.take<float>(N);
     m.n_contrib = c.take<uint32_t>(N);
     // one block, cleared before every render: ranges [T], ranges_b [T], counters [4],
-    // open_bits [ceil(T/32)], bounds_a [bins], bounds_b [bins], bin_cnt [bins]
+    // open_bits [ceil(T/32)], bounds_a [bins], bounds_b [bins], bin_cnt [bins], bin_cnt_a [bins]
     const size_t nbits = ((size_t)T + 31) / 32;
     const size_t NB = (size_t)std::max(bins_x(grid_x(W)) * bins_y(grid_y(H)), 1);
-    const size_t nz = 2 * (size_t)T + 2 + (nbits + 1) / 2 + 2 * NB + (NB + 1) / 2;
+    const size_t nz = 2 * (size_t)T + 2 + (nbits + 1) / 2 + 2 * NB + 2 * ((NB + 1) / 2);
     m.ranges = c.take<uint2>(nz);
     m.ranges_b = m.ranges ? m.ranges + T : nullptr;
     m.counters = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T) : nullptr;
@@ -136,6 +137,7 @@ Img carve_img(void* buf, int W, int H) {
     m.bounds_a = m.ranges ? m.ranges + 2 * T + 2 + (nbits + 1) / 2 : nullptr;
     m.bounds_b = m.ranges ? m.bounds_a + NB : nullptr;
     m.bin_cnt = m.ranges ? reinterpret_cast<uint32_t*>(m.bounds_b + NB) : nullptr;
+    m.bin_cnt_a = m.ranges ? m.bin_cnt + 2 * ((NB + 1) / 2) : nullptr;
     m.zero_bytes = nz * sizeof(uint2);
     m.tile_max = c.take<uint32_t>(T);
     m.open = c.take<uint8_t>(T);
@@ -154,11 +156,29 @@ Img carve_img(void* buf, int W, int H) {
 constexpr uint32_t kEarlyDen = 3, kEarlyMin = 1u << 16;
 uint32_t g_early_den = kEarlyDen, g_early_min = kEarlyMin;
 
+// Binning paths (count_pairs below).  g_a_gather: phase A by the windowed duplicate + stable bin sort
+// (0, default), by the gather path over the split scan's phase-A list (2) or over every Gaussian of
+// the frame (1, no split scan then if phase B does without it too).  g_b_gather: phase B by the
+// gather path over the phase-B list (1, default) or over every Gaussian (2), by the windowed path (0),
+// or by the last frame's phase-B size (-1).
+int g_a_gather = 0;
+int g_b_gather = 1;
+constexpr int kGatherMaxBins = 16384;  // rr_bin.hip kBinScanMax
+bool gather_bins_fit(int W, int H) { return bins_x(grid_x(W)) * bins_y(grid_y(H)) <= kGatherMaxBins; }
+// Both phases always by the gather paths: the compact binning layout (carve_bin).
+bool compact_binning(int W, int H) {
+    return g_a_gather != 0 && (g_b_gather == 1 || g_b_gather == 2) && gather_bins_fit(W, H);
+}
+
 struct Bin {
     // FIRST, so the backward finds it without knowing the pair count: the per-tile lists
     // k_sortexpand writes, 4 slots per (bin, Gaussian) pair.  The host knows only the frame's
-    // total L (the phases' split LA + LB = L stays on the device), so every pair array has a phase-A
-    // region [0, L) and a phase-B region [L, 2L) (point_list: [0, 4L) and [4L, 8L)).
+    // total L (the phases' split LA + LB = L stays on the device).  Compact layout (both phases
+    // binned by the gather paths): phase A's lists at [0, 4 LA), phase B's right after them (its
+    // base read on the device), and one region [0, L) of the pair arrays used by phase A and then
+    // again by phase B — 42 B per pair (point_list 16, keys 2, values 4 + 4 sorted, scratch 16).
+    // Otherwise every pair array has a phase-A region [0, L) and a phase-B region [L, 2L)
+    // (point_list: [0, 4L) and [4L, 8L)), plus the bin sort's arrays.
     uint32_t* point_list;
     void* keys;            // bin ids of the (bin, Gaussian) pairs
     void* keys_sorted;
@@ -171,6 +191,7 @@ struct Bin {
     void* temp;            // bin-sort scratch, shared by the two phases
     size_t temp_bytes;
     bool wide;  // 32-bit bin keys (more than 65536 bins)
+    bool compact;  // compact_binning(): see point_list
     int bits;
     uint32_t L;  // (bin, Gaussian) pairs of both phases
     size_t total;
@@ -198,34 +219,42 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     b.wide = NB > 65536 || g_wide_bin_keys;
     b.bits = std::max(1, (int)higher_msb((uint32_t)NB));  // >= 1: the duplicate windows are sort units
     b.L = (uint32_t)std::max(L, 0);
+    b.compact = compact_binning(W, H);
     const size_t n = (size_t)std::max(L, 1);
-    b.point_list = c.take<uint32_t>(8 * n + kPointListPad);
+    const size_t np = b.compact ? n : 2 * n;  // entries of each pair array
+    b.point_list = c.take<uint32_t>(4 * np + kPointListPad);
     if (b.wide) {
-        b.keys = c.take<uint32_t>(2 * n);
-        b.keys_sorted = c.take<uint32_t>(2 * n);
+        b.keys = c.take<uint32_t>(np);
+        b.keys_sorted = b.compact ? nullptr : c.take<uint32_t>(np);
     } else {
-        b.keys = c.take<uint16_t>(2 * n);
-        b.keys_sorted = c.take<uint16_t>(2 * n);
+        b.keys = c.take<uint16_t>(np);
+        b.keys_sorted = b.compact ? nullptr : c.take<uint16_t>(np);
     }
-    b.vals = c.take<uint32_t>(2 * n);
-    b.vals_sorted = c.take<uint32_t>(2 * n);
-    const PhaseHints h = phase_hints(b.L, true);
-    auto units = [&](size_t hint) {
-        return b.wide ? tile_plan<uint32_t>(nullptr, b.L, b.bits, hint).units
-                      : tile_plan<uint16_t>(nullptr, b.L, b.bits, hint).units;
-    };
-    const int ua = std::max(units(h.a), 1), ub = std::max(units(h.b), 1);
-    b.first = c.take<uint32_t>((size_t)ua + ub + 2);
-    b.unit_len = c.take<uint32_t>((size_t)ub + 1);
-    b.scr0 = c.take<uint2>(2 * n);
-    b.scr1 = c.take<uint2>(2 * n);
-    auto temp = [&](size_t hint) {
-        return b.L == 0 ? (size_t)0
-               : b.wide ? radix_sort_temp_bytes<uint32_t>(b.L, b.bits, hint)
-                        : radix_sort_temp_bytes<uint16_t>(b.L, b.bits, hint);
-    };
-    b.temp_bytes = std::max(temp(h.a), temp(h.b));
-    b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
+    b.vals = c.take<uint32_t>(np);
+    b.vals_sorted = c.take<uint32_t>(np);
+    // k_sortexpand's scratch runs: one region, used by phase A's sort-expand and then by phase B's
+    b.scr0 = c.take<uint2>(n);
+    b.scr1 = c.take<uint2>(n);
+    b.first = b.unit_len = nullptr;
+    b.temp = nullptr;
+    b.temp_bytes = 0;
+    if (!b.compact) {
+        const PhaseHints h = phase_hints(b.L, true);
+        auto units = [&](size_t hint) {
+            return b.wide ? tile_plan<uint32_t>(nullptr, b.L, b.bits, hint).units
+                          : tile_plan<uint16_t>(nullptr, b.L, b.bits, hint).units;
+        };
+        const int ua = std::max(units(h.a), 1), ub = std::max(units(h.b), 1);
+        b.first = c.take<uint32_t>((size_t)ua + ub + 2);
+        b.unit_len = c.take<uint32_t>((size_t)ub + 1);
+        auto temp = [&](size_t hint) {
+            return b.L == 0 ? (size_t)0
+                   : b.wide ? radix_sort_temp_bytes<uint32_t>(b.L, b.bits, hint)
+                            : radix_sort_temp_bytes<uint16_t>(b.L, b.bits, hint);
+        };
+        b.temp_bytes = std::max(temp(h.a), temp(h.b));
+        b.temp = c.take<char>(std::max<size_t>(b.temp_bytes, 1));
+    }
     b.total = align_up(c.off);
     return b;
 }
@@ -441,18 +470,43 @@ PreArgs pre_args(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g)
     return a;
 }
 
-// Depth cut -> split pair-count scan -> the one device->host read of the forward, over a geometry
-// buffer whose per-Gaussian arrays (splats, tiles, depth keys, block sums) are filled.  No depth
-// sort: the bins' runs are put in depth order by k_sortexpand (rr_bin.hip).
-int count_pairs(const rr_frame* f, const Geom& gm, int P, hipStream_t st, int* num_rendered, int* num_pairs) {
+// Binning paths (rr_set_tuning): phase A (or the single phase) by the gather path — one thread per
+// Gaussian emitting its pairs densely (rr_forward.hip k_dup_gather), per-bin count / scan / scatter
+// and the per-bin sort restoring (depth, index) order (rr_bin.hip launch_sortexpand_small) — or by
+// the windowed duplicate over the split scan's index-ordered lists + the stable bin sort
+// ("phase_a_gather" 0).  Phase B likewise ("phase_b_gather": 1 (default) the gather path, 0 the
+// windowed one, -1 the gather path when the last frame's phase B held at most kBGatherMax pairs:
+// the phase-B sort-expand leaves its count in mailbox word 5).  The gather paths need no split scan;
+// grids of more bins than one workgroup's count / scan holds (rr_bin.hip kBinScanMax) always take
+// the windowed path.
+constexpr uint32_t kBGatherMax = 1u << 16;
+bool phase_b_gather() {
+    if (g_b_gather >= 0) return g_b_gather != 0;
+    const Mailbox& mb = g_mailbox;
+    return mb.host && !mb.failed && __atomic_load_n(mb.host + 5, __ATOMIC_RELAXED) <= kBGatherMax;
+}
+
+// Depth cut (+ the split pair-count scan when a windowed path needs its lists) -> the one
+// device->host read of the forward, over a geometry buffer whose per-Gaussian arrays (splats, tiles,
+// depth keys, block sums) are filled.  No depth sort: the bins' runs are put in depth order by
+// k_sortexpand (rr_bin.hip).  The same launch as the depth-cut samples clears the image buffer's
+// per-frame block (im: the buffer the frame is then rendered into).
+int count_pairs(const rr_frame* f, const Geom& gm, const Img& im, int P, hipStream_t st, int* num_rendered,
+                int* num_pairs) {
     PairCountRead rd;
     uint32_t* box = pair_counts_box(gm.ft, rd);
     const bool full = (f->flags & RR_FLAG_FULL_BINNING) != 0;
+    const bool fit = gather_bins_fit(f->width, f->height);
+    // the split scan's lists: the windowed paths and the list-driven gather paths read them (it also
+    // keeps the device busy while the host reads the pair counts)
+    const bool need_lists = !fit || g_a_gather != 1 || (!full && g_b_gather != 2);
     {
         StageTimer tm(RR_STAGE_SCAN, st);
         launch_early_cut(P, gm.depth_keys, gm.tiles, gm.block_sums, gm.block_wide, full ? 1u : g_early_den,
-                         g_early_min, gm.ft, gm.temp, box, rd.seq, st);
-        launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(), st);
+                         g_early_min, gm.ft, gm.temp, box, rd.seq, reinterpret_cast<uint32_t*>(im.ranges),
+                         (int)(im.zero_bytes / sizeof(uint32_t)), st);
+        if (need_lists)
+            launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(), st);
         RR_CHECK(hipGetLastError(), "pair-count scan");
     }
     RR_STAGE_CHECK("scan");
@@ -506,35 +560,22 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
         launch_preprocess(a, st);
     }
     RR_STAGE_CHECK("preprocess");
-    return count_pairs(f, gm, P, st, num_rendered, num_pairs);
+    return count_pairs(f, gm, im, P, st, num_rendered, num_pairs);
 }
 
 }  // extern "C"
 
 namespace {
 
-// Phase B's binning: the gather path (k_duplicate_b_gather: one thread per phase-B Gaussian;
-// k_bin_count + k_bin_scan + k_bin_scatter: the pairs into their bins; k_sortexpand restoring
-// (depth, index) order — 5 launches) or the windowed duplicate + bin sort + bounds + sort-expand (8
-// launches).  Both give the same lists.  rr_set_tuning "phase_b_gather": 1 (default) the gather
-// path, 0 the windowed one, -1 the gather path when the last frame's phase B held at most
-// kBGatherMax pairs (the phase-B sort-expand leaves its count in mailbox word 5).
-int g_b_gather = 1;
 // The bins' runs from the bin sort's last scatter (default) or from a k_bin_bounds launch over the
-// sorted keys (rr_set_tuning "bounds_in_sort" 0).
+// sorted keys (rr_set_tuning "bounds_in_sort" 0); windowed paths only.
 int g_bounds_in_sort = 1;
-constexpr uint32_t kBGatherMax = 1u << 16;
-bool phase_b_gather() {
-    if (g_b_gather >= 0) return g_b_gather != 0;
-    const Mailbox& mb = g_mailbox;
-    return mb.host && !mb.failed && __atomic_load_n(mb.host + 5, __ATOMIC_RELAXED) <= kBGatherMax;
-}
 
-// Tile lists for one frame: duplicate -> bin sort -> per-bin depth order + tile lists -> blend,
-// once (single phase) or as the two phases of early-stop binning (rr_kernels.hpp BlendPhase).
-// The host knows the frame's total L only: phase A's pairs (split-scan offsets .x, [0, LA)) go to
-// region [0, L) of the pair arrays and phase B's (.y, [0, LB)) to region [L, 2L); every launch is
-// sized for L and reads its phase's count from FrameTotals (empty windows and units past it).
+// Tile lists for one frame: duplicate -> pairs into their bins -> per-bin depth order + tile lists
+// -> blend, once (single phase) or as the two phases of early-stop binning (rr_kernels.hpp
+// BlendPhase).  The host knows the frame's total L only: phase A's pairs go to region [0, L) of the
+// pair arrays and phase B's to region [L, 2L); every launch is sized for L and reads its phase's
+// count on the device (the gather paths' counters, or FrameTotals LA / LB for the windowed ones).
 template <typename K>
 int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn, const int* radii, int P, int W,
                  int H, int cull, bool early, BlendFwdArgs b, hipStream_t st) {
@@ -545,19 +586,41 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     DupArgs<K> d{};
     d.P = P; d.splats = gm.splats; d.radii = radii;
     d.gx = gx; d.gy = gy; d.cull = cull;
+    d.tiles = gm.tiles; d.depth_keys = gm.depth_keys; d.ft = gm.ft;
     const PhaseHints h = phase_hints(L, early);
-    // (the one-workgroup bin count holds up to 16384 bins: 4K frames have 8160)
-    const bool gather = early && bins_x(gx) * bins_y(gy) <= 16384 && phase_b_gather();
+    const bool fit = gather_bins_fit(W, H);
+    const bool gather_a = fit && g_a_gather;
+    const bool gather = early && fit && phase_b_gather();
+    if (bn.compact != (gather_a && (gather || !early)) && bn.compact)
+        return fail(RR_ERR_ARG, "binning path changed between carving and rendering");
+    // phase B's region of the pair arrays (compact: phase A's, dead once its sort-expand has run)
+    const uint32_t offB = bn.compact ? 0u : L;
     uint32_t* report = g_mailbox.failed ? nullptr : g_mailbox.dev;
     // phase A (or the only phase): its pairs for every tile
-    const RadixPlan pa = tile_plan<K>(bn.temp, L, bn.bits, h.a);
-    const RadixPlan pb = tile_plan<K>(bn.temp, L, bn.bits, h.b);  // phase B (early-stop binning)
+    const RadixPlan pa = bn.compact ? RadixPlan{} : tile_plan<K>(bn.temp, L, bn.bits, h.a);
+    const RadixPlan pb = bn.compact ? RadixPlan{} : tile_plan<K>(bn.temp, L, bn.bits, h.b);  // phase B
     bool starts_b = false;  // phase B's window starts computed with phase A's
+    if (gather_a) {
+        {
+            StageTimer tm(RR_STAGE_DUPLICATE, st);
+            d.keys = keys; d.vals = bn.vals; d.n_total = im.counters + 2;
+            d.n_list = &gm.ft->GA; d.idx = g_a_gather == 2 ? gm.lists.idx_a : nullptr;
+            launch_dup_gather<K>(d, false, st);
+            d.n_total = nullptr; d.idx = nullptr;
+        }
+        RR_STAGE_CHECK("duplicate (gather)");
+        {
+            StageTimer tm(RR_STAGE_RANGES, st);
+            launch_sortexpand_small<K>(P, keys, bn.vals, im.counters + 2, im.bin_cnt_a, bn.vals_sorted, gm.depth_keys,
+                                       gm.ft, gx, gy, 0u, bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1,
+                                       im.bounds_a, nullptr, st);
+        }
+        RR_STAGE_CHECK("sort-expand (gather)");
+    } else {
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
         d.n_list = &gm.ft->GA; d.idx = gm.lists.idx_a; d.off = gm.lists.off_a;
         d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L_dev = &gm.ft->LA;
-        d.zero = reinterpret_cast<uint32_t*>(im.ranges); d.nzero = (int)(im.zero_bytes / sizeof(uint32_t));
         d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
         if (early && !gather) {
             d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
@@ -581,6 +644,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
                              nullptr, st);
     }
     RR_STAGE_CHECK("sort-expand");
+    }
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = early ? kBlendPhaseA : kBlendSingle;
@@ -594,20 +658,22 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     if (gather) {
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
-            d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b;
-            d.keys = keys + L; d.vals = bn.vals + L;
+            d.keys = keys + offB; d.vals = bn.vals + offB;
             d.open_bits = im.open_bits; d.n_total = im.counters;
+            d.n_list = &gm.ft->GB; d.idx = g_b_gather == 2 ? nullptr : gm.lists.idx_b;
             if (bwd_tile_order() && !fwd_tile_order() && dup_tile_order()) {
                 d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
             }
-            launch_duplicate_b_gather<K>(d, st);
+            launch_dup_gather<K>(d, true, st);
         }
         RR_STAGE_CHECK("duplicate (phase B gather)");
         {
             StageTimer tm(RR_STAGE_RANGES, st);
-            launch_sortexpand_small<K>(P, keys + L, bn.vals + L, im.counters, im.bin_cnt, bn.vals_sorted + L,
-                                       gm.depth_keys, gm.ft, gx, gy, 4u * L, bn.point_list, im.ranges_b, im.open_bits,
-                                       bn.scr0 + L, bn.scr1 + L, im.bounds_b, report, st);
+            // phase B's tile lists right after phase A's (compact: at 4 LA, read on the device)
+            launch_sortexpand_small<K>(P, keys + offB, bn.vals + offB, im.counters, im.bin_cnt, bn.vals_sorted + offB,
+                                       gm.depth_keys, gm.ft, gx, gy, bn.compact ? 0u : 4u * L, bn.point_list,
+                                       im.ranges_b, im.open_bits, bn.scr0, bn.scr1, im.bounds_b, report, st,
+                                       bn.compact ? im.counters + 2 : nullptr);
         }
         RR_STAGE_CHECK("sort-expand (phase B gather)");
     } else {
@@ -639,7 +705,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_sortexpand<K>(L, im.counters, keys_sorted + L, bn.vals_sorted + L, gm.depth_keys, gm.ft, gx, gy,
-                             4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0 + L, bn.scr1 + L, im.bounds_b,
+                             4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0, bn.scr1, im.bounds_b,
                              g_bounds_in_sort != 0, report, st);
     }
     RR_STAGE_CHECK("sort-expand (phase B)");
@@ -1003,7 +1069,7 @@ int rr_forward_from_geometry(const rr_frame* f, const rr_camera* cam, const int*
     const Img im = carve_img(image_buffer, W, H);
     if (geom_bytes < gm.total || image_bytes < im.total) return fail(RR_ERR_CAPACITY, "scratch buffer too small");
     hipStream_t st = (hipStream_t)stream;
-    if (int rc = count_pairs(f, gm, P, st, num_rendered, num_pairs)) return rc;
+    if (int rc = count_pairs(f, gm, im, P, st, num_rendered, num_pairs)) return rc;
     const size_t need = *num_pairs > 0 ? carve_bin(nullptr, *num_pairs, W, H).total : 0;
     *binning_needed = need;
     if (binning_bytes < need) return RR_INCOMPLETE;
@@ -1124,19 +1190,21 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     RR_CHECK(hipMemcpyAsync(&ft, gm.ft, sizeof(ft), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(per.data(), gm.tiles, (size_t)P * sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
-    uint32_t nb = 0;  // phase-B pairs of the last render into this image buffer
-    RR_CHECK(hipMemcpyAsync(&nb, im.counters, 4, hipMemcpyDeviceToHost, st), "stats");
+    uint32_t cnt[4] = {0u, 0u, 0u, 0u};  // [0] phase-B pairs, [2] phase-A pairs of the gather path
+    RR_CHECK(hipMemcpyAsync(cnt, im.counters, sizeof(cnt), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipStreamSynchronize(st), "stats");
     int64_t vis = 0;
     for (const uint2& v : per) vis += v.y > 0;  // a Gaussian is visible iff its rect is non-empty (radii > 0)
     out->num_visible = vis;
     out->num_rendered = (int64_t)ft.rect;
-    out->num_pairs = (int64_t)ft.LA + ft.LB;
+    out->num_pairs = (int64_t)ft.L;
     int64_t s = 0;
     for (uint32_t v : tm) s += v;
     out->l_eff = s;
-    // phase A's pairs, and the phase-B pairs kept for the tiles phase A left open
-    out->num_binned = ft.LB > 0 ? (int64_t)ft.LA + nb : (int64_t)ft.LA;
+    // phase A's pairs, and the phase-B pairs kept for the tiles phase A left open (the binning path
+    // the frame took: the tuning in force now, as at its render)
+    const bool gather_a = g_a_gather && gather_bins_fit(W, H);
+    out->num_binned = (gather_a ? (int64_t)cnt[2] : (int64_t)ft.LA) + cnt[0];
     return RR_OK;
 }
 
@@ -1179,7 +1247,11 @@ int rr_set_tuning(const char* key, int value) {
         return RR_OK;
     }
     if (key && std::string(key) == "phase_b_gather") {
-        g_b_gather = value < 0 ? -1 : (value != 0);
+        g_b_gather = value < 0 ? -1 : (value > 2 ? 1 : value);
+        return RR_OK;
+    }
+    if (key && std::string(key) == "phase_a_gather") {
+        g_a_gather = value == 1 || value == 2 ? value : 0;
         return RR_OK;
     }
     if (set_tuning(key, value) != 0) return fail(RR_ERR_ARG, std::string("unknown tuning key: ") + (key ? key : "(null)"));

@@ -40,12 +40,24 @@ constexpr int kCutShift = kDepthKeyBits - 12;
 // 2^18 bins each.
 constexpr int kCutSamples = 4096;
 constexpr int kCutSamplesPerThread = kCutSamples / 1024;
+#ifndef RR_MAILBOX_RELEASE
+#define RR_MAILBOX_RELEASE 0  // 1: the sequence number as a system-scope release store (A/B builds)
+#endif
 
 // The samples {depth key, pairs} gathered by many workgroups into a dense array (one workgroup
 // gathering 16384 scattered cache lines itself took 70 us: a single CU's outstanding-miss limit).
+// The same launch clears the image buffer's per-frame block (tile ranges, counters, open bits, bin
+// runs and counts: rr_api.hip carve_img), which the gather path's first kernel already counts into.
 __global__ __launch_bounds__(256) void k_cut_sample(int ns, int stride, const uint32_t* __restrict__ keys,
-                                                    const uint2* __restrict__ tiles, uint2* __restrict__ samples) {
+                                                    const uint2* __restrict__ tiles, uint2* __restrict__ samples,
+                                                    uint32_t* __restrict__ zero, int nzero) {
     const int i = blockIdx.x * 256 + threadIdx.x;
+    const int nth = gridDim.x * 256;
+    if (zero) {  // 16-B aligned (a carved array); the tail word by word
+        const int nv = nzero >> 2;
+        for (int j = i; j < nv; j += nth) reinterpret_cast<uint4*>(zero)[j] = make_uint4(0u, 0u, 0u, 0u);
+        for (int j = 4 * nv + i; j < nzero; j += nth) zero[j] = 0u;
+    }
     if (i >= ns) return;
     const size_t idx = (size_t)i * stride;
     samples[i] = make_uint2(keys[idx], tiles[idx].x);
@@ -166,19 +178,30 @@ __global__ __launch_bounds__(1024) void k_early_cut(int ns, const uint2* __restr
             __hip_atomic_store(box + 1, rect > sat ? sat : (uint32_t)rect, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(box + 3, s_wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#if RR_MAILBOX_RELEASE
             __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+            // The host reads only the mailbox words, which the system-scope stores above write
+            // through to host memory (sc0 sc1): waiting for their completion orders them before the
+            // sequence number.  A release store here would also write back every dirty line of this
+            // XCD's L2 (buffer_wbl2: megabytes after the backward's streaming writes), which nothing
+            // the host reads needs.
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(box + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
         }
     }
 }
 
 void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
                       const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, void* temp,
-                      uint32_t* box, uint32_t seq, hipStream_t st) {
+                      uint32_t* box, uint32_t seq, uint32_t* zero, int nzero, hipStream_t st) {
     if (P <= 0) return;
     const int stride = std::max(1, (P + kCutSamples - 1) / kCutSamples);
     const int ns = (P + stride - 1) / stride;
     uint2* samples = static_cast<uint2*>(temp);
-    k_cut_sample<<<(ns + 255) / 256, 256, 0, st>>>(ns, stride, keys, tiles, samples);
+    k_cut_sample<<<std::max((ns + 255) / 256, zero ? std::min((nzero / 4 + 255) / 256, 64) : 0), 256, 0, st>>>(
+        ns, stride, keys, tiles, samples, zero, nzero);
     k_early_cut<<<1, 1024, 0, st>>>(ns, samples, block_sums, block_wide, (P + 255) / 256, den, min_pairs, ft, box,
                                     seq);
 }
@@ -488,6 +511,107 @@ __device__ __forceinline__ bool fix_ties(uint32_t len, KeyAt key_at, ValAt val_a
     return __syncthreads_or(big);
 }
 
+// Bucket sort of a run of len <= kSxCap items (depth keys kr / values vr in registers, R rounds per
+// wave as in sx_rank_chunk) into (depth key, Gaussian index) order — the reference's per-tile order —
+// in sh.k / sh.v, whatever order the run arrived in: one counting pass over kSxBuckets buckets
+// spanning the run's own key range [kmin, kmax], then each bucket (a few items) insertion-sorted by
+// one thread on (key, index).  One histogram, one scan and one scatter instead of the three 9-bit
+// LSD passes (each a histogram, a 512-digit scan and a ballot ranking), and equal depths need no
+// extra index passes.  Returns false, with nothing written to sh.k / sh.v, when a bucket holds more
+// than kSxBucketMax items (strongly clustered depths, many exact copies): the caller then sorts
+// with the LSD passes.
+constexpr int kSxBuckets = 2048;  // = the 4 x 512 per-wave digit counters of SxShared
+constexpr uint32_t kSxBucketMax = 16;
+int g_sx_bucket = 1;  // rr_set_tuning "sx_bucket"
+__device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&kr)[kSxMaxR],
+                                                const uint32_t (&vr)[kSxMaxR], int R, uint32_t len) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t wl = (uint32_t)w * 64 * R;
+    uint32_t* hist = &sh.wcnt[0][0];
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int r = 0; r < kSxMaxR; r++)
+        if (r < R && wl + (uint32_t)r * 64 + lane < len) {
+            kmin = min(kmin, kr[r]);
+            kmax = max(kmax, kr[r]);
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+    }
+    if (lane == 0) {
+        sh.wsum[w][0] = kmin;
+        sh.wsum[w][1] = kmax;
+    }
+    for (int i = t; i < kSxBuckets; i += 256) hist[i] = 0u;
+    __syncthreads();
+    kmin = min(min(sh.wsum[0][0], sh.wsum[1][0]), min(sh.wsum[2][0], sh.wsum[3][0]));
+    kmax = max(max(sh.wsum[0][1], sh.wsum[1][1]), max(sh.wsum[2][1], sh.wsum[3][1]));
+    const uint32_t span = kmax - kmin;
+    // (span >> shift) < kSxBuckets
+    const int shift = span < (uint32_t)kSxBuckets ? 0 : 32 - __clz((int)span) - 11;
+    uint32_t bk[kSxMaxR];
+#pragma unroll
+    for (int r = 0; r < kSxMaxR; r++) {
+        bk[r] = (kr[r] - kmin) >> shift;
+        if (r < R && wl + (uint32_t)r * 64 + lane < len) atomicAdd(&hist[bk[r]], 1u);
+    }
+    __syncthreads();
+    // exclusive bucket starts: thread t owns buckets [8t, 8t + 8)
+    constexpr int BPT = kSxBuckets / 256;
+    uint32_t c[BPT], sum = 0, mx = 0;
+#pragma unroll
+    for (int k = 0; k < BPT; k++) {
+        c[k] = hist[BPT * t + k];
+        sum += c[k];
+        mx = max(mx, c[k]);
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) sh.wsum[w][2] = incl;
+    if (__syncthreads_or(mx > kSxBucketMax)) return false;  // (the barrier also publishes wsum)
+    uint32_t run = incl - sum;
+    for (int i = 0; i < w; i++) run += sh.wsum[i][2];
+#pragma unroll
+    for (int k = 0; k < BPT; k++) {
+        hist[BPT * t + k] = run;
+        run += c[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSxMaxR; r++)
+        if (r < R && wl + (uint32_t)r * 64 + lane < len) {
+            const uint32_t pos = atomicAdd(&hist[bk[r]], 1u);
+            sh.k[pos] = kr[r];
+            sh.v[pos] = vr[r];
+        }
+    __syncthreads();
+    // hist[b] is now bucket b's end, hist[b - 1] its start
+    for (int b = t; b < kSxBuckets; b += 256) {
+        const uint32_t s0 = b ? hist[b - 1] : 0u, e = hist[b];
+        for (uint32_t a = s0 + 1; a < e; a++) {
+            const uint32_t k = sh.k[a], v = sh.v[a];
+            uint32_t j = a;
+            while (j > s0) {
+                const uint32_t pk = sh.k[j - 1], pv = sh.v[j - 1];
+                if (pk < k || (pk == k && (pv & BIN_ID_MASK) < (v & BIN_ID_MASK))) break;
+                sh.k[j] = pk;
+                sh.v[j] = pv;
+                j--;
+            }
+            sh.k[j] = k;
+            sh.v[j] = v;
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
 // One bin's run of `len` (bin, Gaussian) pairs in index order -> depth order -> its four tiles'
 // lists at out_base + 4 lo + b len, and the tiles' ranges.  The run is vals[lo, lo + len) or, with
 // lds_vals (len <= kSxCap), already in sh.v.  Longer runs use scr0 / scr1 at [lo, lo + len).
@@ -496,7 +620,7 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
                                                const uint32_t* __restrict__ depth_keys, bool wide, int ipasses,
                                                uint32_t out_base, uint32_t* __restrict__ point_list,
                                                uint2* __restrict__ ranges, uint2* __restrict__ scr0,
-                                               uint2* __restrict__ scr1) {
+                                               uint2* __restrict__ scr1, bool bucket) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // The depth key: 27 bits in 3 passes of 9, wider frames in 4 of 8.  A run in no particular order
     // (ipasses > 0: the phase-B pairs of the gather path) needs index order among equal depth keys:
@@ -523,7 +647,13 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
 #pragma unroll
             for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + min(wl + (uint32_t)r * 64 + lane, len - 1)];
         }
-        for (int attempt = 0;; attempt++) {
+        bool sorted = false;
+        if (bucket) {
+#pragma unroll
+            for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
+            sorted = bucket_sort_run(sh, kr, vr, R, len);  // block-uniform
+        }
+        for (int attempt = 0; !sorted; attempt++) {
             const int passes = ip + (wide ? 4 : 3);
 #pragma unroll
             for (int r = 0; r < kSxMaxR; r++) kr[r] = key_of(0, vr[r]);  // all gathers in flight
@@ -772,7 +902,8 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
                                                     uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits,
                                                     uint2* __restrict__ scr0, uint2* __restrict__ scr1,
                                                     const uint32_t* __restrict__ n_dev, uint32_t* report,
-                                                    int ipasses) {
+                                                    int ipasses, const uint32_t* __restrict__ out_base_dev,
+                                                    int bucket) {
     __shared__ SxShared sh;
     const int bgx = bins_x(gx);
     const int bin = blockIdx.x;
@@ -793,8 +924,10 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
     }
     const uint2 run = bounds[bin];  // the bin's run [lo, hi) of the bin-sorted pairs, {~lo, hi}
     const uint32_t lo = run.y ? ~run.x : 0u;
+    // out_base_dev: the lists start after the 4 slots per pair of an earlier phase (compact layout)
+    const uint32_t ob = out_base_dev ? out_base + 4u * *out_base_dev : out_base;
     sortexpand_run(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
-                   out_base, point_list, ranges, scr0, scr1);
+                   ob, point_list, ranges, scr0, scr1, bucket != 0);
 }
 
 template <typename K>
@@ -806,7 +939,8 @@ void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const u
     if (nb <= 0) return;
     if (L > 0 && !bounds_ready) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
-                                        open_bits, scr0, scr1, n_dev, n_dev ? report : nullptr, 0);
+                                        open_bits, scr0, scr1, n_dev, n_dev ? report : nullptr, 0, nullptr,
+                                        g_sx_bucket);
 }
 template void launch_sortexpand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
@@ -814,6 +948,8 @@ template void launch_sortexpand<uint16_t>(uint32_t, const uint32_t*, const uint1
 template void launch_sortexpand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
                                           uint2*, uint2*, uint2*, bool, uint32_t*, hipStream_t);
+
+void set_sx_bucket(bool on) { g_sx_bucket = on ? 1 : 0; }
 
 int index_passes(int P) {  // 9-bit passes covering the Gaussian indices [0, P)
     int b = 1;
@@ -825,7 +961,8 @@ template <typename K>
 bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
-                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st) {
+                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st,
+                             const uint32_t* out_base_dev) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0 || nb > kBinScanMax) return false;
     const int wk = sizeof(K) == 4;
@@ -833,16 +970,17 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
     k_bin_scan<<<1, 1024, 0, st>>>(nb, n_dev, bin_cnt, bounds);
     k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, vals_sorted);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
-                                        open_bits, scr0, scr1, n_dev, report, index_passes(P));
+                                        open_bits, scr0, scr1, n_dev, report, index_passes(P), out_base_dev,
+                                        g_sx_bucket);
     return true;
 }
 template bool launch_sortexpand_small<uint16_t>(int, const uint16_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
                                                 uint32_t*, uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*,
-                                                hipStream_t);
+                                                hipStream_t, const uint32_t*);
 template bool launch_sortexpand_small<uint32_t>(int, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
                                                 uint32_t*, uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*,
-                                                hipStream_t);
+                                                hipStream_t, const uint32_t*);
 
 }  // namespace rr

@@ -457,6 +457,7 @@ int set_tuning(const char* key, int value) {
     else if (k == "pair_scan_direct_blocks") set_pair_scan_direct_blocks(value);
     else if (k == "wide_bin_keys") set_wide_bin_keys(value != 0);
     else if (k == "dup_tile_order") g_dup_order = value != 0;
+    else if (k == "sx_bucket") set_sx_bucket(value != 0);
     else return 1;
     return 0;
 }

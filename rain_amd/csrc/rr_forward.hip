@@ -370,41 +370,74 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
     for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + wb] = hist[d];
 }
 
-// Phase B of few pairs (rr_bin.hip k_sortexpand_gather): one thread per phase-B Gaussian instead of
-// output-driven windows over all of phase B's ~2/3 of the pairs, most of which land on tiles phase A
-// closed.  A Gaussian whose rectangle holds no open tile is done after one record load; the others
-// count their kept (bin, Gaussian) pairs, the workgroup reserves its total with one atomic on
-// *n_total and writes them densely — in no particular order, which the per-bin sort restores.  The extra workgroup 0 computes the backward's tile order as k_duplicate's does.
-template <typename K>
-__global__ __launch_bounds__(256) void k_duplicate_b_gather(const uint32_t* __restrict__ n_dev,
-                                                            const uint32_t* __restrict__ idx,
-                                                            const Splat* __restrict__ splats,
-                                                            const int* __restrict__ radii, int gx, int gy, int cull,
-                                                            K* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                            const uint32_t* __restrict__ open_bits,
-                                                            uint32_t* __restrict__ n_total,
-                                                            const uint32_t* __restrict__ order_cost,
-                                                            uint32_t* __restrict__ order_out,
-                                                            uint32_t* __restrict__ order_flag, int order_T) {
-    if (order_out && blockIdx.x == 0) {
+// The gather path of the duplicate (rasterizer_impl.cu:59-100): one thread per Gaussian of the
+// frame instead of output-driven windows over an index-ordered pair list, so it needs no pair-offset
+// scan, no window starts and no stable bin sort after it.  Phase A (PHASE_B false; also the single
+// phase of a frame binned in one go) takes the Gaussians whose depth key is below the frame's cut
+// (FrameTotals::cut) with their every (bin, Gaussian) pair — tiles[i].x, the preprocess's count, is
+// exactly what the walk emits.  Phase B takes the others and keeps only the pairs on tiles phase A
+// left open: a Gaussian whose rectangle holds no open tile is done after one record load, the
+// others count their kept pairs with a first walk.  Each workgroup reserves its pairs with one
+// atomic on *n_total and writes them densely, in no particular order: the per-bin sort
+// (rr_bin.hip k_sortexpand) restores the reference's (depth, index) order.  The extra workgroup 0
+// of phase B computes the backward's tile order as k_duplicate's does.
+template <typename K, bool PHASE_B>
+__global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restrict__ tiles,
+                                                    const uint32_t* __restrict__ depth_keys,
+                                                    const FrameTotals* __restrict__ ft,
+                                                    const Splat* __restrict__ splats,
+                                                    const int* __restrict__ radii, int gx, int gy, int cull,
+                                                    K* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ open_bits,
+                                                    uint32_t* __restrict__ n_total,
+                                                    const uint32_t* __restrict__ order_cost,
+                                                    uint32_t* __restrict__ order_out,
+                                                    uint32_t* __restrict__ order_flag, int order_T,
+                                                    const uint32_t* __restrict__ list_n,
+                                                    const uint32_t* __restrict__ list_idx) {
+    if (PHASE_B && order_out && blockIdx.x == 0) {
         tile_order_body256(order_T, order_cost, open_bits, order_out);
         if (threadIdx.x == 0) *order_flag = (uint32_t)order_T;
         return;
     }
-    const int wb = order_out ? (int)blockIdx.x - 1 : (int)blockIdx.x;
-    const bool mask_lds = gx * gy <= 65536;
-    __shared__ uint32_t s_open[2048];
+    const int wb = (PHASE_B && order_out) ? (int)blockIdx.x - 1 : (int)blockIdx.x;
+    const bool mask_lds = PHASE_B && gx * gy <= 65536;
+    __shared__ uint32_t s_open[PHASE_B ? 2048 : 1];
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t s_base;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    bool any_open = false;
-    for (int i = t; i < (gx * gy + 31) / 32; i += 256) {
-        const uint32_t word = open_bits[i];
-        if (mask_lds) s_open[i] = word;
-        any_open = any_open || word != 0u;
+    const int s = wb * 256 + t;
+    // this thread's Gaussian and whether it is in the phase (loads first: they overlap the mask's):
+    // entry s of the phase's Gaussian list (the split scan's, in index order: dense lanes), or
+    // Gaussian s of the frame filtered by the depth cut
+    uint32_t n = 0u, g = 0u;
+    bool in_phase;
+    if (list_idx) {
+        if (s < (int)*list_n) {
+            g = list_idx[s];
+            n = tiles[g].x;
+        }
+        in_phase = n > 0u;
+    } else {
+        const uint32_t cut = ft->cut;
+        uint32_t key = 0xffffffffu;
+        g = (uint32_t)s;
+        if (s < P) {
+            n = tiles[s].x;
+            key = depth_keys[s];
+        }
+        in_phase = n > 0u && (PHASE_B ? key >= cut : key < cut);
     }
-    // phase A closed every tile (about half the bench frames): nothing to emit, no record loads
-    if (!__syncthreads_or(any_open)) return;
+    if (PHASE_B) {
+        bool any_open = false;
+        for (int i = t; i < (gx * gy + 31) / 32; i += 256) {
+            const uint32_t word = open_bits[i];
+            if (mask_lds) s_open[i] = word;
+            any_open = any_open || word != 0u;
+        }
+        // phase A closed every tile (about half the bench frames): nothing to emit, no record loads
+        if (!__syncthreads_or(any_open)) return;
+    }
     auto is_open = [&](uint32_t tile) -> bool {
         const uint32_t word = mask_lds ? s_open[tile >> 5] : open_bits[tile >> 5];
         return ((word >> (tile & 31)) & 1u) != 0;
@@ -431,36 +464,34 @@ __global__ __launch_bounds__(256) void k_duplicate_b_gather(const uint32_t* __re
         return false;
     };
     const int bgx = bins_x(gx);
-    const int s = wb * 256 + t;
-    const int P = (int)*n_dev;  // entries of the phase-B list
-    uint32_t g = 0, cnt = 0;
+    uint32_t cnt = 0;
     CullEll ell{};
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     bool live = false;
-    if (s < P) {
-        g = idx[s];
+    if (in_phase) {
         const int r = radii[g];
         const float4 A = splats[g].a;
         const float4 Bv = splats[g].b;
         asm volatile("" ::"v"(r), "v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(Bv.x), "v"(Bv.w));
         tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
-        if (x0 < x1 && y0 < y1 && rect_open(x0, y0, x1, y1)) {
+        if (x0 < x1 && y0 < y1 && (!PHASE_B || rect_open(x0, y0, x1, y1))) {
             float ccx, ccy, ccz;
             splat_conic(A, Bv, ccx, ccy, ccz);
             ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
             live = true;
         }
     }
-    // the kept pairs, in the duplicate's enumeration (bin rows, then bin columns); pass 0 counts,
-    // pass 1 writes
-    auto walk = [&](bool emit, uint32_t pos) {
+    // the kept pairs, in the duplicate's enumeration (bin rows, then bin columns); phase B: pass 0
+    // counts, pass 1 writes; phase A writes its n pairs (never more: the reservation's bound)
+    auto walk = [&](bool emit, uint32_t pos, uint32_t cap) {
         uint32_t c = 0;
-        for (int Y = y0 >> 1; Y < (y1 + 1) >> 1; Y++) {
+        for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && c < cap; Y++) {
             int l0, h0, l1, h1, Xa, Xb;
             bin_row_spans(ell, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
             bin_cols(l0, h0, l1, h1, Xa, Xb);
-            for (int X = Xa; X < Xb; X++) {
-                const uint32_t m = bin_mask(X, l0, h0, l1, h1) & open4(X, Y);
+            for (int X = Xa; X < Xb && c < cap; X++) {
+                uint32_t m = bin_mask(X, l0, h0, l1, h1);
+                if (PHASE_B) m &= open4(X, Y);
                 if (!m) continue;
                 if (emit) {
                     keys[pos + c] = (K)(Y * bgx + X);
@@ -471,7 +502,7 @@ __global__ __launch_bounds__(256) void k_duplicate_b_gather(const uint32_t* __re
         }
         return c;
     };
-    if (live) cnt = walk(false, 0u);
+    if (live) cnt = PHASE_B ? walk(false, 0u, 0xffffffffu) : n;
     // the workgroup's kept pairs: wave prefix sums, one reservation
     uint32_t incl = cnt;
 #pragma unroll
@@ -490,7 +521,16 @@ __global__ __launch_bounds__(256) void k_duplicate_b_gather(const uint32_t* __re
     if (tot == 0) return;  // block-uniform
     if (t == 0) s_base = atomicAdd(n_total, tot);
     __syncthreads();
-    if (cnt) walk(true, s_base + pre + incl - cnt);
+    if (cnt) {
+        const uint32_t pos = s_base + pre + incl - cnt;
+        // phase A: the walk and the preprocess's count are the same closed form on the same record
+        // (rr_preprocess.hpp); should they ever disagree, the reserved slots left over get an empty
+        // tile mask, which the per-bin split writes to no tile list
+        for (uint32_t c = walk(true, pos, cnt); c < cnt; c++) {
+            keys[pos + c] = (K)0;
+            vals[pos + c] = g;
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
@@ -554,15 +594,23 @@ template bool launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
 template bool launch_duplicate<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
 
 template <typename K>
-void launch_duplicate_b_gather(const DupArgs<K>& d, hipStream_t st) {
+void launch_dup_gather(const DupArgs<K>& d, bool phase_b, hipStream_t st) {
     if (d.P == 0) return;
+    if (!phase_b) {
+        k_dup_gather<K, false><<<blocks_for(d.P), 256, 0, st>>>(d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii,
+                                                                 d.gx, d.gy, d.cull, d.keys, d.vals, nullptr,
+                                                                 d.n_total, nullptr, nullptr, nullptr, 0,
+                                                                 d.idx ? d.n_list : nullptr, d.idx);
+        return;
+    }
     const bool ord = d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
-    k_duplicate_b_gather<K><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
-        d.n_list, d.idx, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits, d.n_total,
-        ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T);
+    k_dup_gather<K, true><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
+        d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits,
+        d.n_total, ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T,
+        d.idx ? d.n_list : nullptr, d.idx);
 }
-template void launch_duplicate_b_gather<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
-template void launch_duplicate_b_gather<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
+template void launch_dup_gather<uint16_t>(const DupArgs<uint16_t>&, bool, hipStream_t);
+template void launch_dup_gather<uint32_t>(const DupArgs<uint32_t>&, bool, hipStream_t);
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;

@@ -188,9 +188,11 @@ constexpr int kPairScanDirectBlocks = 512;
 void set_pair_scan_direct_blocks(int nb);
 int pair_scan_direct_blocks();
 // rr_bin.hip: the depth-sort-free binning
+// zero (optional): nzero words cleared by the same launch (the image buffer's per-frame block)
 void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
                       const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, void* temp,
-                      uint32_t* box, uint32_t seq, hipStream_t st);  // temp: split_scan_temp_bytes(P)
+                      uint32_t* box, uint32_t seq, uint32_t* zero, int nzero,
+                      hipStream_t st);  // temp: split_scan_temp_bytes(P)
 // The phases' Gaussian lists (PhaseLists, ft->GA / GB entries); the last thread publishes {LA, rect,
 // seq, wide, LB} to box (may be null) and ft.  temp: split_scan_temp_bytes(P)
 size_t split_scan_temp_bytes(int P);
@@ -211,7 +213,8 @@ template <typename K>
 bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
-                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st);
+                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st,
+                             const uint32_t* out_base_dev = nullptr);  // lists at out_base + 4 * *out_base_dev
 template <typename K>
 struct DupArgs {
     int P;                       // capacity of the lists (the frame's Gaussians)
@@ -255,14 +258,22 @@ struct DupArgs {
     const uint32_t* n_list_b;
     const uint32_t* off_b;
     bool starts_done;
+    // the gather path (launch_dup_gather): every Gaussian's {pairs, rect tiles}, depth key, and the
+    // frame's depth cut (FrameTotals::cut) choose the phase's Gaussians; n_total receives the
+    // phase's pair count (zero on entry)
+    const uint2* tiles;
+    const uint32_t* depth_keys;
+    const FrameTotals* ft;
 };
 // returns whether the window starts (both sets) were computed
 template <typename K>
 bool launch_duplicate(const DupArgs<K>& d, hipStream_t st);
-// phase B of few pairs: one thread per phase-B Gaussian (d.n_list / d.idx), kept pairs written densely
-// and unordered at d.keys / d.vals, their count in *d.n_total (rr_forward.hip k_duplicate_b_gather)
+// the gather path: one thread per Gaussian of the phase — entry of the split scan's list (d.idx, with
+// d.n_list entries) or, with d.idx null, every Gaussian of the frame (d.P) filtered by the depth cut —
+// the phase's pairs (phase A: every pair; phase B: pairs on open tiles only) written densely and
+// unordered at d.keys / d.vals, their count added to *d.n_total (rr_forward.hip k_dup_gather)
 template <typename K>
-void launch_duplicate_b_gather(const DupArgs<K>& d, hipStream_t st);
+void launch_dup_gather(const DupArgs<K>& d, bool phase_b, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
@@ -338,4 +349,5 @@ void set_fwd_trace(void* dev_buf);
 void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
+void set_sx_bucket(bool on);  // rr_bin.hip: per-bin bucket sort (default) or LSD passes only
 }  // namespace rr

@@ -265,18 +265,21 @@ class RasterizeRawParams(torch.autograd.Function):
         color, radii, depth, st = forward_params((xyz, f_dc, f_rest, opacity, scaling, rotation), sh_degree, W, H,
                                                  tanfovx, tanfovy, viewmatrix, projmatrix, campos, bg, low_pass,
                                                  scale_modifier)
-        ctx.st = st
+        # the parameters as saved tensors (the reference saves its inputs, __init__.py:85-87): autograd's
+        # version check then rejects a backward after they were modified in place
+        ctx.save_for_backward(xyz, f_dc, f_rest, opacity, scaling, rotation)
+        ctx.st = st  # scratch buffers: held until the graph is freed (a retained graph's second backward)
         ctx.mark_non_differentiable(radii, depth)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for radii / depth (two fills)
         return color, radii, depth
 
     @staticmethod
     def backward(ctx, grad_color, _grad_radii, _grad_depth):
+        ctx.saved_tensors  # noqa: B018 — raises if a parameter changed in place since the forward
         st = ctx.st
         if grad_color is None:  # the image unused by the loss (materialize_grads off)
             grad_color = torch.zeros((3, st.frame.height, st.frame.width), dtype=torch.float32,
                                      device=st.keep[1][0].device)
-        ctx.st = None
         _keep, p = st.keep  # kernel order: xyz, f_dc, opacity, scaling, rotation, f_rest
         grads = dict(xyz=torch.empty_like(p[0]), f_dc=torch.empty_like(p[1]), opacity=torch.empty_like(p[2]),
                      scaling=torch.empty_like(p[3]), rotation=torch.empty_like(p[4]), f_rest=torch.empty_like(p[5]))

@@ -600,8 +600,9 @@ class GaussianModel:
         """The statistics arrays and inputs in the layout the native kernels take."""
         P = g.shape[0]
         return (g.dtype == torch.float32 and g.dim() == 2 and g.shape[1] >= 2 and g.stride(1) == 1
-                and mask.dtype == torch.bool and mask.is_contiguous() and mask.numel() == P
-                and all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == P
+                and g.stride(0) >= 2 and mask.dtype == torch.bool and mask.is_contiguous() and mask.numel() == P
+                and mask.device == g.device
+                and all(t.device == g.device and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == P
                         for t in (self.xyz_gradient_accum, self.denom, self.max_radii2D)))
 
     def update_max_radii(self, radii, visibility_filter):
@@ -610,7 +611,8 @@ class GaussianModel:
         P = radii.numel()
         if radii.is_cuda and radii.dtype == torch.int32 and radii.is_contiguous() \
                 and visibility_filter.dtype == torch.bool and visibility_filter.is_contiguous() \
-                and visibility_filter.numel() == P and self.max_radii2D.is_cuda \
+                and visibility_filter.numel() == P and visibility_filter.device == radii.device \
+                and self.max_radii2D.device == radii.device \
                 and self.max_radii2D.dtype == torch.float32 and self.max_radii2D.is_contiguous() \
                 and self.max_radii2D.numel() == P:
             from . import _native

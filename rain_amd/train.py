@@ -216,9 +216,14 @@ class Trainer:
         # parameters it has just stepped (rain_amd.fused.prepare_next / include/rain_raster.h
         # rr_next_frame); step s+1 then renders from that geometry.  Step s+1's view, learning rate,
         # SH degree and low-pass are decided at step s (after s's optimizer block is built), in the
-        # order the unfused step would decide them.
+        # order the unfused step would decide them.  So with fuse_next the Trainer's own state (the
+        # view sampler's position, the next step's learning rate and low-pass) is one step ahead of
+        # the last completed step: a checkpoint taken between steps records step s+1's decisions.
+        # The precomputed geometry itself is dropped if the parameters change between the steps
+        # (replaced tensors, or in-place edits such as a manual reset or a checkpoint restore: the
+        # tensors' version counters), and step s+1 then preprocesses normally.
         self.fuse_next = True
-        self._pending = None  # (iteration, view index, camera, low_pass, NextFrame or None)
+        self._pending = None  # (iteration, view index, camera, low_pass, NextFrame or None, params signature)
         self._shard = None
         # the fused step on N > 1 ranks (or a forced exchange): Gaussian-sharded, view-parallel
         # (rain_amd/sharded.py); the autograd step keeps the replicated gradient exchange
@@ -352,6 +357,11 @@ class Trainer:
             self.sync_densify_stats()
             self.sync_optimizer_state()
 
+    def _params_signature(self):
+        """Identity and in-place version of every parameter tensor (the fused backward's own
+        in-place Adam writes go through raw pointers and leave the versions unchanged)."""
+        return tuple((p.data_ptr(), p._version) for p in self.g.params())
+
     def _step_fused(self, iteration: int, sync_loss: bool) -> StepInfo:
         from . import fused
         from .loss import l1_ssim_forward_backward
@@ -364,9 +374,10 @@ class Trainer:
         g, opt = self.g, self.opt
         pend, self._pending = self._pending, None
         if pend is not None and pend[0] == iteration:  # decided (and maybe preprocessed) by step s-1
-            _it, vidx, cam, self.low_pass, nxt = pend
-            if nxt is not None and (nxt.P != g.get_xyz.shape[0] or nxt.frame.D != g.active_sh_degree):
-                nxt = None  # the model changed since (cannot happen inside step(); defensive)
+            _it, vidx, cam, self.low_pass, nxt, sig = pend
+            if nxt is not None and (nxt.P != g.get_xyz.shape[0] or nxt.frame.D != g.active_sh_degree
+                                    or sig != self._params_signature()):
+                nxt = None  # the parameters changed since step s-1's backward preprocessed this frame
         else:
             vidx, cam = self._low_pass_and_view(iteration)
             nxt = None
@@ -401,7 +412,7 @@ class Trainer:
             low_pass_now = self.low_pass
             vidx1, cam1 = self._low_pass_and_view(iteration + 1)
             next_frame = fused.prepare_next(g, cam1, self.background, self.low_pass)
-            self._pending = (iteration + 1, vidx1, cam1, self.low_pass, next_frame)
+            self._pending = [iteration + 1, vidx1, cam1, self.low_pass, next_frame, None]
             self.low_pass = low_pass_now
         with torch.no_grad():
             cache = self._bin_cache if self.reuse_binning else None
@@ -413,6 +424,8 @@ class Trainer:
             loss, _parts, dimg = l1_ssim_forward_backward(image, gt, opt.lambda_dssim)
             fused.backward(st, dimg, grads, stats, adam=adam, next_frame=next_frame)
             densified = self._finish(iteration, flat, densify_now, reset_now, adam_done=fuse_adam)
+        if self._pending is not None:  # the parameters the pending geometry was computed from
+            self._pending[5] = self._params_signature()
         return StepInfo(loss=float(loss.item()) if sync_loss else None, num_gaussians=g.get_xyz.shape[0],
                         view=vidx, low_pass=self.low_pass, densified=densified)
 

@@ -60,6 +60,9 @@ class _LazyGT:
 
 SCENES = {
     "small": dict(P=20_000, W=160, H=120, V=6, iters=range(1, 8), expect=[False, True, False, True, False, True, False]),
+    # world 8: the same scene with 16 cameras (a step takes 8 distinct views)
+    "small8": dict(P=20_000, W=160, H=120, V=16, iters=range(1, 8),
+                   expect=[False, True, False, True, False, True, False]),
     # c2f on, cameras of two image sizes: the low-pass value of a step must be the same
     # on every rank; 1000 Gaussians so that the schedule's H*W / N / 9pi exceeds its 0.3 floor
     # (160x120: 0.68, 128x96: 0.43)
@@ -79,7 +82,7 @@ def _c2f(name):
 def _opt(name):
     from rain_amd.gaussian_model import OptimizationParams
 
-    if name in ("small", "mixed"):
+    if name in ("small", "small8", "mixed"):
         o = OptimizationParams(densify_from_iter=1, densification_interval=2, opacity_reset_interval=3)
         o.densify_grad_threshold = 2e-5  # some clones / splits at this tiny scale
         return o
@@ -101,7 +104,7 @@ def _scene(dev, name):
     g = GaussianModel(3, divide_ratio=0.8, device=dev)
     p = synthetic.random_gaussians(P, sh_degree=3, seed=6, bench=True)
     gen = torch.Generator().manual_seed(1)
-    if name in ("small", "mixed"):
+    if name in ("small", "small8", "mixed"):
         gts = [torch.rand(3, int(c.image_height), int(c.image_width), generator=torch.Generator().manual_seed(20 + i))
                .to(dev) for i, c in enumerate(cams)]
         p["scaling"] = p["scaling"] + 0.3 * torch.randn(p["scaling"].shape, generator=gen)
@@ -270,10 +273,18 @@ def test_view_sharded_fused_step_four_ranks(tmp_path):
     _run(tmp_path, 4, "small")
 
 
-@pytest.mark.parametrize("world", [2, 4])
+def test_view_sharded_fused_step_eight_ranks(tmp_path):
+    """World 8, the node size of BASELINE configs[3] / [4]: eight gloo processes on one GPU, Q = 2560
+    owned rows per rank, 7 peers in every all-to-all; replicas bit-identical and equal to one
+    process summing the same 8 views."""
+    _run(tmp_path, 8, "small8")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_view_sharded_fused_step_cfg4_size(tmp_path, world):
     """BASELINE configs[3]'s workload (1M Gaussians, 200 cameras, 1080p) through the sharded step,
-    including a densify at size (1M -> 2M) and ordinary steps after it."""
+    including a densify at size (1M -> 2M) and ordinary steps after it; at world 8 the partition
+    the driver's 8-GPU run uses (Q = 125,184 rows per rank before the densify)."""
     r0 = _run(tmp_path, world, "cfg4")
     assert r0["xyz"].shape[0] == 2_000_000
 

@@ -1,0 +1,78 @@
+#!/bin/bash
+# One parameterised GPU lease script (run through gpurun); replaces the per-experiment
+# tools/gpu_r0*.sh scripts of rounds 3-4.  Steps run in order, each under its own time limit; the
+# first failing step ends the call (no GPU step runs after a failure).
+#
+#   bash tools/gpu_run.sh TAG STEP [STEP ...]
+#
+# STEP is one of
+#   smoke                 __graft_entry__.smoke()
+#   tests[=EXPR]          pytest -m gpu (EXPR: a -k expression)
+#   bench[=ARGS]          python bench.py ARGS (default: the driver's command line)
+#   ab=T1,T2[,..]         interleaved A/B of the training step (tools/variant_step.py), two rounds;
+#                         Ti = a list of rr_set_tuning key=value (or variant_step.py --options)
+#                         joined by '+', or 'base'
+#   abv=V1,V2[,..]        the same over librain_raster.so variants (tools/build_variant.py names)
+#   prof                  rocprofv3 kernel trace + stats of the default bench, timed-window summary
+#   pmc                   PMC passes (tools/profile_round.sh without the trace) -> pmc_traffic.json
+# Output: gpurun_out/TAG_*.
+set -o pipefail
+TAG=$1; shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+for STEP in "$@"; do
+  case "$STEP" in
+    smoke)
+      timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+        > ${OUT}_smoke.log 2>&1 || { tail -20 ${OUT}_smoke.log; exit 1; }
+      tail -2 ${OUT}_smoke.log ;;
+    tests|tests=*)
+      K=""; [ "$STEP" != tests ] && K="-k ${STEP#tests=}"
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K \
+        > ${OUT}_gpu_tests.log 2>&1; rc=$?; tail -3 ${OUT}_gpu_tests.log
+      [ $rc -eq 0 ] || { grep -E "FAIL|Error|error" ${OUT}_gpu_tests.log | head -30; exit $rc; } ;;
+    bench|bench=*)
+      A="--gpus 1 --steps 20 --warmup 5"; [ "$STEP" != bench ] && A="${STEP#bench=}"
+      timeout -k 10 600 python3 bench.py $A > ${OUT}_bench.json 2> ${OUT}_bench.err \
+        || { tail -20 ${OUT}_bench.err; exit 1; }
+      cat ${OUT}_bench.json ;;
+    ab=*)
+      IFS=',' read -ra VS <<< "${STEP#ab=}"
+      for r in 1 2; do
+        for v in "${VS[@]}"; do
+          TUNE=""
+          if [ "$v" != base ]; then
+            IFS='+' read -ra KV <<< "$v"
+            for kv in "${KV[@]}"; do
+              case "$kv" in -*) TUNE="$TUNE $kv" ;; *) TUNE="$TUNE --tune $kv" ;; esac
+            done
+          fi
+          timeout -k 10 300 python3 -u tools/variant_step.py --tag="$v" $TUNE >> ${OUT}_ab.jsonl 2>> ${OUT}_ab.err \
+            || { tail -20 ${OUT}_ab.err; exit 1; }
+        done
+      done
+      cat ${OUT}_ab.jsonl ;;
+    abv=*)
+      IFS=',' read -ra VS <<< "${STEP#abv=}"
+      for r in 1 2; do
+        for v in "${VS[@]}"; do
+          LIB=""; [ "$v" != base ] && LIB=gpurun_variants/$v.so
+          RAIN_RASTER_LIB=$LIB timeout -k 10 300 python3 -u tools/variant_step.py --tag="$v" >> ${OUT}_ab.jsonl \
+            2>> ${OUT}_ab.err || { tail -20 ${OUT}_ab.err; exit 1; }
+        done
+      done
+      cat ${OUT}_ab.jsonl ;;
+    prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${OUT}_prof -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline > ${OUT}_prof_bench.json 2> ${OUT}_prof.err \
+        || { tail -20 ${OUT}_prof.err; exit 1; }
+      python3 tools/step_breakdown.py ${OUT}_prof --window > ${OUT}_timed_kernels.txt 2>&1
+      python3 tools/step_breakdown.py ${OUT}_prof --window --seq | tail -40 > ${OUT}_launch_sequence.txt 2>&1
+      head -32 ${OUT}_timed_kernels.txt; cat ${OUT}_launch_sequence.txt ;;
+    pmc)
+      bash tools/profile_round.sh ${OUT}_pmcdir pmc-only || exit 1
+      head -60 ${OUT}_pmcdir/pmc_traffic.json ;;
+    *) echo "unknown step $STEP"; exit 2 ;;
+  esac
+done

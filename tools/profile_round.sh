@@ -4,13 +4,15 @@
 #   2. three counter passes over tools/pmc_workload.py (FETCH_SIZE, WRITE_SIZE, SQ VALU activity),
 #      each in its own run with --kernel-trace only (no sys/runtime tracing with --pmc)
 #   3. tools/pmc_traffic.py -> profiles/pmc_traffic.json
-# Usage: bash tools/profile_round.sh gpurun_out/prof_rNN
+# Usage: bash tools/profile_round.sh gpurun_out/prof_rNN [pmc-only]
 set -e -o pipefail
 OUT=${1:-gpurun_out/prof}
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p "$OUT"
+if [ "$2" != pmc-only ]; then
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/bench" -o run --output-format csv \
     -- python3 bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"
+fi
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \
     -- python3 tools/pmc_workload.py > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \

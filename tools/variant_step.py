@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--api", action="store_true", help="also time the reference-API step (Trainer(fused=False))")
     ap.add_argument("--pack", action="store_true", help="parameters and moments in three flat buffers (pack_flat_state)")
     ap.add_argument("--tune", action="append", default=[], help="rr_set_tuning key=value (repeatable)")
+    ap.add_argument("--no-fuse-next", action="store_true",
+                    help="the next frame's preprocess as its own launch (Trainer.fuse_next = False)")
     ap.add_argument("--loss-split", action="store_true",
                     help="the trainer's loss as two calls (forward, backward) instead of rl_l1_ssim_forward_backward")
     a = ap.parse_args()
@@ -62,6 +64,8 @@ def main():
     opt = OptimizationParams()
     g.training_setup(opt)
     tr = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(seed=0), scene_extent=4.4)
+    if a.no_fuse_next:
+        tr.fuse_next = False
     if a.pack:
         g.optimizer.fused_step(g)  # creates the moment state the packing moves
         g.pack_flat_state(1)
