@@ -502,11 +502,15 @@ int count_pairs(const rr_frame* f, const Geom& gm, const Img& im, int P, hipStre
     const bool need_lists = !fit || g_a_gather != 1 || (!full && g_b_gather != 2);
     {
         StageTimer tm(RR_STAGE_SCAN, st);
+        // the image buffer's per-frame block is cleared by the split scan's first launch (many
+        // workgroups) or, without a split scan, by the depth-cut kernel
+        uint32_t* zero = reinterpret_cast<uint32_t*>(im.ranges);
+        const int nzero = (int)(im.zero_bytes / sizeof(uint32_t));
         launch_early_cut(P, gm.depth_keys, gm.tiles, gm.block_sums, gm.block_wide, full ? 1u : g_early_den,
-                         g_early_min, gm.ft, gm.temp, box, rd.seq, reinterpret_cast<uint32_t*>(im.ranges),
-                         (int)(im.zero_bytes / sizeof(uint32_t)), st);
+                         g_early_min, gm.ft, gm.temp, box, rd.seq, need_lists ? nullptr : zero, nzero, st);
         if (need_lists)
-            launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(), st);
+            launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(), zero,
+                              nzero, st);
         RR_CHECK(hipGetLastError(), "pair-count scan");
     }
     RR_STAGE_CHECK("scan");

@@ -107,6 +107,29 @@ __device__ __forceinline__ void put(float* grad, size_t e, float g) {
     if (grad) grad[e] = g;
 }
 
+// Stores of the optimizer state (parameters and moments: read again only by the next step's
+// kernel).  RR_GB_WT builds write them through with sc1 vector stores (the line leaves the XCD's
+// L2 instead of staying dirty there until the kernel-end write-back) — an A/B variant.
+#ifndef RR_GB_WT
+#define RR_GB_WT 0
+#endif
+typedef float gb_v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_state(float* p, float v) {
+#if RR_GB_WT
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void st_state4(float* p, float4 v) {
+#if RR_GB_WT
+    const gb_v4f w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+#else
+    *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+
 // Adam over n elements whose (param, moment) addresses are given: all loads first, then the
 // math, then the stores (the compiler cannot batch them itself: the arrays may alias).
 template <int N>
@@ -123,9 +146,9 @@ __device__ __forceinline__ void adam_batch(float* const (&pp)[N], float* const (
     for (int i = 0; i < N; i++) adam_elem(p[i], g[i], m[i], v[i], c[i]);
 #pragma unroll
     for (int i = 0; i < N; i++) {
-        *pp[i] = p[i];
-        *mp[i] = m[i];
-        *vp[i] = v[i];
+        st_state(pp[i], p[i]);
+        st_state(mp[i], m[i]);
+        st_state(vp[i], v[i]);
     }
 }
 
@@ -655,9 +678,9 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                             adam_elem(p4[q].y, g4[q].y, m4[q].y, s4[q].y, c);
                             adam_elem(p4[q].z, g4[q].z, m4[q].z, s4[q].z, c);
                             adam_elem(p4[q].w, g4[q].w, m4[q].w, s4[q].w, c);
-                            reinterpret_cast<float4*>(grp->param + gb)[i] = p4[q];
-                            reinterpret_cast<float4*>(grp->exp_avg + gb)[i] = m4[q];
-                            reinterpret_cast<float4*>(grp->exp_avg_sq + gb)[i] = s4[q];
+                            st_state4(grp->param + gb + 4 * (size_t)i, p4[q]);
+                            st_state4(grp->exp_avg + gb + 4 * (size_t)i, m4[q]);
+                            st_state4(grp->exp_avg_sq + gb + 4 * (size_t)i, s4[q]);
                             if (back) {
                                 put_back(4 * i, p4[q].x);
                                 put_back(4 * i + 1, p4[q].y);
@@ -731,7 +754,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
             if (nf > 3) stage_out(a.dL_dsh_rest, ad ? &ad->f_rest : nullptr, nf - 3, 3);
         }
     }
-    if constexpr (!MULTI && KGB == 256) {
+    if constexpr (!MULTI) {
         if (back) {
             // Cross-step fusion (include/rain_raster.h rr_next_frame): the next frame's preprocess
             // (forward.cu:144-246) of this block's Gaussians on the parameters this pass has just
@@ -755,7 +778,26 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                                                       mk(row[0], row[1], row[2]), row + 3, wide);
                 }
             }
-            preprocess_block_sums(nx, blockIdx.x, c, wide);
+            if constexpr (KGB == 256) {
+                preprocess_block_sums(nx, blockIdx.x, c, wide);
+            } else {
+                // a 256-row block sum from 256 / KGB workgroups: atomic adds into the entries the
+                // launcher zeroed (launch_gauss_bwd)
+                static_assert(256 % KGB == 0, "workgroups must tile the 256-row block sums");
+                uint32_t n = c.x, r = c.y;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    n += (uint32_t)__shfl_xor((int)n, o);
+                    r += (uint32_t)__shfl_xor((int)r, o);
+                }
+                const bool wave_wide = __any(wide);
+                if (lane == 0) {
+                    const int blk = (blockIdx.x * KGB) / 256;
+                    if (n) atomicAdd(&nx.block_sums[blk].x, n);
+                    if (r) atomicAdd(&nx.block_sums[blk].y, r);
+                    if (wave_wide) atomicOr(&nx.block_wide[blk], 1u);
+                }
+            }
         }
     }
 }
@@ -818,6 +860,11 @@ void launch_pack_records(const float* gacc, const int* radii, int P, int Q, int 
 
 void launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t st) {
     if (a.P == 0) return;
+    if (kGB1 != 256 && a.has_next) {  // the next frame's block sums are accumulated atomically
+        const size_t nbs = ((size_t)a.P + 255) / 256;
+        (void)hipMemsetAsync(a.next.block_sums, 0, nbs * sizeof(uint2), st);
+        (void)hipMemsetAsync(a.next.block_wide, 0, nbs * sizeof(uint32_t), st);
+    }
     // a.M <= 16 is validated by the API: the LDS row holds at most 16 coefficients
     const int nb = (a.P + kGB1 - 1) / kGB1;
     switch (a.shs ? a.D : 0) {

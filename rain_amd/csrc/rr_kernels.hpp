@@ -197,7 +197,8 @@ void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uin
 // seq, wide, LB} to box (may be null) and ft.  temp: split_scan_temp_bytes(P)
 size_t split_scan_temp_bytes(int P);
 void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
-                       int direct_blocks, hipStream_t st);
+                       int direct_blocks, uint32_t* zero, int nzero,
+                       hipStream_t st);  // zero (optional): nzero words cleared by its first launch
 template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
@@ -305,7 +306,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
                             bool first_counts_ready = false, const uint32_t* unit_len = nullptr,
                             const uint32_t* n_dev = nullptr, size_t n_hint = 0, uint2* bounds = nullptr);
 // bounds (optional, [1 << (end_bit - begin_bit)], zero on entry): each key's run in the sorted output,
-// encoded {~start, end} (a key without items keeps {0, 0}; rr_bin.hip bin_run decodes), written by
+// encoded {~start, end} (a key without items keeps {0, 0}; rr_bin.hip k_sortexpand decodes), written by
 // the last pass's scatter
 const char* radix_sort_last_error();
 void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)

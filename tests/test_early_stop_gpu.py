@@ -25,7 +25,7 @@ def split(request, monkeypatch):
 
     N.check(N.raster().rr_set_tuning(b"phase_b_gather", 1 if request.param == "gather" else 0), "tuning")
     yield set_split
-    N.check(N.raster().rr_set_tuning(b"phase_b_gather", -1), "tuning")
+    N.check(N.raster().rr_set_tuning(b"phase_b_gather", 1), "tuning")  # the default
     N.check(N.raster().rr_set_binning_config(0, 0), "binning config")
     monkeypatch.setattr(_C, "EARLY_STOP", True)
 
