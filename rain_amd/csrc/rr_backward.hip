@@ -107,28 +107,11 @@ __device__ __forceinline__ void put(float* grad, size_t e, float g) {
     if (grad) grad[e] = g;
 }
 
-// Stores of the optimizer state (parameters and moments: read again only by the next step's
-// kernel).  RR_GB_WT builds write them through with sc1 vector stores (the line leaves the XCD's
-// L2 instead of staying dirty there until the kernel-end write-back) — an A/B variant.
-#ifndef RR_GB_WT
-#define RR_GB_WT 0
-#endif
-typedef float gb_v4f __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_state(float* p, float v) {
-#if RR_GB_WT
-    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-#else
-    *p = v;
-#endif
-}
-__device__ __forceinline__ void st_state4(float* p, float4 v) {
-#if RR_GB_WT
-    const gb_v4f w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
-#else
-    *reinterpret_cast<float4*>(p) = v;
-#endif
-}
+// Stores of the optimizer state (parameters and moments).  (Written through with sc1 vector
+// stores, so that the lines leave the XCD's L2 instead of staying dirty until the kernel-end
+// write-back, the kernel took 0.66 vs 0.37 ms: profiles/r05_gauss_bwd_variants_ab.jsonl.)
+__device__ __forceinline__ void st_state(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st_state4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // Adam over n elements whose (param, moment) addresses are given: all loads first, then the
 // math, then the stores (the compiler cannot batch them itself: the arrays may alias).
@@ -654,7 +637,10 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                                  (dst ? (uintptr_t)(dst + gb) : 0u);
             if ((al & 15u) == 0) {
                 // float4 per lane: kB / 4 vectors per batch, (param, m, v) loads all in flight
-                constexpr int kV = kB / 4 > 0 ? kB / 4 : 1;
+#ifndef RR_GB_ADAM_VEC
+#define RR_GB_ADAM_VEC (kB / 4 > 0 ? kB / 4 : 1)
+#endif
+                constexpr int kV = RR_GB_ADAM_VEC;
                 const int nv = total >> 2;
                 for (int v0 = t; v0 < nv; v0 += kV * KGB) {
                     float4 g4[kV], p4[kV], m4[kV], s4[kV];

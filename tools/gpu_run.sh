@@ -14,6 +14,7 @@
 #                         joined by '+', or 'base'
 #   abv=V1,V2[,..]        the same over librain_raster.so variants (tools/build_variant.py names)
 #   prof                  rocprofv3 kernel trace + stats of the default bench, timed-window summary
+#   stalls=PATTERN        one SQ stall-counter pass, summarised for the kernels matching PATTERN
 #   pmc                   PMC passes (tools/profile_round.sh without the trace) -> pmc_traffic.json
 # Output: gpurun_out/TAG_*.
 set -o pipefail
@@ -70,6 +71,14 @@ for STEP in "$@"; do
       python3 tools/step_breakdown.py ${OUT}_prof --window > ${OUT}_timed_kernels.txt 2>&1
       python3 tools/step_breakdown.py ${OUT}_prof --window --seq | tail -40 > ${OUT}_launch_sequence.txt 2>&1
       head -32 ${OUT}_timed_kernels.txt; cat ${OUT}_launch_sequence.txt ;;
+    stalls=*)
+      # SQ stall counters (one pass, its own run) over the bench's training step, summarised for the
+      # kernels matching the pattern (tools/pmc_stalls.py)
+      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
+        --kernel-trace -d ${OUT}_stall -o run --output-format csv -- python3 tools/pmc_workload.py \
+        > ${OUT}_stall.log 2>&1 || { tail -20 ${OUT}_stall.log; exit 1; }
+      python3 tools/pmc_stalls.py ${OUT}_stall --match "${STEP#stalls=}" | tee ${OUT}_stalls.txt ;;
     pmc)
       bash tools/profile_round.sh ${OUT}_pmcdir pmc-only || exit 1
       head -60 ${OUT}_pmcdir/pmc_traffic.json ;;
