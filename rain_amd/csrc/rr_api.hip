@@ -91,6 +91,10 @@ Geom carve_geom(void* buf, int P) {
     g.lists.off_a = c.take<uint32_t>(n);
     g.lists.idx_b = c.take<uint32_t>(n);
     g.lists.off_b = c.take<uint32_t>(n);
+    // window starts for up to 2048 * P / 16 pairs per phase (more: a window-starts launch)
+    g.lists.nwin = (uint32_t)std::min<size_t>(std::max<size_t>(n / 16, 64), (1u << 29) / kSplitWin + 1);
+    g.lists.first_a = c.take<uint32_t>(g.lists.nwin);
+    g.lists.first_b = c.take<uint32_t>(g.lists.nwin);
     g.normals = c.take<float4>(n);
     g.block_sums = c.take<uint2>((n + 255) / 256);
     g.block_wide = c.take<uint32_t>((n + 255) / 256);
@@ -574,6 +578,9 @@ namespace {
 // The bins' runs from the bin sort's last scatter (default) or from a k_bin_bounds launch over the
 // sorted keys (rr_set_tuning "bounds_in_sort" 0); windowed paths only.
 int g_bounds_in_sort = 1;
+// The windowed duplicate's window starts from the split scan's marks (default) or from a
+// window-starts launch (rr_set_tuning "split_marks" 0)
+int g_split_marks = 1;
 
 // Tile lists for one frame: duplicate -> pairs into their bins -> per-bin depth order + tile lists
 // -> blend, once (single phase) or as the two phases of early-stop binning (rr_kernels.hpp
@@ -604,6 +611,9 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     const RadixPlan pa = bn.compact ? RadixPlan{} : tile_plan<K>(bn.temp, L, bn.bits, h.a);
     const RadixPlan pb = bn.compact ? RadixPlan{} : tile_plan<K>(bn.temp, L, bn.bits, h.b);  // phase B
     bool starts_b = false;  // phase B's window starts computed with phase A's
+    // window starts marked by the split scan (units of kSplitWin pairs), else a window-starts launch
+    const bool marks_a = g_split_marks && pa.unit_items == kSplitWin && (uint32_t)pa.units <= gm.lists.nwin;
+    const bool marks_b = g_split_marks && pb.unit_items == kSplitWin && (uint32_t)pb.units <= gm.lists.nwin;
     if (gather_a) {
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
@@ -624,14 +634,16 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
         d.n_list = &gm.ft->GA; d.idx = gm.lists.idx_a; d.off = gm.lists.off_a;
-        d.first = bn.first; d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L_dev = &gm.ft->LA;
+        d.first = marks_a ? gm.lists.first_a : bn.first;
+        d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L_dev = &gm.ft->LA;
         d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
-        if (early && !gather) {
+        d.starts_done = marks_a;
+        if (early && !gather && !marks_a && !marks_b) {
             d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
             d.n_list_b = &gm.ft->GB; d.off_b = gm.lists.off_b;
         }
         starts_b = launch_duplicate<K>(d, st);
-        d.first_b = nullptr; d.nwin_b = 0;
+        d.first_b = nullptr; d.nwin_b = 0; d.starts_done = false;
     }
     RR_STAGE_CHECK("duplicate");
     {
@@ -684,7 +696,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
         d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b; d.off = gm.lists.off_b;
-        d.first = bn.first + pa.units; d.pair0 = 0; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units;
+        d.first = marks_b ? gm.lists.first_b : bn.first + pa.units;
+        d.pair0 = 0; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units;
         d.L_dev = &gm.ft->LB;
         d.keys = keys + L; d.vals = bn.vals + L; d.dbits = pb.dbits0; d.counts = pb.counts;
         d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
@@ -694,7 +707,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
             d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
         }
         d.zero = nullptr; d.nzero = 0;
-        d.starts_done = starts_b;
+        d.starts_done = starts_b || marks_b;
         launch_duplicate<K>(d, st);
     }
     RR_STAGE_CHECK("duplicate (phase B)");
@@ -1244,6 +1257,10 @@ int rr_debug_set_fwd_trace(void* dev_buf) {
 int rr_set_tuning(const char* key, int value) {
     if (key && std::string(key) == "early_den") {  // early-stop split: phase A ~1/den of the pairs
         g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
+        return RR_OK;
+    }
+    if (key && std::string(key) == "split_marks") {
+        g_split_marks = value != 0;
         return RR_OK;
     }
     if (key && std::string(key) == "bounds_in_sort") {

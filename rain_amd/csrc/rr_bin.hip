@@ -290,6 +290,14 @@ __device__ __forceinline__ void store_split(FrameTotals* ft, const Quad& q) {
     ft->GB = (uint32_t)q.cb;
 }
 
+// Entry r covers the pairs [a, b) of its phase: it is the first entry of every window of kSplitWin
+// pairs that starts in that range (the duplicate's window starts, one launch less).
+__device__ __forceinline__ void mark_windows(uint32_t* first, uint32_t nwin, unsigned long long a,
+                                             unsigned long long b, uint32_t r) {
+    for (unsigned long long k = (a + kSplitWin - 1) / kSplitWin; k * kSplitWin < b && k < nwin; k++)
+        first[k] = r;
+}
+
 template <bool PREFIX>
 __global__ __launch_bounds__(256) void k_split_scan(const uint2* __restrict__ tiles, const uint32_t* __restrict__ keys,
                                                     int P, const Quad* __restrict__ tot, PhaseLists lists,
@@ -333,9 +341,11 @@ __global__ __launch_bounds__(256) void k_split_scan(const uint2* __restrict__ ti
         if (v[k].ca) {
             lists.idx_a[e.ca] = (uint32_t)i;
             lists.off_a[e.ca] = sat32(ex.pa);
+            mark_windows(lists.first_a, lists.nwin, e.pa, ex.pa, (uint32_t)e.ca);
         } else if (v[k].cb) {
             lists.idx_b[e.cb] = (uint32_t)i;
             lists.off_b[e.cb] = sat32(ex.pb);
+            mark_windows(lists.first_b, lists.nwin, e.pb, ex.pb, (uint32_t)e.cb);
         }
     }
     // the last thread of the grid holds the frame's totals (items past P count as 0)

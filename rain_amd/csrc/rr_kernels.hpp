@@ -24,7 +24,14 @@ struct PhaseLists {
     uint32_t* off_a;
     uint32_t* idx_b;
     uint32_t* off_b;
+    // first entry of every window of kSplitWin consecutive pairs of the phase's list (window k starts
+    // inside entry first[k]'s pair range), for the first nwin windows: the windowed duplicate's
+    // starts, marked by the split scan when the bin sort's unit is kSplitWin pairs
+    uint32_t* first_a;
+    uint32_t* first_b;
+    uint32_t nwin;
 };
+constexpr uint32_t kSplitWin = 2048;
 
 struct PreArgs {
     int P, D, M, W, H, gx, gy, prefiltered;

@@ -2,7 +2,8 @@
 gives the reference's per-tile lists: phase A by the windowed duplicate + bin sort (default) or by
 the gather paths (every Gaussian / the split scan's list); phase B by the gather path over its list
 (default), over every Gaussian, or by the windowed path; per-bin order by the bucket sort (default)
-or by the LSD passes only; bin runs from the bin sort's last scatter (default) or a bounds launch.
+or by the LSD passes only; bin runs from the bin sort's last scatter (default) or a bounds launch;
+the windowed duplicate's window starts from the split scan's marks or from their own launch.
 
 For each path: the exact (depth, index) lists of the reference's 64-bit-key sort with culling and
 early stop off (tests/test_parity_gpu.py::_check_pair_order, against the oracle), the two-phase
@@ -26,6 +27,12 @@ PATHS = {
     "gather_a_list_lsd": {"phase_a_gather": (2, 0), "sx_bucket": (0, 1)},
     "windowed_b": {"phase_b_gather": (0, 1)},
     "bin_bounds_launch": {"bounds_in_sort": (0, 1)},
+    # units of kSplitWin (2048) pairs at these sizes: window starts from the split scan's marks
+    "split_marks": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16)},
+    "split_marks_windowed_b": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16),
+                               "phase_b_gather": (0, 1)},
+    "window_starts_launch": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16),
+                             "phase_b_gather": (0, 1), "split_marks": (0, 1)},
 }
 
 @pytest.fixture(params=list(PATHS))

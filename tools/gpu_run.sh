@@ -29,8 +29,8 @@ for STEP in "$@"; do
         > ${OUT}_smoke.log 2>&1 || { tail -20 ${OUT}_smoke.log; exit 1; }
       tail -2 ${OUT}_smoke.log ;;
     tests|tests=*)
-      K=""; [ "$STEP" != tests ] && K="-k ${STEP#tests=}"
-      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K \
+      K=(); [ "$STEP" != tests ] && K=(-k "${STEP#tests=}")
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
         > ${OUT}_gpu_tests.log 2>&1; rc=$?; tail -3 ${OUT}_gpu_tests.log
       [ $rc -eq 0 ] || { grep -E "FAIL|Error|error" ${OUT}_gpu_tests.log | head -30; exit $rc; } ;;
     bench|bench=*)
