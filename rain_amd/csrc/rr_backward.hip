@@ -485,6 +485,8 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                                                 float* s_gr);
 
 template <int DEG>
+// Occupancy: 3 waves per SIMD, set by LDS (a 196-B coefficient row per Gaussian, 12.5 KiB per
+// wave at either workgroup size), not by the 144 VGPRs.
 __global__ __launch_bounds__(kGB1) void k_gauss_bwd(GaussBwdArgs a) {
     __shared__ float s_sh[kGB1 * kShStride];
     gauss_bwd_block<DEG, false, kGB1>(a, nullptr, s_sh, s_sh);
@@ -649,7 +651,12 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                         const int i = min(v0 + q * KGB, nv - 1);  // clamped duplicates are not stored
                         g4[q] = make_float4(grad_at(4 * i), grad_at(4 * i + 1), grad_at(4 * i + 2), grad_at(4 * i + 3));
                         if (grp) {
+#ifdef RR_GB_TIMING_NO_PARAM_LOAD  // timing experiment only (wrong values): the parameter re-read
+                                   // (the LDS rows hold gradients by now) costs <= 5 us per step
+                            p4[q] = g4[q];
+#else
                             p4[q] = reinterpret_cast<const float4*>(grp->param + gb)[i];
+#endif
                             m4[q] = reinterpret_cast<const float4*>(grp->exp_avg + gb)[i];
                             s4[q] = reinterpret_cast<const float4*>(grp->exp_avg_sq + gb)[i];
                         }
