@@ -38,6 +38,13 @@ int rl_l1_ssim_forward_backward(const float* img, const float* gt, int C, int H,
                                 const float* window, void* workspace, size_t workspace_bytes, float* loss,
                                 float* parts, const float* grad_loss, float* dimg, void* stream);
 
+/* rl_l1_ssim_forward_backward's form: the forward + backward passes over maps in the workspace
+ * (rows = 0, default), or one band walk of `rows` output rows per block (16, 24, 32, 48 or 64) that
+ * forms the derivative maps on chip and blurs them back in the same pass (measured slower: its
+ * per-row dependency chain is twice as long).  dimg agrees between the two to float contraction and
+ * the loss to float rounding (the one-walk form sums its partials over another block partition). */
+int rl_set_fused_band(int rows);
+
 const char* rl_last_error(void);
 
 #ifdef __cplusplus

@@ -67,9 +67,10 @@ typedef struct rr_frame {
 #define RR_FLAG_RAW_PARAMS 2
 
 /* Early-stop binning (default ON for frames of >= 2^16 pairs; rr_set_binning_config): the tile
- * lists are built in two phases.  The first 1/4 of the depth-ordered pairs is binned and blended
- * for every tile; the rest is binned only for tiles with a pixel still unsaturated, and their
- * blend resumes where it stopped.  Pairs past a tile's saturation are never blended by any pixel
+ * lists are built in two phases.  The pairs of the Gaussians nearer than a per-frame depth cut
+ * (~1/3 of the pairs; rr_set_binning_config's denominator) are binned and blended for every tile;
+ * the rest are binned only for tiles with a pixel still unsaturated, and their blend resumes
+ * where it stopped.  Pairs past a tile's saturation are never blended by any pixel
  * (forward.cu:337-341; the backward walk starts at the last contributor), so images, depth and
  * gradients are those of the full lists; only the internal lists are shorter.  The flag bins
  * every pair in one phase (the pair-order tests compare full lists with the reference's). */
@@ -83,6 +84,11 @@ typedef struct rr_frame {
  * scales/rotations; set the flag on both forward stages and pass out_normal to
  * rr_forward_render_aux. */
 #define RR_FLAG_AUX_NORMAL 8
+
+/* Backward only: the workspace is the one registered with rr_set_forward_workspace before this
+ * frame's forward render (already zero-filled there; see rr_set_forward_workspace).  Without it, or
+ * when the workspace is not that registered buffer, rr_backward clears the workspace itself. */
+#define RR_FLAG_WORKSPACE_REGISTERED 16
 
 /* Camera / per-frame device arrays (reference args of the same names). */
 typedef struct rr_camera {
@@ -223,6 +229,13 @@ typedef struct rr_next_frame {
  * Backward (replaces Rasterizer::backward rasterizer_impl.cu:334-430 and the zero-filled
  * allocations of rasterize_points.cu:145-153).  dL_dpix is [3,H,W].
  */
+/* Optional: the workspace (rr_backward_workspace_bytes, 16-B aligned) of the backward that will
+ * follow the NEXT forward render on this thread.  That render zero-fills it inside its blend launch
+ * (workgroups dispatched after the tiles', in the blend's drain), and an rr_backward given the same
+ * workspace skips its own clear (one launch's worth of stores less between the loss and the blend
+ * backward, with RR_FLAG_WORKSPACE_REGISTERED).  The caller must not write the workspace in
+ * between.  NULL: drop a registration. */
+int rr_set_forward_workspace(void* workspace, size_t workspace_bytes);
 int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                 const void* geom_buffer, const void* image_buffer, const void* binning_buffer,
                 int num_rendered, const float* dL_dpix, void* workspace, size_t workspace_bytes,
@@ -395,6 +408,13 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *   "sx_bucket" 0/1       per-bin order by one bucket pass + per-bucket insertion sort (default 1)
  *                         or by 9-bit LSD passes only,
  *   "bounds_in_sort" 0/1  windowed paths: bin runs from the bin sort's last scatter (default 1),
+ *   "split_marks" 0/1     windowed duplicate: window starts marked by the split scan when the
+ *                         sort unit is 2048 pairs (default 1) or computed by their own launch,
+ *   "sx_lds_cap" n        per-bin runs of more than n pairs (1..2048, default 2048) depth-sorted
+ *                         through their own point_list region instead of LDS,
+ *   "forward_clear" 0/1   rr_set_forward_workspace registrations honoured (default 1) or dropped,
+ *   "cut_in_scan" 0/1     the early-stop depth cut computed by every workgroup of the split scan's
+ *                         first launch (default 1) or by its own one-workgroup launch,
  *   "early_den" n         early-stop split: phase A holds ~1/n of the pairs (default 3).
  * Frames of more than 16384 bins always take the windowed paths.
  * Results are identical for every setting.  Unknown keys return RR_ERR_ARG. */

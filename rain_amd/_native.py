@@ -34,6 +34,7 @@ RR_FLAG_NO_TILE_CULLING = 1
 RR_FLAG_RAW_PARAMS = 2
 RR_FLAG_FULL_BINNING = 4
 RR_FLAG_AUX_NORMAL = 8
+RR_FLAG_WORKSPACE_REGISTERED = 16
 RR_INCOMPLETE = 4  # rr_forward: stage 1 done, binning buffer too small
 
 
@@ -99,7 +100,7 @@ RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name", "rr_host_wait_stats", "rr_geometry_layout",
                   "rr_preprocess_rows", "rr_preprocess_rows_views", "rr_unpack_rows", "rr_forward_from_geometry",
                   "rr_forward_render_geometry",
-                  "rr_backward_records", "rr_gauss_backward_views"]
+                  "rr_backward_records", "rr_gauss_backward_views", "rr_set_forward_workspace"]
 
 _raster = None
 _knn = None
@@ -152,6 +153,8 @@ def raster():
         L.rr_host_wait_stats.argtypes = [ci, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         L.rr_profile_enable.restype = ci
         L.rr_profile_enable.argtypes = [ci]
+        L.rr_set_forward_workspace.restype = ci
+        L.rr_set_forward_workspace.argtypes = [vp, sz]
         L.rr_set_tuning.restype = ci
         L.rr_set_tuning.argtypes = [ctypes.c_char_p, ci]
         L.rr_debug_set_fwd_trace.restype = ci
@@ -190,7 +193,7 @@ def raster():
 
 LOSS_LIB = os.environ.get("RAIN_LOSS_LIB") or os.path.join(LIB_DIR, "librain_loss.so")
 LOSS_SYMBOLS = ["rl_workspace_bytes", "rl_l1_ssim_forward", "rl_l1_ssim_backward", "rl_l1_ssim_forward_backward",
-                "rl_last_error"]
+                "rl_set_fused_band", "rl_last_error"]
 _loss = None
 
 
@@ -201,6 +204,8 @@ def loss_lib():
         vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         L.rl_workspace_bytes.restype = ctypes.c_size_t
         L.rl_workspace_bytes.argtypes = [ci, ci, ci]
+        L.rl_set_fused_band.restype = ci
+        L.rl_set_fused_band.argtypes = [ci]
         L.rl_l1_ssim_forward.restype = ci
         L.rl_l1_ssim_forward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, ctypes.c_size_t, vp, vp, vp]
         L.rl_l1_ssim_backward.restype = ci

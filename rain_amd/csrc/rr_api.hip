@@ -180,9 +180,12 @@ struct Bin {
     // total L (the phases' split LA + LB = L stays on the device).  Compact layout (both phases
     // binned by the gather paths): phase A's lists at [0, 4 LA), phase B's right after them (its
     // base read on the device), and one region [0, L) of the pair arrays used by phase A and then
-    // again by phase B — 42 B per pair (point_list 16, keys 2, values 4 + 4 sorted, scratch 16).
+    // again by phase B — 26 B per pair (point_list 16, keys 2, values 4 + 4 sorted).
     // Otherwise every pair array has a phase-A region [0, L) and a phase-B region [L, 2L)
-    // (point_list: [0, 4L) and [4L, 8L)), plus the bin sort's arrays.
+    // (point_list: [0, 4L) and [4L, 8L)), plus the bin sort's arrays — 56 B per pair with 16-bit
+    // bin keys (point_list 32, keys 4 + 4 sorted, values 8 + 8 sorted) + ~0.5 B of sort counts.
+    // Bins of more than 2048 pairs are depth-sorted inside their own point_list region (rr_bin.hip
+    // sortexpand_run): no scratch arrays.
     uint32_t* point_list;
     void* keys;            // bin ids of the (bin, Gaussian) pairs
     void* keys_sorted;
@@ -190,8 +193,6 @@ struct Bin {
     uint32_t* vals_sorted;
     uint32_t* first;       // first Gaussian of every duplicate window (= sort unit), phase A then B
     uint32_t* unit_len;    // phase B: pairs kept per window
-    uint2* scr0;           // k_sortexpand's scratch runs for bins of more than kSxCap pairs
-    uint2* scr1;
     void* temp;            // bin-sort scratch, shared by the two phases
     size_t temp_bytes;
     bool wide;  // 32-bit bin keys (more than 65536 bins)
@@ -236,9 +237,6 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     }
     b.vals = c.take<uint32_t>(np);
     b.vals_sorted = c.take<uint32_t>(np);
-    // k_sortexpand's scratch runs: one region, used by phase A's sort-expand and then by phase B's
-    b.scr0 = c.take<uint2>(n);
-    b.scr1 = c.take<uint2>(n);
     b.first = b.unit_len = nullptr;
     b.temp = nullptr;
     b.temp_bytes = 0;
@@ -490,6 +488,10 @@ bool phase_b_gather() {
     return mb.host && !mb.failed && __atomic_load_n(mb.host + 5, __ATOMIC_RELAXED) <= kBGatherMax;
 }
 
+// The depth cut inside the split scan's first launch (default) or by k_early_cut before it
+// (rr_set_tuning "cut_in_scan" 0; always without a split scan)
+int g_cut_in_scan = 1;
+
 // Depth cut (+ the split pair-count scan when a windowed path needs its lists) -> the one
 // device->host read of the forward, over a geometry buffer whose per-Gaussian arrays (splats, tiles,
 // depth keys, block sums) are filled.  No depth sort: the bins' runs are put in depth order by
@@ -510,11 +512,18 @@ int count_pairs(const rr_frame* f, const Geom& gm, const Img& im, int P, hipStre
         // workgroups) or, without a split scan, by the depth-cut kernel
         uint32_t* zero = reinterpret_cast<uint32_t*>(im.ranges);
         const int nzero = (int)(im.zero_bytes / sizeof(uint32_t));
-        launch_early_cut(P, gm.depth_keys, gm.tiles, gm.block_sums, gm.block_wide, full ? 1u : g_early_den,
-                         g_early_min, gm.ft, gm.temp, box, rd.seq, need_lists ? nullptr : zero, nzero, st);
-        if (need_lists)
+        const uint32_t den = full ? 1u : g_early_den;
+        if (need_lists && g_cut_in_scan) {  // the cut computed by every workgroup of the scan's first launch
+            const CutArgs ca{gm.block_sums, gm.block_wide, den, g_early_min, box, rd.seq};
             launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(), zero,
-                              nzero, st);
+                              nzero, st, &ca);
+        } else {
+            launch_early_cut(P, gm.depth_keys, gm.tiles, gm.block_sums, gm.block_wide, den, g_early_min, gm.ft, gm.temp,
+                             box, rd.seq, need_lists ? nullptr : zero, nzero, st);
+            if (need_lists)
+                launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(),
+                                  zero, nzero, st);
+        }
         RR_CHECK(hipGetLastError(), "pair-count scan");
     }
     RR_STAGE_CHECK("scan");
@@ -578,6 +587,19 @@ namespace {
 // The bins' runs from the bin sort's last scatter (default) or from a k_bin_bounds launch over the
 // sorted keys (rr_set_tuning "bounds_in_sort" 0); windowed paths only.
 int g_bounds_in_sort = 1;
+// The backward's accumulator workspace: registered for the next forward render on this thread
+// (rr_set_forward_workspace), which zero-fills it inside its first blend launch and records it as
+// clean; a backward whose workspace is the clean one skips its own clear.
+struct WsRange {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+thread_local WsRange g_fwd_ws, g_ws_clean;
+// The backward's tile order of the last render, when its phase-B duplicate launch computed it
+// (its order array): the backward then needs no prologue at all once the workspace is clean.
+thread_local const uint32_t* g_order_ready = nullptr;
+int g_fwd_clear = 1;  // rr_set_tuning "forward_clear" 0: registrations are dropped (A/B)
+
 // The windowed duplicate's window starts from the split scan's marks (default) or from a
 // window-starts launch (rr_set_tuning "split_marks" 0)
 int g_split_marks = 1;
@@ -626,8 +648,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         {
             StageTimer tm(RR_STAGE_RANGES, st);
             launch_sortexpand_small<K>(P, keys, bn.vals, im.counters + 2, im.bin_cnt_a, bn.vals_sorted, gm.depth_keys,
-                                       gm.ft, gx, gy, 0u, bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1,
-                                       im.bounds_a, nullptr, st);
+                                       gm.ft, gx, gy, 0u, bn.point_list, im.ranges, nullptr, im.bounds_a, nullptr, st);
         }
         RR_STAGE_CHECK("sort-expand (gather)");
     } else {
@@ -656,8 +677,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_sortexpand<K>(L, &gm.ft->LA, keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u,
-                             bn.point_list, im.ranges, nullptr, bn.scr0, bn.scr1, im.bounds_a, g_bounds_in_sort != 0,
-                             nullptr, st);
+                             bn.point_list, im.ranges, nullptr, im.bounds_a, g_bounds_in_sort != 0, nullptr, st);
     }
     RR_STAGE_CHECK("sort-expand");
     }
@@ -666,7 +686,11 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         b.phase = early ? kBlendPhaseA : kBlendSingle;
         b.order = fwd_tile_order() ? im.order : nullptr;
         if (b.order) launch_tile_order_by_length(gx * gy, im.ranges, im.order, st);
+        // the registered backward workspace (render_frame), cleared in this launch's drain
+        if (b.clear) g_ws_clean = WsRange{b.clear, b.clear_n4 * sizeof(float4)};
         launch_blend_fwd(b, st);
+        b.clear = nullptr;
+        b.clear_n4 = 0;
     }
     RR_STAGE_CHECK("blend forward");
     if (!early) return RR_OK;
@@ -679,6 +703,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
             d.n_list = &gm.ft->GB; d.idx = g_b_gather == 2 ? nullptr : gm.lists.idx_b;
             if (bwd_tile_order() && !fwd_tile_order() && dup_tile_order()) {
                 d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
+                if (P > 0) g_order_ready = im.order;  // launch_dup_gather's extra workgroup sorts them
             }
             launch_dup_gather<K>(d, true, st);
         }
@@ -688,7 +713,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
             // phase B's tile lists right after phase A's (compact: at 4 LA, read on the device)
             launch_sortexpand_small<K>(P, keys + offB, bn.vals + offB, im.counters, im.bin_cnt, bn.vals_sorted + offB,
                                        gm.depth_keys, gm.ft, gx, gy, bn.compact ? 0u : 4u * L, bn.point_list,
-                                       im.ranges_b, im.open_bits, bn.scr0, bn.scr1, im.bounds_b, report, st,
+                                       im.ranges_b, im.open_bits, im.bounds_b, report, st,
                                        bn.compact ? im.counters + 2 : nullptr);
         }
         RR_STAGE_CHECK("sort-expand (phase B gather)");
@@ -722,8 +747,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     {
         StageTimer tm(RR_STAGE_RANGES, st);
         launch_sortexpand<K>(L, im.counters, keys_sorted + L, bn.vals_sorted + L, gm.depth_keys, gm.ft, gx, gy,
-                             4u * L, bn.point_list, im.ranges_b, im.open_bits, bn.scr0, bn.scr1, im.bounds_b,
-                             g_bounds_in_sort != 0, report, st);
+                             4u * L, bn.point_list, im.ranges_b, im.open_bits, im.bounds_b, g_bounds_in_sort != 0,
+                             report, st);
     }
     RR_STAGE_CHECK("sort-expand (phase B)");
     }
@@ -754,9 +779,16 @@ int blend_backward(const rr_frame* f, const rr_camera* cam, const void* geom_buf
     const int gx = grid_x(W), gy = grid_y(H);
     const bool blend = L > 0 && binning_buffer;
     uint32_t* order = blend && bwd_tile_order() ? im.order : nullptr;
-    {
+    // the accumulators already zero-filled by the forward (rr_set_forward_workspace): no clear
+    const size_t nacc = (size_t)P * GACC_STRIDE;
+    const bool clean = (f->flags & RR_FLAG_WORKSPACE_REGISTERED) && g_ws_clean.ptr == gacc &&
+                       g_ws_clean.bytes >= nacc * sizeof(float);
+    g_ws_clean = WsRange{};  // this backward's accumulation dirties it
+    const bool order_ready = order && g_order_ready == order;
+    if (!clean || (order && !order_ready)) {
         StageTimer tm(RR_STAGE_MEMSET, st);
-        launch_bwd_prologue(gacc, (size_t)P * GACC_STRIDE, gx * gy, im.tile_max, order, im.counters + 1, st);
+        launch_bwd_prologue(gacc, clean ? 0 : nacc, gx * gy, im.tile_max, order_ready ? nullptr : order,
+                            im.counters + 1, st);
         RR_CHECK(hipGetLastError(), "clear accumulators");
     }
     if (blend) {
@@ -807,6 +839,11 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
                  float* out_normal, void* stream) {
     const int P = f->P, W = f->width, H = f->height, L = num_pairs;
     const int cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
+    // a workspace registration is used by this render (or dropped by it) either way
+    const WsRange reg = g_fwd_clear ? g_fwd_ws : WsRange{};
+    g_fwd_ws = WsRange{};
+    g_ws_clean = WsRange{};
+    g_order_ready = nullptr;
     if (P == 0) return RR_OK;
     if (!out_color || !out_depth || !geom_buffer || !image_buffer || (L > 0 && !binning_buffer))
         return fail(RR_ERR_ARG, "null buffer");
@@ -825,6 +862,8 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
     b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.open = im.open; b.open_bits = im.open_bits;
     b.point_list = bn.point_list; b.splats = gm.splats; b.bg = cam->background;
     b.final_T = im.final_T; b.n_contrib = im.n_contrib; b.tile_max = im.tile_max;
+    b.clear = static_cast<float4*>(reg.ptr);
+    b.clear_n4 = reg.bytes / sizeof(float4);
     b.out_color = out_color; b.out_depth = out_depth;
     b.normals = out_normal ? gm.normals : nullptr; b.out_normal = out_normal;
     if (L == 0) {  // no pairs: every tile keeps the background (one blend over empty lists)
@@ -1254,9 +1293,28 @@ int rr_debug_set_fwd_trace(void* dev_buf) {
     return RR_OK;
 }
 
+int rr_set_forward_workspace(void* workspace, size_t bytes) {
+    if (workspace && (((uintptr_t)workspace & 15u) != 0 || bytes % 16 != 0))
+        return fail(RR_ERR_ARG, "workspace must be 16-byte aligned and a multiple of 16 bytes");
+    g_fwd_ws = workspace && bytes ? WsRange{workspace, bytes} : WsRange{};
+    return RR_OK;
+}
+
 int rr_set_tuning(const char* key, int value) {
     if (key && std::string(key) == "early_den") {  // early-stop split: phase A ~1/den of the pairs
         g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
+        return RR_OK;
+    }
+    if (key && std::string(key) == "cut_in_scan") {
+        g_cut_in_scan = value != 0;
+        return RR_OK;
+    }
+    if (key && std::string(key) == "sx_lds_cap") {  // runs longer than this: global sort path
+        set_sx_lds_cap(value);
+        return RR_OK;
+    }
+    if (key && std::string(key) == "forward_clear") {
+        g_fwd_clear = value != 0;
         return RR_OK;
     }
     if (key && std::string(key) == "split_marks") {

@@ -60,46 +60,58 @@ __device__ __forceinline__ void clear_words(uint32_t* __restrict__ zero, int nze
 // indices are as good a sample as evenly spaced Gaussians here: the cut only steers the split's
 // balance, any cut gives the same lists.
 constexpr int kCutChunks = kCutSamples / 64;
-__global__ __launch_bounds__(1024) void k_early_cut(int P, const uint32_t* __restrict__ keys,
-                                                    const uint2* __restrict__ tiles,
-                                                    const uint2* __restrict__ block_sums,
-                                                    const uint32_t* __restrict__ block_wide, int nb, uint32_t den,
-                                                    uint32_t min_pairs, FrameTotals* __restrict__ ft, uint32_t* box,
-                                                    uint32_t seq, uint32_t* __restrict__ zero, int nzero) {
-    __shared__ uint32_t hist[kCutBuckets];
-    __shared__ unsigned long long s_red[3][16];
-    __shared__ uint32_t s_wide, s_cut;
+
+// The frame's totals (L, rect, wide: the preprocess block sums) and the depth cut, computed by one
+// workgroup of NT threads: k_early_cut (1024 threads, alone) or every workgroup of k_cut_totals
+// (256, the split scan's first launch, each from the same inputs by the same steps: the same cut).
+template <int NT>
+struct CutShared {
+    uint32_t hist[kCutBuckets];
+    unsigned long long red[3][NT / 64];
+    uint32_t wide, cut;
+};
+struct CutResult {
+    unsigned long long L, rect;
+    uint32_t wide, cut;  // cut: all ones for a one-phase frame
+};
+template <int NT>
+__device__ __forceinline__ CutResult depth_cut(CutShared<NT>& sh, int P, const uint32_t* __restrict__ keys,
+                                               const uint2* __restrict__ tiles, const uint2* __restrict__ block_sums,
+                                               const uint32_t* __restrict__ block_wide, int nb, uint32_t den,
+                                               uint32_t min_pairs) {
+    constexpr int SPT = kCutSamples / NT;  // samples per thread
+    constexpr int QB = SPT;                // block records per thread and round (all in flight)
+    constexpr int NW = NT / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    for (int i = t; i < kCutBuckets; i += 1024) hist[i] = 0u;
+    for (int i = t; i < kCutBuckets; i += NT) sh.hist[i] = 0u;
     if (t == 0) {
-        s_wide = 0u;
-        s_cut = 0xffffffffu;
+        sh.wide = 0u;
+        sh.cut = 0xffffffffu;
     }
     // every sample load in flight before the first LDS atomic
-    uint2 sm[kCutSamplesPerThread];
+    uint2 sm[SPT];
 #pragma unroll
-    for (int r = 0; r < kCutSamplesPerThread; r++) {
-        const int s = t + r * 1024;
+    for (int r = 0; r < SPT; r++) {
+        const int s = t + r * NT;
         const int idx = P <= kCutSamples ? min(s, P - 1)
                                          : min((int)(((long long)(s >> 6) * P) / kCutChunks) + (s & 63), P - 1);
         sm[r] = make_uint2(keys[idx], tiles[idx].x);
         if (P <= kCutSamples && s >= P) sm[r].y = 0u;
     }
-    if (zero) clear_words(zero, nzero);
     unsigned long long L = 0, rect = 0, S = 0;
     uint32_t wide = 0;
-    for (int i0 = 0; i0 < nb; i0 += 4 * 1024) {  // 4 block records per thread in flight at once
-        uint2 v[4];
-        uint32_t wd[4];
+    for (int i0 = 0; i0 < nb; i0 += QB * NT) {
+        uint2 v[QB];
+        uint32_t wd[QB];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int i = min(i0 + q * 1024 + t, nb - 1);
+        for (int q = 0; q < QB; q++) {
+            const int i = min(i0 + q * NT + t, nb - 1);
             v[q] = block_sums[i];
             wd[q] = block_wide[i];
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (i0 + q * 1024 + t < nb) {
+        for (int q = 0; q < QB; q++)
+            if (i0 + q * NT + t < nb) {
                 L += v[q].x;
                 rect += v[q].y;
                 wide |= wd[q];
@@ -107,13 +119,13 @@ __global__ __launch_bounds__(1024) void k_early_cut(int P, const uint32_t* __res
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kCutSamplesPerThread; r++)
+    for (int r = 0; r < SPT; r++)
         if (sm[r].y) {
             const uint32_t n = min(sm[r].y, 1u << 18);
-            atomicAdd(&hist[min(sm[r].x >> kCutShift, (uint32_t)kCutBuckets - 1u)], n);
+            atomicAdd(&sh.hist[min(sm[r].x >> kCutShift, (uint32_t)kCutBuckets - 1u)], n);
             S += n;
         }
-    if (wide) atomicOr(&s_wide, 1u);
+    if (wide) atomicOr(&sh.wide, 1u);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         L += __shfl_xor(L, o);
@@ -121,26 +133,26 @@ __global__ __launch_bounds__(1024) void k_early_cut(int P, const uint32_t* __res
         S += __shfl_xor(S, o);
     }
     if (lane == 0) {
-        s_red[0][w] = L;
-        s_red[1][w] = rect;
-        s_red[2][w] = S;
+        sh.red[0][w] = L;
+        sh.red[1][w] = rect;
+        sh.red[2][w] = S;
     }
     __syncthreads();
     L = rect = S = 0;
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-        L += s_red[0][i];
-        rect += s_red[1][i];
-        S += s_red[2][i];
+    for (int i = 0; i < NW; i++) {
+        L += sh.red[0][i];
+        rect += sh.red[1][i];
+        S += sh.red[2][i];
     }
     const bool one_phase = den <= 1u || L < (unsigned long long)min_pairs || S == 0ull;
     if (!one_phase) {
-        // 4 buckets per thread, block-wide inclusive scan of their sums
-        constexpr int BPT = kCutBuckets / 1024;
+        // BPT buckets per thread, block-wide inclusive scan of their sums
+        constexpr int BPT = kCutBuckets / NT;
         unsigned long long v[BPT], sum = 0;
 #pragma unroll
         for (int k = 0; k < BPT; k++) {
-            v[k] = hist[BPT * t + k];
+            v[k] = sh.hist[BPT * t + k];
             sum += v[k];
         }
         unsigned long long incl = sum;
@@ -149,49 +161,64 @@ __global__ __launch_bounds__(1024) void k_early_cut(int P, const uint32_t* __res
             const unsigned long long y = __shfl_up(incl, o);
             if (lane >= o) incl += y;
         }
-        __syncthreads();  // s_red reads above are done
-        if (lane == 63) s_red[0][w] = incl;
+        __syncthreads();  // sh.red reads above are done
+        if (lane == 63) sh.red[0][w] = incl;
         __syncthreads();
         unsigned long long run = incl - sum;
-        for (int i = 0; i < w; i++) run += s_red[0][i];
+        for (int i = 0; i < w; i++) run += sh.red[0][i];
         // first bucket whose inclusive prefix reaches S / den (prefix * den >= S)
 #pragma unroll
         for (int k = 0; k < BPT; k++) {
             run += v[k];
             if (run * den >= S) {
                 const uint32_t b = (uint32_t)(BPT * t + k);
-                atomicMin(&s_cut, b + 1u >= (uint32_t)kCutBuckets ? 0xffffffffu : (b + 1u) << kCutShift);
+                atomicMin(&sh.cut, b + 1u >= (uint32_t)kCutBuckets ? 0xffffffffu : (b + 1u) << kCutShift);
                 break;
             }
         }
     }
     __syncthreads();
-    if (t == 0) {
-        ft->L = L;
-        ft->rect = rect;
-        ft->wide = s_wide;
-        ft->cut = one_phase ? 0xffffffffu : s_cut;
-        // the frame's counts to the host (rr_api.hip pair_counts_wait) now, while the split scan
-        // runs: the host sizes the binning by the total and leaves the phases' split on the device
-        if (box) {
-            const uint32_t sat = 0xffffffffu;
-            __hip_atomic_store(box + 0, L > sat ? sat : (uint32_t)L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(box + 1, rect > sat ? sat : (uint32_t)rect, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(box + 3, s_wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return CutResult{L, rect, sh.wide, one_phase ? 0xffffffffu : sh.cut};
+}
+
+// The frame's counts and cut into FrameTotals, and to the host (rr_api.hip pair_counts_wait) now,
+// while the split scan runs: the host sizes the binning by the total and leaves the phases' split
+// on the device.  One thread.
+__device__ __forceinline__ void publish_cut(const CutResult& r, FrameTotals* ft, uint32_t* box, uint32_t seq) {
+    ft->L = r.L;
+    ft->rect = r.rect;
+    ft->wide = r.wide;
+    ft->cut = r.cut;
+    if (box) {
+        const uint32_t sat = 0xffffffffu;
+        __hip_atomic_store(box + 0, r.L > sat ? sat : (uint32_t)r.L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(box + 1, r.rect > sat ? sat : (uint32_t)r.rect, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(box + 3, r.wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #if RR_MAILBOX_RELEASE
-            __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 #else
-            // The host reads only the mailbox words, which the system-scope stores above write
-            // through to host memory (sc0 sc1): waiting for their completion orders them before the
-            // sequence number.  A release store here would also write back every dirty line of this
-            // XCD's L2 (buffer_wbl2: megabytes after the backward's streaming writes), which nothing
-            // the host reads needs.
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(box + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // The host reads only the mailbox words, which the system-scope stores above write
+        // through to host memory (sc0 sc1): waiting for their completion orders them before the
+        // sequence number.  A release store here would also write back every dirty line of this
+        // XCD's L2 (buffer_wbl2: megabytes after the backward's streaming writes), which nothing
+        // the host reads needs.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(box + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
-        }
     }
+}
+
+__global__ __launch_bounds__(1024) void k_early_cut(int P, const uint32_t* __restrict__ keys,
+                                                    const uint2* __restrict__ tiles,
+                                                    const uint2* __restrict__ block_sums,
+                                                    const uint32_t* __restrict__ block_wide, int nb, uint32_t den,
+                                                    uint32_t min_pairs, FrameTotals* __restrict__ ft, uint32_t* box,
+                                                    uint32_t seq, uint32_t* __restrict__ zero, int nzero) {
+    __shared__ CutShared<1024> sh;
+    if (zero) clear_words(zero, nzero);
+    const CutResult r = depth_cut<1024>(sh, P, keys, tiles, block_sums, block_wide, nb, den, min_pairs);
+    if (threadIdx.x == 0) publish_cut(r, ft, box, seq);
 }
 
 void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
@@ -237,13 +264,25 @@ __device__ __forceinline__ Quad quad_block_sum(Quad x, Quad* s) {
     return quad_add(quad_add(s[0], s[1]), quad_add(s[2], s[3]));
 }
 
+// CUT: the depth cut computed here by every workgroup (depth_cut<256>: the same cut in each) and
+// published by workgroup 0 — k_early_cut's job without its launch; else the cut from ft.
+template <bool CUT>
 __global__ __launch_bounds__(256) void k_split_scan_totals(const uint2* __restrict__ tiles,
                                                            const uint32_t* __restrict__ keys, int P,
-                                                           const FrameTotals* __restrict__ ft, Quad* __restrict__ tot,
-                                                           uint32_t* __restrict__ zero, int nzero) {
+                                                           FrameTotals* __restrict__ ft, Quad* __restrict__ tot,
+                                                           uint32_t* __restrict__ zero, int nzero, CutArgs ca) {
     __shared__ Quad s[4];
+    __shared__ CutShared<CUT ? 256 : 64> sh;
+    uint32_t cut;
+    if constexpr (CUT) {
+        const CutResult r = depth_cut<256>(sh, P, keys, tiles, ca.block_sums, ca.block_wide, (P + 255) / 256, ca.den,
+                                           ca.min_pairs);
+        if (blockIdx.x == 0 && threadIdx.x == 0) publish_cut(r, ft, ca.box, ca.seq);
+        cut = r.cut;
+    } else {
+        cut = ft->cut;
+    }
     if (zero) clear_words(zero, nzero);
-    const uint32_t cut = ft->cut;
     const size_t b0 = (size_t)blockIdx.x * kPairScanItems;
     Quad x{0, 0, 0, 0};
 #pragma unroll
@@ -359,11 +398,14 @@ size_t split_scan_temp_bytes(int P) {
 }
 
 void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
-                       int direct_blocks, uint32_t* zero, int nzero, hipStream_t st) {
+                       int direct_blocks, uint32_t* zero, int nzero, hipStream_t st, const CutArgs* cut) {
     if (P <= 0) return;
     const int nb = (P + kPairScanItems - 1) / kPairScanItems;
     Quad* tot = static_cast<Quad*>(temp);
-    k_split_scan_totals<<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot, zero, nzero);
+    if (cut)
+        k_split_scan_totals<true><<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot, zero, nzero, *cut);
+    else
+        k_split_scan_totals<false><<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot, zero, nzero, CutArgs{});
     if (nb <= direct_blocks) {
         k_split_scan<false><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft);
     } else {
@@ -532,6 +574,8 @@ __device__ __forceinline__ bool fix_ties(uint32_t len, KeyAt key_at, ValAt val_a
 constexpr int kSxBuckets = 2048;  // = the 4 x 512 per-wave digit counters of SxShared
 constexpr uint32_t kSxBucketMax = 16;
 int g_sx_bucket = 1;  // rr_set_tuning "sx_bucket"
+int g_sx_lds_cap = kSxCap;  // rr_set_tuning "sx_lds_cap": longer runs take the global path (tests)
+uint32_t sx_lds_cap() { return (uint32_t)g_sx_lds_cap; }
 __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&kr)[kSxMaxR],
                                                 const uint32_t (&vr)[kSxMaxR], int R, uint32_t len) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -623,13 +667,15 @@ __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&k
 
 // One bin's run of `len` (bin, Gaussian) pairs in index order -> depth order -> its four tiles'
 // lists at out_base + 4 lo + b len, and the tiles' ranges.  The run is vals[lo, lo + len) or, with
-// lds_vals (len <= kSxCap), already in sh.v.  Longer runs use scr0 / scr1 at [lo, lo + len).
+// lds_vals (len <= kSxCap), already in sh.v.  Runs longer than lds_cap (<= kSxCap) are sorted
+// through global scratch: the run's own output region of point_list (4 slots per pair = two uint2
+// arrays of len), with the sorted values put back into vals[lo, lo + len) before the tile split
+// overwrites that region — no scratch arrays in the binning buffer.
 __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int gx, int gy, uint32_t lo, uint32_t len,
                                                const uint32_t* __restrict__ vals, bool lds_vals,
                                                const uint32_t* __restrict__ depth_keys, bool wide, int ipasses,
                                                uint32_t out_base, uint32_t* __restrict__ point_list,
-                                               uint2* __restrict__ ranges, uint2* __restrict__ scr0,
-                                               uint2* __restrict__ scr1, bool bucket) {
+                                               uint2* __restrict__ ranges, uint32_t lds_cap, bool bucket) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // The depth key: 27 bits in 3 passes of 9, wider frames in 4 of 8.  A run in no particular order
     // (ipasses > 0: the phase-B pairs of the gather path) needs index order among equal depth keys:
@@ -640,8 +686,8 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
     auto shift_of = [&](int p) { return p < ip ? 9 * p : (p - ip) * dbd; };
     auto db_of = [&](int p) { return p < ip ? 9 : dbd; };
     auto key_of = [&](int p, uint32_t v) { return p < ip ? (v & BIN_ID_MASK) : depth_keys[v & BIN_ID_MASK]; };
-    const uint2* sorted_g = nullptr;  // global path: the sorted run
-    if (len > 1 && len <= (uint32_t)kSxCap) {
+    bool global = false;  // the sorted run is back in vals[lo, lo + len)
+    if (len > 1 && len <= lds_cap) {
         const int R = (int)((len + 255) / 256);
         const uint32_t wl = (uint32_t)w * 64 * R;
         uint32_t kr[kSxMaxR], vr[kSxMaxR];
@@ -696,17 +742,21 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
             for (int r = 0; r < kSxMaxR; r++) vr[r] = sh.v[min(wl + (uint32_t)r * 64 + lane, len - 1)];
             __syncthreads();  // every read of the depth order before the index passes write sh.v
         }
-    } else if (RR_SX_GLOBAL && len > (uint32_t)kSxCap) {
+    } else if (RR_SX_GLOBAL && len > lds_cap) {
         // chunks of kSxCap in order; pass p reads run p - 1 (pass 0: the run's values with their
-        // keys) and writes the run at lo of scratch p % 2
+        // keys) and writes scratch p % 2 (halves of the run's point_list region, 8-B aligned:
+        // out_base is a multiple of 4 slots)
+        uint2* const scr0 = reinterpret_cast<uint2*>(point_list + out_base + 4u * lo);
+        uint2* const scr1 = scr0 + len;
+        const uint2* sorted_g = nullptr;
       for (int attempt = 0;; attempt++) {
         const int passes = ip + (wide ? 4 : 3);
         for (int p = 0; p < passes; p++) {
             const int db = db_of(p), shift = shift_of(p);
             const int ndig = 1 << db;
             const uint32_t mask = (uint32_t)ndig - 1u;
-            const uint2* src = p == 0 ? nullptr : ((p & 1) ? scr0 : scr1) + lo;
-            uint2* dst = ((p & 1) ? scr1 : scr0) + lo;
+            const uint2* src = p == 0 ? nullptr : ((p & 1) ? scr0 : scr1);
+            uint2* dst = (p & 1) ? scr1 : scr0;
             const bool fresh = src == nullptr || p == ip;  // keys recomputed from the values
             // digit totals of the whole run -> each digit's first slot
             for (int d = t; d < ndig; d += 256) sh.cursor[d] = 0;
@@ -757,7 +807,7 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
             }
             __syncthreads();
         }
-        sorted_g = (((passes - 1) & 1) ? scr1 : scr0) + lo;
+        sorted_g = ((passes - 1) & 1) ? scr1 : scr0;
         if (ipasses == 0 || attempt > 0) break;
         uint2* sg = const_cast<uint2*>(sorted_g);
         __threadfence_block();
@@ -768,6 +818,11 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
         // a long group: the full sort, index passes first, from the run's original values
         ip = ipasses;
       }
+        // the sorted values back over the run's input (read only by pass 0), freeing the region
+        uint32_t* const vw = const_cast<uint32_t*>(vals) + lo;
+        for (uint32_t i = t; i < len; i += 256) vw[i] = sorted_g[i].y;
+        __syncthreads();
+        global = true;
     }
     // the four tile lists, stable, from the depth-ordered run (LDS, global scratch, or the single /
     // empty run straight from vals)
@@ -777,7 +832,7 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
     for (uint32_t r0 = 0; r0 < len; r0 += 256) {
         const uint32_t j = r0 + (uint32_t)t;
         uint32_t v = 0u;
-        if (j < len) v = (len <= 1 && !lds_vals) ? vals[lo + j] : sorted_g ? sorted_g[j].y : sh.v[j];
+        if (j < len) v = (global || (len <= 1 && !lds_vals)) ? vals[lo + j] : sh.v[j];
         const uint32_t m = j < len ? v >> BIN_SHIFT : 0u;
         uint32_t rank[4];
 #pragma unroll
@@ -909,8 +964,8 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
                                                     const FrameTotals* __restrict__ ft, int gx, int gy,
                                                     uint32_t out_base, uint32_t* __restrict__ point_list,
                                                     uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits,
-                                                    uint2* __restrict__ scr0, uint2* __restrict__ scr1,
-                                                    const uint32_t* __restrict__ n_dev, uint32_t* report,
+                                                    uint32_t lds_cap, const uint32_t* __restrict__ n_dev,
+                                                    uint32_t* report,
                                                     int ipasses, const uint32_t* __restrict__ out_base_dev,
                                                     int bucket) {
     __shared__ SxShared sh;
@@ -936,29 +991,30 @@ __global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bo
     // out_base_dev: the lists start after the 4 slots per pair of an earlier phase (compact layout)
     const uint32_t ob = out_base_dev ? out_base + 4u * *out_base_dev : out_base;
     sortexpand_run(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
-                   ob, point_list, ranges, scr0, scr1, bucket != 0);
+                   ob, point_list, ranges, lds_cap, bucket != 0);
 }
 
 template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
-                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                       uint2* bounds, bool bounds_ready, uint32_t* report, hipStream_t st) {
+                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* bounds,
+                       bool bounds_ready, uint32_t* report, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0) return;
     if (L > 0 && !bounds_ready) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
-                                        open_bits, scr0, scr1, n_dev, n_dev ? report : nullptr, 0, nullptr,
+                                        open_bits, sx_lds_cap(), n_dev, n_dev ? report : nullptr, 0, nullptr,
                                         g_sx_bucket);
 }
 template void launch_sortexpand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, uint2*, uint2*, bool, uint32_t*, hipStream_t);
+                                          uint2*, bool, uint32_t*, hipStream_t);
 template void launch_sortexpand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                           const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, uint2*, uint2*, bool, uint32_t*, hipStream_t);
+                                          uint2*, bool, uint32_t*, hipStream_t);
 
 void set_sx_bucket(bool on) { g_sx_bucket = on ? 1 : 0; }
+void set_sx_lds_cap(int cap) { g_sx_lds_cap = (cap >= 1 && cap <= kSxCap) ? cap : kSxCap; }
 
 int index_passes(int P) {  // 9-bit passes covering the Gaussian indices [0, P)
     int b = 1;
@@ -970,8 +1026,7 @@ template <typename K>
 bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
-                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st,
-                             const uint32_t* out_base_dev) {
+                             uint2* bounds, uint32_t* report, hipStream_t st, const uint32_t* out_base_dev) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0 || nb > kBinScanMax) return false;
     const int wk = sizeof(K) == 4;
@@ -979,17 +1034,17 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
     k_bin_scan<<<1, 1024, 0, st>>>(nb, n_dev, bin_cnt, bounds);
     k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, vals_sorted);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
-                                        open_bits, scr0, scr1, n_dev, report, index_passes(P), out_base_dev,
+                                        open_bits, sx_lds_cap(), n_dev, report, index_passes(P), out_base_dev,
                                         g_sx_bucket);
     return true;
 }
 template bool launch_sortexpand_small<uint16_t>(int, const uint16_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
-                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*,
-                                                hipStream_t, const uint32_t*);
+                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t,
+                                                const uint32_t*);
 template bool launch_sortexpand_small<uint32_t>(int, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
-                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint2*, uint2*, uint32_t*,
-                                                hipStream_t, const uint32_t*);
+                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t,
+                                                const uint32_t*);
 
 }  // namespace rr

@@ -383,9 +383,10 @@ __global__ __launch_bounds__(1024) void k_bwd_prologue(float4* __restrict__ gacc
 
 void launch_bwd_prologue(float* gacc, size_t nfloats, int T, const uint32_t* tile_max, uint32_t* order,
                          const uint32_t* order_flag, hipStream_t st) {
-    const size_t n4 = nfloats / 4;  // P * GACC_STRIDE, a multiple of 4
-    const size_t zb = std::max<size_t>(1, std::min<size_t>((n4 + 1023) / 1024, 2048));
+    const size_t n4 = nfloats / 4;  // P * GACC_STRIDE, a multiple of 4 (0: already clear)
+    const size_t zb = n4 ? std::max<size_t>(1, std::min<size_t>((n4 + 1023) / 1024, 2048)) : 0;
     const bool ord = order && T > 0;
+    if (zb + (ord ? 1 : 0) == 0) return;
     k_bwd_prologue<<<(unsigned)(zb + (ord ? 1 : 0)), 1024, 0, st>>>(reinterpret_cast<float4*>(gacc), n4, T, tile_max,
                                                                     ord ? order : nullptr, order_flag);
 }

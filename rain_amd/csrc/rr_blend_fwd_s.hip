@@ -21,6 +21,8 @@
 //     1/255) skips the pair's blend with a uniform branch; a wave leaves when all its pixels closed.
 // Measured (tools/fwd_trace.py, per-wave s_memrealtime records): phase A runs ~6 waves per SIMD
 // for ~2/3 of its span, then drains; a wave walks ~100 pairs (its 8 rows saturate) in ~40 us.
+#include <algorithm>
+
 #include "rr_common.hpp"
 #include "rr_kernels.hpp"
 
@@ -47,6 +49,12 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
 #endif
     constexpr int G = RR_FWD_S_GROUP;
     const int ntiles = a.gx * a.gy;
+    if ((int)blockIdx.x >= ntiles) {  // the workspace clear (block-uniform, after every tile's block)
+        const size_t nb = gridDim.x - (unsigned)ntiles, i0 = (blockIdx.x - (unsigned)ntiles) * (size_t)blockDim.x;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (size_t i = i0 + threadIdx.x; i < a.clear_n4; i += nb * blockDim.x) a.clear[i] = z;
+        return;
+    }
     const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
     const int tx = tile % a.gx, ty = tile / a.gx;
@@ -318,15 +326,19 @@ void launch_blend_fwd_s(const BlendFwdArgs& a_in, int waves, hipStream_t st) {
     const int T = a.gx * a.gy;
     if (T == 0) return;
     const bool aux = a.out_normal != nullptr;
+    // workspace clear: ~16 float4 stores per thread, at most 4096 extra workgroups
+    const size_t per_block = (size_t)64 * waves * 16;
+    const int nc = (a.clear && a.clear_n4) ? (int)std::min<size_t>((a.clear_n4 + per_block - 1) / per_block, 4096) : 0;
+    const int nb = T + nc;
     if (waves == 1) {
-        if (aux) k_blend_fwd_s<1, true><<<T, 64, 0, st>>>(a);
-        else k_blend_fwd_s<1, false><<<T, 64, 0, st>>>(a);
+        if (aux) k_blend_fwd_s<1, true><<<nb, 64, 0, st>>>(a);
+        else k_blend_fwd_s<1, false><<<nb, 64, 0, st>>>(a);
     } else if (waves == 4) {
-        if (aux) k_blend_fwd_s<4, true><<<T, 256, 0, st>>>(a);
-        else k_blend_fwd_s<4, false><<<T, 256, 0, st>>>(a);
+        if (aux) k_blend_fwd_s<4, true><<<nb, 256, 0, st>>>(a);
+        else k_blend_fwd_s<4, false><<<nb, 256, 0, st>>>(a);
     } else {
-        if (aux) k_blend_fwd_s<2, true><<<T, 128, 0, st>>>(a);
-        else k_blend_fwd_s<2, false><<<T, 128, 0, st>>>(a);
+        if (aux) k_blend_fwd_s<2, true><<<nb, 128, 0, st>>>(a);
+        else k_blend_fwd_s<2, false><<<nb, 128, 0, st>>>(a);
     }
 }
 

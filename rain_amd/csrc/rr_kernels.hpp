@@ -112,6 +112,10 @@ struct BlendFwdArgs {
     float* out_normal;      // the blended normal map [3,H,W]; both null otherwise
     const uint32_t* order;  // [T] tile of each workgroup, longest list first; null: XCD order
     uint32_t* trace;        // RR_FWD_TRACE builds only: per-wave timing records (rr_debug_set_fwd_trace)
+    // the backward's accumulator workspace (rr_set_forward_workspace), zero-filled by extra
+    // workgroups after the tiles' (dispatched last: they run in the blend's drain); null: none
+    float4* clear;
+    size_t clear_n4;
 };
 
 struct BlendBwdArgs {
@@ -203,15 +207,25 @@ void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uin
 // The phases' Gaussian lists (PhaseLists, ft->GA / GB entries); the last thread publishes {LA, rect,
 // seq, wide, LB} to box (may be null) and ft.  temp: split_scan_temp_bytes(P)
 size_t split_scan_temp_bytes(int P);
+// The depth cut's inputs when the split scan's first launch computes it (instead of k_early_cut)
+struct CutArgs {
+    const uint2* block_sums;
+    const uint32_t* block_wide;
+    uint32_t den, min_pairs;
+    uint32_t* box;  // host mailbox (may be null) and this read's sequence number
+    uint32_t seq;
+};
 void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
-                       int direct_blocks, uint32_t* zero, int nzero,
-                       hipStream_t st);  // zero (optional): nzero words cleared by its first launch
+                       int direct_blocks, uint32_t* zero, int nzero, hipStream_t st,
+                       const CutArgs* cut = nullptr);  // zero (optional): nzero words cleared by its first launch
 template <typename K>
 void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
                        const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
-                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* scr0, uint2* scr1,
-                       uint2* bounds, bool bounds_ready, uint32_t* report,
+                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* bounds,
+                       bool bounds_ready, uint32_t* report,
                        hipStream_t st);  // bounds: [bins], zero on entry, or filled by the sort (bounds_ready)
+// Runs longer than the LDS cap are sorted in their own point_list region and written back over
+// vals (launch_sortexpand*: vals is overwritten for those runs).
 // Phase B of the gather path (rr_bin.hip k_bin_count + k_bin_scan + k_bin_scatter + k_sortexpand):
 // the densely emitted, unordered phase-B pairs (k_duplicate_b_gather) counted per bin (bin_cnt, zero
 // on entry) and dropped into their bins' runs — no bin sort, no bounds launch.  report:
@@ -221,7 +235,7 @@ template <typename K>
 bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
-                             uint2* scr0, uint2* scr1, uint2* bounds, uint32_t* report, hipStream_t st,
+                             uint2* bounds, uint32_t* report, hipStream_t st,
                              const uint32_t* out_base_dev = nullptr);  // lists at out_base + 4 * *out_base_dev
 template <typename K>
 struct DupArgs {
@@ -358,4 +372,5 @@ void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
 void set_sx_bucket(bool on);  // rr_bin.hip: per-bin bucket sort (default) or LSD passes only
+void set_sx_lds_cap(int cap);  // runs longer than cap (1..2048; other values: 2048) take the global path
 }  // namespace rr

@@ -215,8 +215,10 @@ def debug_views(geomBuffer, binningBuffer, imageBuffer, num_rendered, P, W, H):
 
     return dict(
         # per-tile lists live at the ranges' absolute positions: 4 slots per (bin, Gaussian) pair
-        point_list=grab(v.point_list, 8 * num_rendered, torch.int32, binningBuffer) if num_rendered else
-        torch.empty((0,), dtype=torch.int32, device=dev),
+        # (the compact layout of the all-gather binning holds 4 L slots: clamped to the buffer)
+        point_list=grab(v.point_list, min(8 * num_rendered, (binningBuffer.numel() - (v.point_list -
+                                          binningBuffer.data_ptr())) // 4), torch.int32, binningBuffer)
+        if num_rendered else torch.empty((0,), dtype=torch.int32, device=dev),
         ranges=grab(v.ranges, 2 * T, torch.int32, imageBuffer).view(T, 2),
         tile_max=grab(v.tile_max, T, torch.int32, imageBuffer),
         final_T=grab(v.final_T, H * W, torch.float32, imageBuffer).view(H, W),

@@ -40,6 +40,9 @@ class RawFrame:
     num_rendered: int
     P: int
     M: int
+    # the backward's accumulator workspace, zero-filled by the forward render
+    # (rr_set_forward_workspace); the first backward uses it, a second one allocates its own
+    ws: torch.Tensor | None = None
 
 
 class BinningCache:
@@ -108,6 +111,7 @@ def forward_params(params, sh_degree: int, W: int, H: int, tanfovx: float, tanfo
     img = torch.empty((L.rr_image_bytes(W, H),), **u8)
     stream = N.stream_of(xyz)
     nr, npairs = ctypes.c_int(0), ctypes.c_int(0)
+    ws = _register_workspace(L, P, dev)
     if P > 0 and cache is not None:
         binning = cache.buf if cache.buf is not None and cache.buf.device == dev else torch.empty((0,), **u8)
         need = ctypes.c_size_t(0)
@@ -119,23 +123,41 @@ def forward_params(params, sh_degree: int, W: int, H: int, tanfovx: float, tanfo
             rc = L.rr_forward_render(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii), _p(geom),
                                      _p(img), _p(binning), binning.numel(), npairs.value, _p(color), _p(depth),
                                      stream)
-        N.check(rc, "fused forward")
-        st = RawFrame(frame, cam, gs, (keep, params), radii, geom, img, binning, nr.value, P, M)
+        _check_render(L, rc, "fused forward")
+        st = RawFrame(frame, cam, gs, (keep, params), radii, geom, img, binning, nr.value, P, M, ws)
         return color, radii, depth, st
     if P > 0:
-        N.check(L.rr_forward_geometry(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii), _p(geom),
-                                      geom.numel(), _p(img), img.numel(), ctypes.byref(nr), ctypes.byref(npairs),
-                                      stream), "fused forward")
+        _check_render(L, L.rr_forward_geometry(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii),
+                                               _p(geom), geom.numel(), _p(img), img.numel(), ctypes.byref(nr),
+                                               ctypes.byref(npairs), stream), "fused forward")
     binning = torch.empty((L.rr_binning_bytes(npairs.value, W, H) if npairs.value > 0 else 0,), **u8)
     if P > 0:
-        N.check(L.rr_forward_render(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii), _p(geom),
-                                    _p(img), _p(binning), binning.numel(), npairs.value, _p(color), _p(depth),
-                                    stream), "fused forward")
+        _check_render(L, L.rr_forward_render(ctypes.byref(frame), ctypes.byref(cam), ctypes.byref(gs), _p(radii),
+                                             _p(geom), _p(img), _p(binning), binning.numel(), npairs.value, _p(color),
+                                             _p(depth), stream), "fused forward")
     else:
         color.copy_(bg.view(3, 1, 1).expand(3, H, W))
         depth.zero_()
-    st = RawFrame(frame, cam, gs, (keep, params), radii, geom, img, binning, nr.value, P, M)
+    st = RawFrame(frame, cam, gs, (keep, params), radii, geom, img, binning, nr.value, P, M, ws)
     return color, radii, depth, st
+
+
+def _register_workspace(L, P: int, dev) -> torch.Tensor | None:
+    """The backward's accumulator workspace, registered for the coming render to zero-fill
+    (rr_set_forward_workspace: the backward then skips its clear)."""
+    if P <= 0:
+        return None
+    ws = torch.empty((L.rr_backward_workspace_bytes(P),), dtype=torch.uint8, device=dev)
+    N.check(L.rr_set_forward_workspace(_p(ws), ws.numel()), "register workspace")
+    return ws
+
+
+def _check_render(L, rc: int, what: str):
+    """N.check, dropping a workspace registration a failed call left pending (it must not outlive
+    its buffer)."""
+    if rc not in (0, N.RR_INCOMPLETE):
+        L.rr_set_forward_workspace(None, 0)
+    N.check(rc, what)
 
 
 @dataclass
@@ -197,6 +219,7 @@ def forward_next(nxt: NextFrame, model, cache: BinningCache | None = None):
     stream = N.stream_of(nxt.geom)
     nr, npairs = ctypes.c_int(0), ctypes.c_int(0)
     need = ctypes.c_size_t(0)
+    ws = _register_workspace(L, P, dev)
     binning = cache.buf if cache is not None and cache.buf is not None and cache.buf.device == dev \
         else torch.empty((0,), **u8)
     rc = L.rr_forward_from_geometry(ctypes.byref(nxt.frame), ctypes.byref(nxt.cam), _p(nxt.radii), _p(nxt.geom),
@@ -208,8 +231,9 @@ def forward_next(nxt: NextFrame, model, cache: BinningCache | None = None):
         rc = L.rr_forward_render_geometry(ctypes.byref(nxt.frame), ctypes.byref(nxt.cam), _p(nxt.radii),
                                           _p(nxt.geom), _p(img), _p(binning), binning.numel(), npairs.value,
                                           _p(color), _p(depth), stream)
-    N.check(rc, "fused forward (precomputed geometry)")
-    st = RawFrame(nxt.frame, nxt.cam, gs, (nxt.keep, params), nxt.radii, nxt.geom, img, binning, nr.value, P, nxt.M)
+    _check_render(L, rc, "fused forward (precomputed geometry)")
+    st = RawFrame(nxt.frame, nxt.cam, gs, (nxt.keep, params), nxt.radii, nxt.geom, img, binning, nr.value, P, nxt.M,
+                  ws)
     return color, nxt.radii, depth, st
 
 
@@ -244,8 +268,14 @@ def backward(st: RawFrame, dL_dpix: torch.Tensor, grads: dict | None, stats: tup
                     ctypes.pointer(adam) if adam is not None else None,
                     ctypes.pointer(next_frame.desc) if next_frame is not None else None)
     dev = dpix.device
-    ws = torch.empty((L.rr_backward_workspace_bytes(st.P),), dtype=torch.uint8, device=dev)
-    N.check(L.rr_backward(ctypes.byref(st.frame), ctypes.byref(st.cam), ctypes.byref(st.gs), _p(st.radii),
+    frame = st.frame
+    if st.ws is not None:  # zero-filled by the forward render: the backward skips its clear
+        ws, st.ws = st.ws, None
+        frame = N.RRFrame.from_buffer_copy(st.frame)
+        frame.flags |= N.RR_FLAG_WORKSPACE_REGISTERED
+    else:
+        ws = torch.empty((L.rr_backward_workspace_bytes(st.P),), dtype=torch.uint8, device=dev)
+    N.check(L.rr_backward(ctypes.byref(frame), ctypes.byref(st.cam), ctypes.byref(st.gs), _p(st.radii),
                           _p(st.geom), _p(st.img), _p(st.binning), st.num_rendered, _p(dpix), _p(ws), ws.numel(),
                           ctypes.byref(out), N.stream_of(dpix)), "fused backward")
 

@@ -3,7 +3,8 @@ gives the reference's per-tile lists: phase A by the windowed duplicate + bin so
 the gather paths (every Gaussian / the split scan's list); phase B by the gather path over its list
 (default), over every Gaussian, or by the windowed path; per-bin order by the bucket sort (default)
 or by the LSD passes only; bin runs from the bin sort's last scatter (default) or a bounds launch;
-the windowed duplicate's window starts from the split scan's marks or from their own launch.
+the windowed duplicate's window starts from the split scan's marks or from their own launch; long
+runs depth-sorted in LDS or through their own output region (sx_lds_cap).
 
 For each path: the exact (depth, index) lists of the reference's 64-bit-key sort with culling and
 early stop off (tests/test_parity_gpu.py::_check_pair_order, against the oracle), the two-phase
@@ -31,6 +32,11 @@ PATHS = {
     "split_marks": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16)},
     "split_marks_windowed_b": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16),
                                "phase_b_gather": (0, 1)},
+    # runs over 64 pairs through the global path (their own point_list region as scratch)
+    "global_runs": {"sx_lds_cap": (64, 0)},
+    "global_runs_gather_a": {"sx_lds_cap": (64, 0), "phase_a_gather": (2, 0)},
+    "global_runs_windowed_b": {"sx_lds_cap": (64, 0), "phase_b_gather": (0, 1), "sx_bucket": (0, 1)},
+    "cut_kernel": {"cut_in_scan": (0, 1)},  # the depth cut by its own one-workgroup launch
     "window_starts_launch": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16),
                              "phase_b_gather": (0, 1), "split_marks": (0, 1)},
 }

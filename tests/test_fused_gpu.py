@@ -366,3 +366,70 @@ def test_sharded_adam_equals_full_step(world):
             sa, sb = ga.optimizer.state[pa], gb.optimizer.state[pb]
             assert torch.equal(sa["exp_avg"], sb["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sb["exp_avg_sq"])
             assert float(sa["step"]) == float(sb["step"])
+
+
+@pytest.mark.parametrize("full", [False, True])
+def test_forward_clears_the_registered_workspace(gpu, monkeypatch, full):
+    """rr_set_forward_workspace: the forward render zero-fills the backward's accumulator workspace
+    (extra workgroups of its first blend launch) and the backward (RR_FLAG_WORKSPACE_REGISTERED)
+    skips its own clear.  A registered workspace full of NaN bytes must give the gradients of a
+    backward that clears its workspace itself; a second registration replaces the first; a
+    workspace that is not the registered one is still cleared by the backward."""
+    from rain_amd import _native as N
+
+    if full:  # single-phase frame: the clear rides on the one blend launch
+        monkeypatch.setattr(fused._C, "EARLY_STOP", False)
+    P, W, H = 30_000, 200, 150
+    g = _model(P, 3, 3)
+    cam = cameras.fibonacci_cameras(8, W, H)[2].to("cuda")
+    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+    dimg = torch.randn(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(2))
+    L = N.raster()
+    nbytes = int(L.rr_backward_workspace_bytes(P))
+
+    def nan_bytes():
+        return torch.full((nbytes,), 255, dtype=torch.uint8, device="cuda")  # every float NaN
+
+    def grads(st):
+        out = {k: torch.full_like(v, float("nan")) for k, v in _params(g).items()}
+        fused.backward(st, dimg, out, None)
+        torch.cuda.synchronize()
+        for k in NAMES:
+            assert torch.isfinite(out[k]).all(), k
+        return out
+
+    real = fused._register_workspace
+    # reference: no registration, the backward clears its (dirty) workspace itself
+    monkeypatch.setattr(fused, "_register_workspace", lambda L_, P_, dev: None)
+    _c, _r, _d, st = fused.forward(g, cam, bg, 0.3)
+    assert st.ws is None
+    ref = grads(st)
+
+    def nan_ws(L_, P_, dev):
+        stale = nan_bytes()
+        N.check(L_.rr_set_forward_workspace(stale.data_ptr(), stale.numel()), "register")
+        ws = nan_bytes()
+        N.check(L_.rr_set_forward_workspace(ws.data_ptr(), ws.numel()), "register")  # replaces `stale`
+        return ws
+
+    monkeypatch.setattr(fused, "_register_workspace", nan_ws)
+    _c, _r, _d, st = fused.forward(g, cam, bg, 0.3)
+    torch.cuda.synchronize()
+    assert int(torch.count_nonzero(st.ws)) == 0  # zero-filled by the render
+    out = grads(st)
+    for k in NAMES:
+        assert rel_l1(out[k], ref[k]) < 1e-5, (k, rel_l1(out[k], ref[k]))
+    # flag set but a different buffer: the backward clears it
+    _c, _r, _d, st = fused.forward(g, cam, bg, 0.3)
+    st.ws = nan_bytes()
+    out = grads(st)
+    for k in NAMES:
+        assert rel_l1(out[k], ref[k]) < 1e-5, (k, rel_l1(out[k], ref[k]))
+    # the default registration (fused._register_workspace) gives the same gradients
+    monkeypatch.setattr(fused, "_register_workspace", real)
+    _c, _r, _d, st = fused.forward(g, cam, bg, 0.3)
+    assert st.ws is not None
+    out = grads(st)
+    for k in NAMES:
+        assert rel_l1(out[k], ref[k]) < 1e-5, (k, rel_l1(out[k], ref[k]))
+    assert L.rr_set_forward_workspace(None, 0) == 0

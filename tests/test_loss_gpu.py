@@ -41,10 +41,29 @@ def test_fused_loss_grad_scale(gpu):
     torch.testing.assert_close(x1.grad, 3.0 * x2.grad, rtol=1e-6, atol=1e-12)
 
 
+@pytest.fixture
+def two_pass():
+    """rl_l1_ssim_forward_backward as the two passes over stored maps (rl_set_fused_band(0), the
+    default)."""
+    from rain_amd import _native as N
+
+    N.loss_lib().rl_set_fused_band(0)
+    yield
+
+
+@pytest.fixture(params=[16, 32, 64])
+def band_walk(request):
+    from rain_amd import _native as N
+
+    assert N.loss_lib().rl_set_fused_band(request.param) == 0
+    yield request.param
+    N.loss_lib().rl_set_fused_band(0)
+
+
 @pytest.mark.parametrize("H,W", [(75, 100), (9, 200), (1080, 1920)])
-def test_forward_backward_in_one_call_is_bitwise_the_two_calls(gpu, H, W):
-    """rl_l1_ssim_forward_backward (the training step's form: the loss finalize rides on the
-    backward launch) gives bitwise the loss / parts of rl_l1_ssim_forward and the dimg of
+def test_forward_backward_in_one_call_is_bitwise_the_two_calls(gpu, two_pass, H, W):
+    """rl_l1_ssim_forward_backward in its two-pass form (the loss finalize rides on the backward
+    launch) gives bitwise the loss / parts of rl_l1_ssim_forward and the dimg of
     rl_l1_ssim_backward, also with a grad_loss scale."""
     from rain_amd.loss import l1_ssim_backward, l1_ssim_forward, l1_ssim_forward_backward
 
@@ -58,3 +77,29 @@ def test_forward_backward_in_one_call_is_bitwise_the_two_calls(gpu, H, W):
         loss2, parts2, dimg2 = l1_ssim_forward_backward(img, gt, 0.2, gl)
         assert torch.equal(loss, loss2) and torch.equal(parts, parts2)
         assert torch.equal(dimg, dimg2)
+
+
+@pytest.mark.parametrize("H,W", [(75, 100), (9, 200), (33, 55), (96, 54), (540, 960), (1080, 1920)])
+def test_one_band_walk_matches_the_two_passes(gpu, band_walk, H, W):
+    """rl_l1_ssim_forward_backward's one-band-walk form (rl_set_fused_band: the derivative maps
+    formed and blurred on chip, 54-column blocks) against the separate forward + backward passes: dimg to float
+    contraction (1e-6 of its scale), loss and parts to float rounding (a different block partition
+    of the sums), also with a grad_loss scale; and against the float64 reference like the two-pass
+    loss."""
+    from rain_amd.loss import l1_ssim_backward, l1_ssim_forward, l1_ssim_forward_backward
+
+    g = torch.Generator().manual_seed(11 * H + W)
+    img = torch.rand((3, H, W), generator=g).to(gpu)
+    gt = (img.cpu() * 0.6 + 0.4 * torch.rand((3, H, W), generator=g)).to(gpu)
+    for scale in (None, 2.5):
+        gl = None if scale is None else torch.tensor([scale], device=gpu)
+        loss, parts, ws = l1_ssim_forward(img, gt, 0.2)
+        dimg = l1_ssim_backward(img, gt, 0.2, ws, gl)
+        loss2, parts2, dimg2 = l1_ssim_forward_backward(img, gt, 0.2, gl)
+        assert torch.isfinite(dimg2).all()
+        assert float((dimg2 - dimg).abs().max()) <= 1e-6 * float(dimg.abs().max()), (H, W, scale)
+        torch.testing.assert_close(loss2, loss, rtol=2e-6, atol=0)
+        torch.testing.assert_close(parts2, parts, rtol=2e-6, atol=1e-9)
+    xr = img.double().cpu()
+    ref = 0.8 * l1_loss(xr, gt.double().cpu()) + 0.2 * (1 - ssim(xr, gt.double().cpu()))
+    assert abs(float(loss2) - float(ref)) <= 2e-6 * abs(float(ref)) + 1e-7

@@ -109,6 +109,18 @@ def test_validation_errors_without_gpu():
                                  ctypes.byref(nr), ctypes.byref(nr), None) == 0 and nr.value == 0
 
 
+def test_forward_workspace_registration_validation():
+    """rr_set_forward_workspace (no device call): 16-B alignment and size, NULL drops it; the
+    tuning keys of round 5 exist."""
+    L = N.raster()
+    assert L.rr_set_forward_workspace(8, 64) == 1 and b"16-byte" in L.rr_last_error()
+    assert L.rr_set_forward_workspace(16, 40) == 1
+    assert L.rr_set_forward_workspace(None, 0) == 0
+    for key, dflt in (("split_marks", 1), ("sx_lds_cap", 0), ("forward_clear", 1), ("cut_in_scan", 1)):
+        assert L.rr_set_tuning(key.encode(), dflt) == 0, key
+    assert N.RR_FLAG_WORKSPACE_REGISTERED == 16
+
+
 def _settings(device="cpu"):
     return GaussianRasterizationSettings(
         image_height=48, image_width=64, tanfovx=0.5, tanfovy=0.4, bg=torch.zeros(3, device=device),

@@ -15,6 +15,7 @@
 #   abv=V1,V2[,..]        the same over librain_raster.so variants (tools/build_variant.py names)
 #   prof                  rocprofv3 kernel trace + stats of the default bench, timed-window summary
 #   stalls=PATTERN        one SQ stall-counter pass, summarised for the kernels matching PATTERN
+#   owner                 owner-kernel time of the sharded step for N = 1, 2, 4, 8 (tools/owner_bench.py)
 #   pmc                   PMC passes (tools/profile_round.sh without the trace) -> pmc_traffic.json
 # Output: gpurun_out/TAG_*.
 set -o pipefail
@@ -64,6 +65,11 @@ for STEP in "$@"; do
         done
       done
       cat ${OUT}_ab.jsonl ;;
+    owner)
+      # owner-kernel time of the Gaussian-sharded step by N (tools/owner_bench.py)
+      timeout -k 10 400 python3 -u tools/owner_bench.py > ${OUT}_owner.jsonl 2> ${OUT}_owner.err \
+        || { tail -20 ${OUT}_owner.err; exit 1; }
+      cat ${OUT}_owner.jsonl ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${OUT}_prof -o run --output-format csv \
         -- python3 bench.py --no-cpu-baseline > ${OUT}_prof_bench.json 2> ${OUT}_prof.err \

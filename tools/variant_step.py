@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--tune", action="append", default=[], help="rr_set_tuning key=value (repeatable)")
     ap.add_argument("--no-fuse-next", action="store_true",
                     help="the next frame's preprocess as its own launch (Trainer.fuse_next = False)")
+    ap.add_argument("--ssim-band", type=int, default=0,
+                    help="rl_l1_ssim_forward_backward as one band walk of this many rows (rl_set_fused_band)")
     ap.add_argument("--loss-split", action="store_true",
                     help="the trainer's loss as two calls (forward, backward) instead of rl_l1_ssim_forward_backward")
     a = ap.parse_args()
@@ -44,6 +46,8 @@ def main():
             return loss, parts, RL.l1_ssim_backward(img, gt, lam, ws, grad_loss)
 
         RL.l1_ssim_forward_backward = split
+    if a.ssim_band:
+        _native.check(_native.loss_lib().rl_set_fused_band(a.ssim_band), "rl_set_fused_band")
     for kv in a.tune:
         k, v = kv.split("=")
         _native.check(_native.raster().rr_set_tuning(k.encode(), int(v)), "rr_set_tuning " + kv)
