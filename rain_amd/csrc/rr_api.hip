@@ -1305,6 +1305,10 @@ int rr_set_tuning(const char* key, int value) {
         g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
         return RR_OK;
     }
+    if (key && std::string(key) == "dup_big_bins") {
+        set_dup_big_bins(value);
+        return RR_OK;
+    }
     if (key && std::string(key) == "cut_in_scan") {
         g_cut_in_scan = value != 0;
         return RR_OK;

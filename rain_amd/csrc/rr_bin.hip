@@ -957,8 +957,12 @@ __global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ k
 }
 
 // per bin: open test (phase B), the bin's run from k_bin_bounds, then sortexpand_run
+#ifndef RR_SX_OCC
+#define RR_SX_OCC 1  // a minimum of 6 workgroups per CU (69 VGPRs instead of 81) measured neutral:
+                     // ranges 0.0925 vs 0.0919 ms/step (profiles/r05_dup_big_sx_occ_ab.jsonl)
+#endif
 template <typename K>
-__global__ __launch_bounds__(256) void k_sortexpand(const uint2* __restrict__ bounds,
+__global__ __launch_bounds__(256, RR_SX_OCC) void k_sortexpand(const uint2* __restrict__ bounds,
                                                     const K* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ depth_keys,
                                                     const FrameTotals* __restrict__ ft, int gx, int gy,

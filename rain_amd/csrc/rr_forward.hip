@@ -381,6 +381,12 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
 // atomic on *n_total and writes them densely, in no particular order: the per-bin sort
 // (rr_bin.hip k_sortexpand) restores the reference's (depth, index) order.  The extra workgroup 0
 // of phase B computes the backward's tile order as k_duplicate's does.
+// Phase-B Gaussians whose bounding rect spans more than big_bins bins (default 32; rr_set_tuning
+// "dup_big_bins", 0: none) are emitted by their whole workgroup, 256 bins at a time.
+namespace {
+int g_dup_big_bins = 32;
+}
+void set_dup_big_bins(int n) { g_dup_big_bins = n >= 0 ? n : 32; }
 template <typename K, bool PHASE_B>
 __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restrict__ tiles,
                                                     const uint32_t* __restrict__ depth_keys,
@@ -394,7 +400,7 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
                                                     uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ order_flag, int order_T,
                                                     const uint32_t* __restrict__ list_n,
-                                                    const uint32_t* __restrict__ list_idx) {
+                                                    const uint32_t* __restrict__ list_idx, int big_bins) {
     if (PHASE_B && order_out && blockIdx.x == 0) {
         tile_order_body256(order_T, order_cost, open_bits, order_out);
         if (threadIdx.x == 0) *order_flag = (uint32_t)order_T;
@@ -405,6 +411,9 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
     __shared__ uint32_t s_open[PHASE_B ? 2048 : 1];
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t s_base;
+    __shared__ uint32_t s_big[PHASE_B ? 256 : 1];  // phase B: Gaussians of > kDupBigBins bins, done by
+    __shared__ uint32_t s_nbig;                      // the whole workgroup after the per-thread walks
+    if (PHASE_B && threadIdx.x == 0) s_nbig = 0u;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int s = wb * 256 + t;
     // this thread's Gaussian and whether it is in the phase (loads first: they overlap the mask's):
@@ -474,7 +483,10 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         const float4 Bv = splats[g].b;
         asm volatile("" ::"v"(r), "v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(Bv.x), "v"(Bv.w));
         tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
-        if (x0 < x1 && y0 < y1 && (!PHASE_B || rect_open(x0, y0, x1, y1))) {
+        const int nbins = (((x1 + 1) >> 1) - (x0 >> 1)) * (((y1 + 1) >> 1) - (y0 >> 1));
+        if (PHASE_B && big_bins > 0 && x0 < x1 && y0 < y1 && nbins > big_bins) {
+            s_big[atomicAdd(&s_nbig, 1u)] = g;  // one thread's walk would hold up its workgroup
+        } else if (x0 < x1 && y0 < y1 && (!PHASE_B || rect_open(x0, y0, x1, y1))) {
             float ccx, ccy, ccz;
             splat_conic(A, Bv, ccx, ccy, ccz);
             ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
@@ -518,17 +530,68 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         pre += i < w ? wsum[i] : 0u;
         tot += wsum[i];
     }
-    if (tot == 0) return;  // block-uniform
-    if (t == 0) s_base = atomicAdd(n_total, tot);
-    __syncthreads();
-    if (cnt) {
-        const uint32_t pos = s_base + pre + incl - cnt;
-        // phase A: the walk and the preprocess's count are the same closed form on the same record
-        // (rr_preprocess.hpp); should they ever disagree, the reserved slots left over get an empty
-        // tile mask, which the per-bin split writes to no tile list
-        for (uint32_t c = walk(true, pos, cnt); c < cnt; c++) {
-            keys[pos + c] = (K)0;
-            vals[pos + c] = g;
+    if (tot != 0) {  // block-uniform
+        if (t == 0) s_base = atomicAdd(n_total, tot);
+        __syncthreads();
+        if (cnt) {
+            const uint32_t pos = s_base + pre + incl - cnt;
+            // phase A: the walk and the preprocess's count are the same closed form on the same
+            // record (rr_preprocess.hpp); should they ever disagree, the reserved slots left over get
+            // an empty tile mask, which the per-bin split writes to no tile list
+            for (uint32_t c = walk(true, pos, cnt); c < cnt; c++) {
+                keys[pos + c] = (K)0;
+                vals[pos + c] = g;
+            }
+        }
+    }
+    if constexpr (PHASE_B) {
+        // the large Gaussians: 256 bins of one Gaussian at a time, one per thread (its bin row's
+        // spans, mask and open tiles), compacted by ballots, one reservation per round
+        const uint32_t nbig = s_nbig;  // read after the barrier above (or the one at the top)
+        const uint64_t lt = (1ull << lane) - 1ull;
+        for (uint32_t j = 0; j < nbig; j++) {
+            const uint32_t gb = s_big[j];
+            const int rb = radii[gb];
+            const float4 A = splats[gb].a;
+            const float4 Bv = splats[gb].b;
+            int bx0, by0, bx1, by1;
+            tile_rect(A.x, A.y, rb, gx, gy, bx0, by0, bx1, by1);
+            float ccx, ccy, ccz;
+            splat_conic(A, Bv, ccx, ccy, ccz);
+            const CullEll eb = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
+            const int Xs = bx0 >> 1, bw = ((bx1 + 1) >> 1) - Xs, Ys = by0 >> 1;
+            const int nb = bw * (((by1 + 1) >> 1) - Ys);
+            for (int b0 = 0; b0 < nb; b0 += 256) {
+                const int b = b0 + t;
+                uint32_t m = 0u;
+                int X = 0, Y = 0;
+                if (b < nb) {
+                    Y = Ys + b / bw;
+                    X = Xs + b % bw;
+                    int l0, h0, l1, h1;
+                    bin_row_spans(eb, cull, Y, bx0, bx1, by0, by1, l0, h0, l1, h1);
+                    m = bin_mask(X, l0, h0, l1, h1);
+                    if (m) m &= open4(X, Y);
+                }
+                const uint64_t bal = __ballot(m != 0u);
+                __syncthreads();  // the previous round's reads of wsum / s_base are done
+                if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
+                __syncthreads();
+                uint32_t bpre = 0, btot = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    bpre += i < w ? wsum[i] : 0u;
+                    btot += wsum[i];
+                }
+                if (btot == 0) continue;  // block-uniform
+                if (t == 0) s_base = atomicAdd(n_total, btot);
+                __syncthreads();
+                if (m) {
+                    const uint32_t pos = s_base + bpre + (uint32_t)__popcll(bal & lt);
+                    keys[pos] = (K)(Y * bgx + X);
+                    vals[pos] = gb | (m << BIN_SHIFT);
+                }
+            }
         }
     }
 }
@@ -600,14 +663,14 @@ void launch_dup_gather(const DupArgs<K>& d, bool phase_b, hipStream_t st) {
         k_dup_gather<K, false><<<blocks_for(d.P), 256, 0, st>>>(d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii,
                                                                  d.gx, d.gy, d.cull, d.keys, d.vals, nullptr,
                                                                  d.n_total, nullptr, nullptr, nullptr, 0,
-                                                                 d.idx ? d.n_list : nullptr, d.idx);
+                                                                 d.idx ? d.n_list : nullptr, d.idx, 0);
         return;
     }
     const bool ord = d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
     k_dup_gather<K, true><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
         d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits,
         d.n_total, ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T,
-        d.idx ? d.n_list : nullptr, d.idx);
+        d.idx ? d.n_list : nullptr, d.idx, g_dup_big_bins);
 }
 template void launch_dup_gather<uint16_t>(const DupArgs<uint16_t>&, bool, hipStream_t);
 template void launch_dup_gather<uint32_t>(const DupArgs<uint32_t>&, bool, hipStream_t);

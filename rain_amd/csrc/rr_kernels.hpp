@@ -372,5 +372,6 @@ void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
 void set_sx_bucket(bool on);  // rr_bin.hip: per-bin bucket sort (default) or LSD passes only
-void set_sx_lds_cap(int cap);  // runs longer than cap (1..2048; other values: 2048) take the global path
+void set_sx_lds_cap(int cap);
+void set_dup_big_bins(int n);  // rr_forward.hip: phase-B Gaussians over n bins emitted per workgroup (0: none)  // runs longer than cap (1..2048; other values: 2048) take the global path
 }  // namespace rr
