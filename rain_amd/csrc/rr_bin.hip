@@ -53,13 +53,12 @@ __device__ __forceinline__ void clear_words(uint32_t* __restrict__ zero, int nze
     for (int j = 4 * nv + i; j < nzero; j += nth) zero[j] = 0u;
 }
 
-// The samples: kCutChunks evenly spaced runs of 64 consecutive Gaussians (every Gaussian up to
-// kCutSamples): a wave's 64 lanes read one run's keys and pair counts as two contiguous 256-B and
+// The samples: NS / 64 evenly spaced runs of 64 consecutive Gaussians (every Gaussian up to
+// NS): a wave's 64 lanes read one run's keys and pair counts as two contiguous 256-B and
 // 512-B pieces, so the one workgroup gathers its 4096 samples from ~400 cache lines instead of ~8000
 // scattered ones (which took a separate many-workgroup launch: 4.4 us).  Runs of consecutive
 // indices are as good a sample as evenly spaced Gaussians here: the cut only steers the split's
 // balance, any cut gives the same lists.
-constexpr int kCutChunks = kCutSamples / 64;
 
 // The frame's totals (L, rect, wide: the preprocess block sums) and the depth cut, computed by one
 // workgroup of NT threads: k_early_cut (1024 threads, alone) or every workgroup of k_cut_totals
@@ -74,13 +73,15 @@ struct CutResult {
     unsigned long long L, rect;
     uint32_t wide, cut;  // cut: all ones for a one-phase frame
 };
-template <int NT>
+template <int NT, int NS = kCutSamples>
 __device__ __forceinline__ CutResult depth_cut(CutShared<NT>& sh, int P, const uint32_t* __restrict__ keys,
                                                const uint2* __restrict__ tiles, const uint2* __restrict__ block_sums,
                                                const uint32_t* __restrict__ block_wide, int nb, uint32_t den,
                                                uint32_t min_pairs) {
-    constexpr int SPT = kCutSamples / NT;  // samples per thread
-    constexpr int QB = SPT;                // block records per thread and round (all in flight)
+    static_assert(NS % NT == 0 && NS % 64 == 0 && NS <= kCutSamples, "samples: runs of 64, whole rounds");
+    constexpr int SPT = NS / NT;           // samples per thread
+    constexpr int QB = kCutSamples / NT;   // block records per thread and round (all in flight)
+    constexpr int NCH = NS / 64;           // runs of 64 consecutive Gaussians
     constexpr int NW = NT / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     for (int i = t; i < kCutBuckets; i += NT) sh.hist[i] = 0u;
@@ -93,10 +94,9 @@ __device__ __forceinline__ CutResult depth_cut(CutShared<NT>& sh, int P, const u
 #pragma unroll
     for (int r = 0; r < SPT; r++) {
         const int s = t + r * NT;
-        const int idx = P <= kCutSamples ? min(s, P - 1)
-                                         : min((int)(((long long)(s >> 6) * P) / kCutChunks) + (s & 63), P - 1);
+        const int idx = P <= NS ? min(s, P - 1) : min((int)(((long long)(s >> 6) * P) / NCH) + (s & 63), P - 1);
         sm[r] = make_uint2(keys[idx], tiles[idx].x);
-        if (P <= kCutSamples && s >= P) sm[r].y = 0u;
+        if (P <= NS && s >= P) sm[r].y = 0u;
     }
     unsigned long long L = 0, rect = 0, S = 0;
     uint32_t wide = 0;
@@ -265,7 +265,13 @@ __device__ __forceinline__ Quad quad_block_sum(Quad x, Quad* s) {
 }
 
 // CUT: the depth cut computed here by every workgroup (depth_cut<256>: the same cut in each) and
-// published by workgroup 0 — k_early_cut's job without its launch; else the cut from ft.
+// published by workgroup 0 — k_early_cut's job without its launch; else the cut from ft.  Each
+// workgroup samples kCutScanSamples Gaussians (16 runs of 64: the cut only steers the phases'
+// balance, and the per-workgroup histogram is 4x cheaper than k_early_cut's 4096 samples).
+#ifndef RR_CUT_SCAN_SAMPLES
+#define RR_CUT_SCAN_SAMPLES 1024
+#endif
+constexpr int kCutScanSamples = RR_CUT_SCAN_SAMPLES;
 template <bool CUT>
 __global__ __launch_bounds__(256) void k_split_scan_totals(const uint2* __restrict__ tiles,
                                                            const uint32_t* __restrict__ keys, int P,
@@ -273,22 +279,32 @@ __global__ __launch_bounds__(256) void k_split_scan_totals(const uint2* __restri
                                                            uint32_t* __restrict__ zero, int nzero, CutArgs ca) {
     __shared__ Quad s[4];
     __shared__ CutShared<CUT ? 256 : 64> sh;
+    // this block's items first: their loads overlap the cut's
+    constexpr int IPT = kPairScanItems / 256;
+    const size_t b0 = (size_t)blockIdx.x * kPairScanItems;
+    uint32_t in[IPT], ik[IPT];
+#pragma unroll
+    for (int r = 0; r < IPT; r++) {
+        const size_t i = b0 + (size_t)r * 256 + threadIdx.x;
+        in[r] = i < (size_t)P ? tiles[i].x : 0u;
+        ik[r] = i < (size_t)P ? keys[i] : 0u;
+    }
     uint32_t cut;
     if constexpr (CUT) {
-        const CutResult r = depth_cut<256>(sh, P, keys, tiles, ca.block_sums, ca.block_wide, (P + 255) / 256, ca.den,
-                                           ca.min_pairs);
+        const CutResult r = depth_cut<256, kCutScanSamples>(sh, P, keys, tiles, ca.block_sums, ca.block_wide,
+                                                            (P + 255) / 256, ca.den, ca.min_pairs);
         if (blockIdx.x == 0 && threadIdx.x == 0) publish_cut(r, ft, ca.box, ca.seq);
         cut = r.cut;
     } else {
         cut = ft->cut;
     }
     if (zero) clear_words(zero, nzero);
-    const size_t b0 = (size_t)blockIdx.x * kPairScanItems;
     Quad x{0, 0, 0, 0};
 #pragma unroll
-    for (int r = 0; r < kPairScanItems / 256; r++) {
-        const size_t i = b0 + (size_t)r * 256 + threadIdx.x;
-        if (i < (size_t)P) x = quad_add(x, split_item(tiles, keys, cut, i));
+    for (int r = 0; r < IPT; r++) {  // split_item's arithmetic on the prefetched values
+        const bool a = ik[r] < cut;
+        const uint32_t n = in[r];
+        x = quad_add(x, Quad{a ? n : 0ull, a ? 0ull : n, (a && n) ? 1ull : 0ull, (!a && n) ? 1ull : 0ull});
     }
     x = quad_block_sum(x, s);
     if (threadIdx.x == 0) tot[blockIdx.x] = x;
@@ -644,23 +660,37 @@ __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&k
             sh.v[pos] = vr[r];
         }
     __syncthreads();
-    // hist[b] is now bucket b's end, hist[b - 1] its start
-    for (int b = t; b < kSxBuckets; b += 256) {
-        const uint32_t s0 = b ? hist[b - 1] : 0u, e = hist[b];
-        for (uint32_t a = s0 + 1; a < e; a++) {
-            const uint32_t k = sh.k[a], v = sh.v[a];
-            uint32_t j = a;
-            while (j > s0) {
-                const uint32_t pk = sh.k[j - 1], pv = sh.v[j - 1];
-                if (pk < k || (pk == k && (pv & BIN_ID_MASK) < (v & BIN_ID_MASK))) break;
-                sh.k[j] = pk;
-                sh.v[j] = pv;
-                j--;
+    // hist[b] is now bucket b's end, hist[b - 1] its start.  Each item's place inside its bucket in
+    // parallel: its rank among the bucket's items on (depth key, Gaussian index) — a strict order,
+    // the indices of one bin being distinct — then every item written to its place.  (One thread
+    // insertion-sorting each bucket cost 17.5 us of the 90 us ranges stage: the buckets' lengths
+    // are skewed and the workgroup waits for the longest; profiles/r05_sortexpand_probe_ab.jsonl.)
+    uint32_t pk[kSxMaxR], pv[kSxMaxR], pr[kSxMaxR];
+#pragma unroll
+    for (int r = 0; r < kSxMaxR; r++) {
+        const uint32_t a = (uint32_t)t + 256u * (uint32_t)r;
+        pr[r] = 0xffffffffu;
+        if (r < R && a < len) {
+            const uint32_t k = sh.k[a], v = sh.v[a], vi = v & BIN_ID_MASK;
+            const uint32_t b = (k - kmin) >> shift;
+            const uint32_t s0 = b ? hist[b - 1] : 0u, e = hist[b];
+            uint32_t rank = s0;
+            for (uint32_t j = s0; j < e; j++) {
+                const uint32_t qk = sh.k[j];
+                rank += (qk < k || (qk == k && (sh.v[j] & BIN_ID_MASK) < vi)) ? 1u : 0u;
             }
-            sh.k[j] = k;
-            sh.v[j] = v;
+            pk[r] = k;
+            pv[r] = v;
+            pr[r] = rank;
         }
     }
+    __syncthreads();  // every read of the bucket order before the first write
+#pragma unroll
+    for (int r = 0; r < kSxMaxR; r++)
+        if (pr[r] != 0xffffffffu) {
+            sh.k[pr[r]] = pk[r];
+            sh.v[pr[r]] = pv[r];
+        }
     __syncthreads();
     return true;
 }
@@ -704,8 +734,13 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
         }
         bool sorted = false;
         if (bucket) {
+#ifdef RR_SX_TIMING_NO_GATHER  // timing experiment only (wrong order): the depth-key gathers' cost
+#pragma unroll
+            for (int r = 0; r < kSxMaxR; r++) kr[r] = vr[r] & BIN_ID_MASK;
+#else
 #pragma unroll
             for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
+#endif
             sorted = bucket_sort_run(sh, kr, vr, R, len);  // block-uniform
         }
         for (int attempt = 0; !sorted; attempt++) {

@@ -407,6 +407,9 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         return;
     }
     const int wb = (PHASE_B && order_out) ? (int)blockIdx.x - 1 : (int)blockIdx.x;
+    // list mode: the grid covers every Gaussian, the list only the phase's (block-uniform exit
+    // before the open-tile mask is staged)
+    if (list_idx && wb * 256 >= (int)*list_n) return;
     const bool mask_lds = PHASE_B && gx * gy <= 65536;
     __shared__ uint32_t s_open[PHASE_B ? 2048 : 1];
     __shared__ uint32_t wsum[4];

@@ -47,9 +47,17 @@ def main():
             lo = np.where(b[:, 1] > 0, 0xFFFFFFFF - b[:, 0], 0)  # {~start, end} (rr_kernels.hpp)
             n = b[:, 1] - lo
             q = {p: int(np.percentile(n, p)) for p in (50, 90, 99, 100)}
+            # where the long runs are: each bin's distance from the image centre (in bins,
+            # normalised by the half-diagonal), for the longest 2 % against all bins
+            bx, by = (gx + 1) // 2, (gy + 1) // 2
+            X, Y = np.meshgrid(np.arange(bx), np.arange(by))
+            dist = (np.hypot(X + 0.5 - bx / 2, Y + 0.5 - by / 2) / np.hypot(bx / 2, by / 2)).ravel()
+            top = np.argsort(n)[-max(1, len(n) // 50):]
             res[ph] = dict(sum=int(n.sum()), nonempty=int((n > 0).sum()), pct=q,
                            over_2048=int((n > 2048).sum()), over_4096=int((n > 4096).sum()),
-                           pairs_over_4096=int(n[n > 4096].sum()), top8=sorted(n.tolist())[-8:])
+                           pairs_over_4096=int(n[n > 4096].sum()), top8=sorted(n.tolist())[-8:],
+                           dist_all=round(float(dist.mean()), 3), dist_top2pct=round(float(dist[top].mean()), 3),
+                           corr_len_dist=round(float(np.corrcoef(n, dist)[0, 1]), 3))
         out[v] = res
     print(json.dumps(out, indent=1))
 

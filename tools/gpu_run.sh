@@ -65,6 +65,11 @@ for STEP in "$@"; do
         done
       done
       cat ${OUT}_ab.jsonl ;;
+    binstats)
+      # per-bin run lengths of three bench frames (tools/bin_stats.py)
+      timeout -k 10 300 python3 -u tools/bin_stats.py > ${OUT}_bin_stats.json 2> ${OUT}_bin_stats.err \
+        || { tail -20 ${OUT}_bin_stats.err; exit 1; }
+      cat ${OUT}_bin_stats.json ;;
     owner)
       # owner-kernel time of the Gaussian-sharded step by N (tools/owner_bench.py)
       timeout -k 10 400 python3 -u tools/owner_bench.py > ${OUT}_owner.jsonl 2> ${OUT}_owner.err \
