@@ -117,8 +117,8 @@ struct Img {
     uint32_t* open_bits;  // [ceil(T/32)] open as a bitmask (in the zeroed block; the phase-A blend sets it)
     uint2* bounds_a;      // [bins] phase A's (or the single phase's) bin runs (zeroed block; k_bin_bounds)
     uint2* bounds_b;      // [bins] phase B's
-    uint32_t* bin_cnt;    // [bins] phase B's pair count per bin (the gather path)
-    uint32_t* bin_cnt_a;  // [bins] phase A's
+    uint32_t* bin_cnt;    // [2 bins] phase B's pair count per bin (the gather path), then its fill
+    uint32_t* bin_cnt_a;  // [2 bins] phase A's
     uint32_t* order;      // [T] backward blend dispatch order (heaviest tiles first)
     size_t total;
 };
@@ -130,10 +130,10 @@ Img carve_img(void* buf, int W, int H) {
     m.final_T = c.take<float>(N);
     m.n_contrib = c.take<uint32_t>(N);
     // one block, cleared before every render: ranges [T], ranges_b [T], counters [4],
-    // open_bits [ceil(T/32)], bounds_a [bins], bounds_b [bins], bin_cnt [bins], bin_cnt_a [bins]
+    // open_bits [ceil(T/32)], bounds_a [bins], bounds_b [bins], bin_cnt [2 bins], bin_cnt_a [2 bins]
     const size_t nbits = ((size_t)T + 31) / 32;
     const size_t NB = (size_t)std::max(bins_x(grid_x(W)) * bins_y(grid_y(H)), 1);
-    const size_t nz = 2 * (size_t)T + 2 + (nbits + 1) / 2 + 2 * NB + 2 * ((NB + 1) / 2);
+    const size_t nz = 2 * (size_t)T + 2 + (nbits + 1) / 2 + 2 * NB + 2 * NB;
     m.ranges = c.take<uint2>(nz);
     m.ranges_b = m.ranges ? m.ranges + T : nullptr;
     m.counters = m.ranges ? reinterpret_cast<uint32_t*>(m.ranges + 2 * T) : nullptr;
@@ -141,7 +141,7 @@ Img carve_img(void* buf, int W, int H) {
     m.bounds_a = m.ranges ? m.ranges + 2 * T + 2 + (nbits + 1) / 2 : nullptr;
     m.bounds_b = m.ranges ? m.bounds_a + NB : nullptr;
     m.bin_cnt = m.ranges ? reinterpret_cast<uint32_t*>(m.bounds_b + NB) : nullptr;
-    m.bin_cnt_a = m.ranges ? m.bin_cnt + 2 * ((NB + 1) / 2) : nullptr;
+    m.bin_cnt_a = m.ranges ? m.bin_cnt + 2 * NB : nullptr;
     m.zero_bytes = nz * sizeof(uint2);
     m.tile_max = c.take<uint32_t>(T);
     m.open = c.take<uint8_t>(T);

@@ -588,7 +588,10 @@ __device__ __forceinline__ bool fix_ties(uint32_t len, KeyAt key_at, ValAt val_a
 // than kSxBucketMax items (strongly clustered depths, many exact copies): the caller then sorts
 // with the LSD passes.
 constexpr int kSxBuckets = 2048;  // = the 4 x 512 per-wave digit counters of SxShared
-constexpr uint32_t kSxBucketMax = 16;
+#ifndef RR_SX_BUCKET_MAX
+#define RR_SX_BUCKET_MAX 16
+#endif
+constexpr uint32_t kSxBucketMax = RR_SX_BUCKET_MAX;
 int g_sx_bucket = 1;  // rr_set_tuning "sx_bucket"
 int g_sx_lds_cap = kSxCap;  // rr_set_tuning "sx_lds_cap": longer runs take the global path (tests)
 uint32_t sx_lds_cap() { return (uint32_t)g_sx_lds_cap; }
@@ -903,11 +906,12 @@ __device__ __forceinline__ void report_phase_b(uint32_t* box, uint32_t n) {
     __hip_atomic_store(box + 5, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Phase B of the gather path (k_duplicate_b_gather emitted its pairs densely, [0, n), in no
-// particular order): k_bin_count counts them per bin, k_bin_scan turns the counts into every bin's
-// run (bounds) and a cursor, k_bin_scatter drops each pair's value into its bin's run (order inside a
-// bin arbitrary: k_sortexpand restores (depth, index) order).  Three launches instead of the bin
-// sort's five and the bounds launch.  Count and scatter run kBinGroups workgroups over the same
+// Phase B of the gather path (k_dup_gather emitted its pairs densely, [0, n), in no particular
+// order): k_bin_count counts them per bin, k_bin_scatter turns the counts into every bin's run
+// (bounds) and drops each pair's value into its bin's run (order inside a bin arbitrary:
+// k_sortexpand restores (depth, index) order).  Two launches instead of the bin sort's five and the
+// bounds launch (a separate one-workgroup scan launch between them until round 5).  Count and
+// scatter run kBinGroups workgroups over the same
 // strided item sets; each aggregates its items per bin in LDS, so a global atomic is paid per
 // (workgroup, bin) and not per pair (per-pair atomics on a few hot bins serialise: +40 us).
 constexpr int kBinScanMax = 16384;  // bins one workgroup holds (4K frames: 8160)
@@ -932,11 +936,27 @@ __global__ __launch_bounds__(1024) void k_bin_count(const void* __restrict__ key
         if (h[b]) atomicAdd(&bin_cnt[b], h[b]);
 }
 
-__global__ __launch_bounds__(1024) void k_bin_scan(int nb, const uint32_t* __restrict__ n_dev,
-                                                   uint32_t* __restrict__ bin_cnt, uint2* __restrict__ bounds) {
+// The bins' runs and the scatter in one launch: every workgroup scans the final per-bin counts
+// itself (bin_cnt[0, nb): k_bin_count's), workgroup 0 writes the runs (bounds), and each workgroup
+// reserves its slots of each bin with an atomic on the zeroed fill counters bin_cnt[nb, 2 nb) —
+// the one-workgroup scan launch between count and scatter is gone.
+__global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ keys_v, int wide_keys,
+                                                      const uint32_t* __restrict__ vals,
+                                                      const uint32_t* __restrict__ n_dev, int nb,
+                                                      uint32_t* __restrict__ bin_cnt, uint2* __restrict__ bounds,
+                                                      uint32_t* __restrict__ vals_out) {
+    __shared__ uint32_t h[kBinScanMax];
+    __shared__ uint32_t s_start[kBinScanMax];
     __shared__ uint32_t wsum[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (*n_dev == 0) return;  // no pairs: the zeroed bounds already say so
+    const uint32_t n = *n_dev;
+    const uint32_t per = (n + kBinGroups - 1) / kBinGroups;
+    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    if (i0 >= i1) return;  // (n == 0: the zeroed bounds already say so)
+    auto key = [&](uint32_t i) -> uint32_t {
+        return wide_keys ? static_cast<const uint32_t*>(keys_v)[i] : static_cast<const uint16_t*>(keys_v)[i];
+    };
+    // exclusive scan of the counts: thread t owns bins [kPer t, kPer t + kPer)
     constexpr int kPer = kBinScanMax / 1024;
     const int b0 = t * kPer;
     uint32_t c[kPer], sum = 0;
@@ -945,6 +965,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int nb, const uint32_t* __res
         c[k] = b0 + k < nb ? bin_cnt[b0 + k] : 0u;
         sum += c[k];
     }
+    for (int b = t; b < nb; b += 1024) h[b] = 0u;
     uint32_t incl = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -958,32 +979,15 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int nb, const uint32_t* __res
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
         if (b0 + k < nb) {
-            bounds[b0 + k] = make_uint2(~run, run + c[k]);  // {~start, end}
-            bin_cnt[b0 + k] = run;  // the bin's next free slot
+            s_start[b0 + k] = run;
+            if (blockIdx.x == 0) bounds[b0 + k] = make_uint2(~run, run + c[k]);  // {~start, end}
         }
         run += c[k];
     }
-}
-
-__global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ keys_v, int wide_keys,
-                                                      const uint32_t* __restrict__ vals,
-                                                      const uint32_t* __restrict__ n_dev, int nb,
-                                                      uint32_t* __restrict__ bin_cur, uint32_t* __restrict__ vals_out) {
-    __shared__ uint32_t h[kBinScanMax];
-    const int t = threadIdx.x;
-    const uint32_t n = *n_dev;
-    const uint32_t per = (n + kBinGroups - 1) / kBinGroups;
-    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
-    if (i0 >= i1) return;
-    auto key = [&](uint32_t i) -> uint32_t {
-        return wide_keys ? static_cast<const uint32_t*>(keys_v)[i] : static_cast<const uint16_t*>(keys_v)[i];
-    };
-    for (int b = t; b < nb; b += 1024) h[b] = 0u;
-    __syncthreads();
     for (uint32_t i = i0 + t; i < i1; i += 1024) atomicAdd(&h[key(i)], 1u);
     __syncthreads();
     for (int b = t; b < nb; b += 1024)  // this workgroup's slots of each bin
-        if (h[b]) h[b] = atomicAdd(&bin_cur[b], h[b]);
+        if (h[b]) h[b] = s_start[b] + atomicAdd(&bin_cnt[nb + b], h[b]);
     __syncthreads();
     for (uint32_t i = i0 + t; i < i1; i += 1024) {
         const uint32_t k = key(i), v = vals[i];
@@ -1070,8 +1074,7 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
     if (nb <= 0 || nb > kBinScanMax) return false;
     const int wk = sizeof(K) == 4;
     k_bin_count<<<kBinGroups, 1024, 0, st>>>(keys, wk, n_dev, nb, bin_cnt);
-    k_bin_scan<<<1, 1024, 0, st>>>(nb, n_dev, bin_cnt, bounds);
-    k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, vals_sorted);
+    k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, bounds, vals_sorted);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
                                         open_bits, sx_lds_cap(), n_dev, report, index_passes(P), out_base_dev,
                                         g_sx_bucket);
