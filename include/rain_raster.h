@@ -413,6 +413,8 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *   "sx_lds_cap" n        per-bin runs of more than n pairs (1..2048, default 2048) depth-sorted
  *                         through their own point_list region instead of LDS,
  *   "forward_clear" 0/1   rr_set_forward_workspace registrations honoured (default 1) or dropped,
+ *   "dup_b_reserve" 0/1   phase-B gather: one walk per Gaussian with its pair count reserved as an
+ *                         upper bound (default 1) or a counting walk first,
  *   "dup_big_bins" n      phase-B gather: Gaussians spanning more than n bins (default 32) emitted
  *                         by their whole workgroup, 256 bins at a time; 0: each by its own thread,
  *   "cut_in_scan" 0/1     the early-stop depth cut computed by every workgroup of the split scan's

@@ -714,7 +714,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
             launch_sortexpand_small<K>(P, keys + offB, bn.vals + offB, im.counters, im.bin_cnt, bn.vals_sorted + offB,
                                        gm.depth_keys, gm.ft, gx, gy, bn.compact ? 0u : 4u * L, bn.point_list,
                                        im.ranges_b, im.open_bits, im.bounds_b, report, st,
-                                       bn.compact ? im.counters + 2 : nullptr);
+                                       bn.compact ? im.counters + 2 : nullptr, im.counters + 3);
         }
         RR_STAGE_CHECK("sort-expand (phase B gather)");
     } else {
@@ -1246,7 +1246,9 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     RR_CHECK(hipMemcpyAsync(&ft, gm.ft, sizeof(ft), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(per.data(), gm.tiles, (size_t)P * sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
-    uint32_t cnt[4] = {0u, 0u, 0u, 0u};  // [0] phase-B pairs, [2] phase-A pairs of the gather path
+    // [0] phase-B pairs (the gather path: slots reserved), [2] phase-A pairs of the gather path,
+    // [3] phase-B pairs the gather path's bin runs hold
+    uint32_t cnt[4] = {0u, 0u, 0u, 0u};
     RR_CHECK(hipMemcpyAsync(cnt, im.counters, sizeof(cnt), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipStreamSynchronize(st), "stats");
     int64_t vis = 0;
@@ -1260,7 +1262,8 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     // phase A's pairs, and the phase-B pairs kept for the tiles phase A left open (the binning path
     // the frame took: the tuning in force now, as at its render)
     const bool gather_a = g_a_gather && gather_bins_fit(W, H);
-    out->num_binned = (gather_a ? (int64_t)cnt[2] : (int64_t)ft.LA) + cnt[0];
+    const bool gather_b = phase_b_gather() && gather_bins_fit(W, H);
+    out->num_binned = (gather_a ? (int64_t)cnt[2] : (int64_t)ft.LA) + (gather_b ? cnt[3] : cnt[0]);
     return RR_OK;
 }
 
@@ -1303,6 +1306,10 @@ int rr_set_forward_workspace(void* workspace, size_t bytes) {
 int rr_set_tuning(const char* key, int value) {
     if (key && std::string(key) == "early_den") {  // early-stop split: phase A ~1/den of the pairs
         g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
+        return RR_OK;
+    }
+    if (key && std::string(key) == "dup_b_reserve") {
+        set_dup_b_reserve(value != 0);
         return RR_OK;
     }
     if (key && std::string(key) == "dup_big_bins") {

@@ -927,9 +927,9 @@ __global__ __launch_bounds__(1024) void k_bin_count(const void* __restrict__ key
     if (i0 >= i1) return;
     for (int b = t; b < nb; b += 1024) h[b] = 0u;
     __syncthreads();
-    for (uint32_t i = i0 + t; i < i1; i += 1024) {
+    for (uint32_t i = i0 + t; i < i1; i += 1024) {  // keys >= nb: the duplicate's unused reserved slots
         const uint32_t k = wide_keys ? static_cast<const uint32_t*>(keys_v)[i] : static_cast<const uint16_t*>(keys_v)[i];
-        atomicAdd(&h[k], 1u);
+        if (k < (uint32_t)nb) atomicAdd(&h[k], 1u);
     }
     __syncthreads();
     for (int b = t; b < nb; b += 1024)
@@ -944,7 +944,7 @@ __global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ k
                                                       const uint32_t* __restrict__ vals,
                                                       const uint32_t* __restrict__ n_dev, int nb,
                                                       uint32_t* __restrict__ bin_cnt, uint2* __restrict__ bounds,
-                                                      uint32_t* __restrict__ vals_out) {
+                                                      uint32_t* __restrict__ vals_out, uint32_t* __restrict__ kept) {
     __shared__ uint32_t h[kBinScanMax];
     __shared__ uint32_t s_start[kBinScanMax];
     __shared__ uint32_t wsum[16];
@@ -984,14 +984,18 @@ __global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ k
         }
         run += c[k];
     }
-    for (uint32_t i = i0 + t; i < i1; i += 1024) atomicAdd(&h[key(i)], 1u);
+    if (kept && blockIdx.x == 0 && t == 1023) *kept = run;  // the pairs the bins hold (frame stats)
+    for (uint32_t i = i0 + t; i < i1; i += 1024) {
+        const uint32_t k = key(i);
+        if (k < (uint32_t)nb) atomicAdd(&h[k], 1u);
+    }
     __syncthreads();
     for (int b = t; b < nb; b += 1024)  // this workgroup's slots of each bin
         if (h[b]) h[b] = s_start[b] + atomicAdd(&bin_cnt[nb + b], h[b]);
     __syncthreads();
     for (uint32_t i = i0 + t; i < i1; i += 1024) {
-        const uint32_t k = key(i), v = vals[i];
-        vals_out[atomicAdd(&h[k], 1u)] = v;
+        const uint32_t k = key(i);
+        if (k < (uint32_t)nb) vals_out[atomicAdd(&h[k], 1u)] = vals[i];
     }
 }
 
@@ -1069,12 +1073,13 @@ template <typename K>
 bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
-                             uint2* bounds, uint32_t* report, hipStream_t st, const uint32_t* out_base_dev) {
+                             uint2* bounds, uint32_t* report, hipStream_t st, const uint32_t* out_base_dev,
+                             uint32_t* kept) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0 || nb > kBinScanMax) return false;
     const int wk = sizeof(K) == 4;
     k_bin_count<<<kBinGroups, 1024, 0, st>>>(keys, wk, n_dev, nb, bin_cnt);
-    k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, bounds, vals_sorted);
+    k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, bounds, vals_sorted, kept);
     k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
                                         open_bits, sx_lds_cap(), n_dev, report, index_passes(P), out_base_dev,
                                         g_sx_bucket);
@@ -1083,10 +1088,10 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
 template bool launch_sortexpand_small<uint16_t>(int, const uint16_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
                                                 uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t,
-                                                const uint32_t*);
+                                                const uint32_t*, uint32_t*);
 template bool launch_sortexpand_small<uint32_t>(int, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
                                                 uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t,
-                                                const uint32_t*);
+                                                const uint32_t*, uint32_t*);
 
 }  // namespace rr

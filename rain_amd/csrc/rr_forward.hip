@@ -385,8 +385,10 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
 // "dup_big_bins", 0: none) are emitted by their whole workgroup, 256 bins at a time.
 namespace {
 int g_dup_big_bins = 32;
+int g_dup_b_reserve = 1;  // rr_set_tuning "dup_b_reserve": phase B reserves the pair count (one walk)
 }
 void set_dup_big_bins(int n) { g_dup_big_bins = n >= 0 ? n : 32; }
+void set_dup_b_reserve(bool on) { g_dup_b_reserve = on ? 1 : 0; }
 template <typename K, bool PHASE_B>
 __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restrict__ tiles,
                                                     const uint32_t* __restrict__ depth_keys,
@@ -400,7 +402,8 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
                                                     uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ order_flag, int order_T,
                                                     const uint32_t* __restrict__ list_n,
-                                                    const uint32_t* __restrict__ list_idx, int big_bins) {
+                                                    const uint32_t* __restrict__ list_idx, int big_bins,
+                                                    int reserve_n) {
     if (PHASE_B && order_out && blockIdx.x == 0) {
         tile_order_body256(order_T, order_cost, open_bits, order_out);
         if (threadIdx.x == 0) *order_flag = (uint32_t)order_T;
@@ -501,6 +504,9 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
     auto walk = [&](bool emit, uint32_t pos, uint32_t cap) {
         uint32_t c = 0;
         for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && c < cap; Y++) {
+            // phase B: a bin row whose two tile rows hold no open tile in [x0, x1) emits nothing
+            // (skipped before its culling spans are evaluated)
+            if (PHASE_B && !rect_open(x0, max(2 * Y, y0), x1, min(2 * Y + 2, y1))) continue;
             int l0, h0, l1, h1, Xa, Xb;
             bin_row_spans(ell, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
             bin_cols(l0, h0, l1, h1, Xa, Xb);
@@ -517,7 +523,10 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         }
         return c;
     };
-    if (live) cnt = PHASE_B ? walk(false, 0u, 0xffffffffu) : n;
+    // phase B: the kept pairs counted by a first walk, or (reserve_n) the Gaussian's pair count
+    // reserved as an upper bound, the slots the one walk leaves filled with a key past the last bin
+    // (the bin count and scatter skip them): one walk per Gaussian instead of two
+    if (live) cnt = (PHASE_B && !reserve_n) ? walk(false, 0u, 0xffffffffu) : n;
     // the workgroup's kept pairs: wave prefix sums, one reservation
     uint32_t incl = cnt;
 #pragma unroll
@@ -541,8 +550,9 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
             // phase A: the walk and the preprocess's count are the same closed form on the same
             // record (rr_preprocess.hpp); should they ever disagree, the reserved slots left over get
             // an empty tile mask, which the per-bin split writes to no tile list
+            const K fill = (PHASE_B && reserve_n) ? (K)(bgx * bins_y(gy)) : (K)0;
             for (uint32_t c = walk(true, pos, cnt); c < cnt; c++) {
-                keys[pos + c] = (K)0;
+                keys[pos + c] = fill;
                 vals[pos + c] = g;
             }
         }
@@ -666,14 +676,14 @@ void launch_dup_gather(const DupArgs<K>& d, bool phase_b, hipStream_t st) {
         k_dup_gather<K, false><<<blocks_for(d.P), 256, 0, st>>>(d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii,
                                                                  d.gx, d.gy, d.cull, d.keys, d.vals, nullptr,
                                                                  d.n_total, nullptr, nullptr, nullptr, 0,
-                                                                 d.idx ? d.n_list : nullptr, d.idx, 0);
+                                                                 d.idx ? d.n_list : nullptr, d.idx, 0, 0);
         return;
     }
     const bool ord = d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
     k_dup_gather<K, true><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
         d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits,
         d.n_total, ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T,
-        d.idx ? d.n_list : nullptr, d.idx, g_dup_big_bins);
+        d.idx ? d.n_list : nullptr, d.idx, g_dup_big_bins, g_dup_b_reserve);
 }
 template void launch_dup_gather<uint16_t>(const DupArgs<uint16_t>&, bool, hipStream_t);
 template void launch_dup_gather<uint32_t>(const DupArgs<uint32_t>&, bool, hipStream_t);

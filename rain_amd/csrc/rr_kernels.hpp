@@ -236,7 +236,8 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
                              uint2* bounds, uint32_t* report, hipStream_t st,
-                             const uint32_t* out_base_dev = nullptr);  // lists at out_base + 4 * *out_base_dev
+                             const uint32_t* out_base_dev = nullptr,  // lists at out_base + 4 * *out_base_dev
+                             uint32_t* kept = nullptr);  // receives the pairs the bins hold
 template <typename K>
 struct DupArgs {
     int P;                       // capacity of the lists (the frame's Gaussians)
@@ -373,5 +374,6 @@ void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hi
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
 void set_sx_bucket(bool on);  // rr_bin.hip: per-bin bucket sort (default) or LSD passes only
 void set_sx_lds_cap(int cap);
-void set_dup_big_bins(int n);  // rr_forward.hip: phase-B Gaussians over n bins emitted per workgroup (0: none)  // runs longer than cap (1..2048; other values: 2048) take the global path
+void set_dup_big_bins(int n);
+void set_dup_b_reserve(bool on);  // phase-B gather: one walk, the pair count reserved (fill keys skipped)  // rr_forward.hip: phase-B Gaussians over n bins emitted per workgroup (0: none)  // runs longer than cap (1..2048; other values: 2048) take the global path
 }  // namespace rr

@@ -38,6 +38,7 @@ PATHS = {
     "global_runs_windowed_b": {"sx_lds_cap": (64, 0), "phase_b_gather": (0, 1), "sx_bucket": (0, 1)},
     "cut_kernel": {"cut_in_scan": (0, 1)},  # the depth cut by its own one-workgroup launch
     "dup_big_serial": {"dup_big_bins": (0, 32)},  # every phase-B Gaussian by its own thread
+    "dup_b_count_walk": {"dup_b_reserve": (0, 1)},  # phase B counts its kept pairs first
     "dup_big_all": {"dup_big_bins": (1, 32)},  # every phase-B Gaussian of > 1 bin per workgroup
     "window_starts_launch": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16),
                              "phase_b_gather": (0, 1), "split_marks": (0, 1)},
