@@ -410,6 +410,7 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *   "bounds_in_sort" 0/1  windowed paths: bin runs from the bin sort's last scatter (default 1),
  *   "split_marks" 0/1     windowed duplicate: window starts marked by the split scan when the
  *                         sort unit is 2048 pairs (default 1) or computed by their own launch,
+ *   "sx_b_threads" n      phase B's per-bin sort-expand workgroup: 1024 threads (default) or 256,
  *   "sx_lds_cap" n        per-bin runs of more than n pairs (1..2048, default 2048) depth-sorted
  *                         through their own point_list region instead of LDS,
  *   "forward_clear" 0/1   rr_set_forward_workspace registrations honoured (default 1) or dropped,

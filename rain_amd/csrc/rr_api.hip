@@ -1308,6 +1308,10 @@ int rr_set_tuning(const char* key, int value) {
         g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
         return RR_OK;
     }
+    if (key && std::string(key) == "sx_b_threads") {
+        set_sx_b_threads(value);
+        return RR_OK;
+    }
     if (key && std::string(key) == "dup_b_reserve") {
         set_dup_b_reserve(value != 0);
         return RR_OK;

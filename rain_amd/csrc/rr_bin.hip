@@ -444,17 +444,19 @@ void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLis
 #define RR_SX_CAP 2048  // 4096: ranges stage 0.110 vs 0.095 ms/step (profiles/r04h_sortexpand_cap_ab.jsonl)
 #endif
 constexpr int kSxCap = RR_SX_CAP;
-constexpr int kSxMaxR = kSxCap / 256;
+constexpr int kSxMaxR = kSxCap / 256;  // rounds of 64 items per wave at 256 threads (NT threads: kSxCap / NT)
 #ifndef RR_SX_GLOBAL
 #define RR_SX_GLOBAL 1  // 0: ISA inspection builds without the long-run path
 #endif
 
-struct SxShared {
+// NW waves per workgroup (4: 256 threads; 16: the 1024-thread phase-B sort-expand)
+template <int NW>
+struct SxSharedT {
     uint32_t k[kSxCap];
     uint32_t v[kSxCap];
-    uint32_t wcnt[4][512];  // per-wave digit counts, then per-wave cursors
-    uint32_t cursor[512];   // global path: next slot of each digit across the chunks
-    uint32_t wsum[4][4];
+    uint32_t wcnt[NW][512];  // per-wave digit counts, then per-wave cursors (>= the 2048 buckets)
+    uint32_t cursor[512];    // global path: next slot of each digit across the chunks
+    uint32_t wsum[NW][4];
 };
 
 // One chunk's items (registers kr / vr, R rounds, `len` valid) ranked on digit (key >> shift) & mask
@@ -462,9 +464,11 @@ struct SxShared {
 // (dst_lds) or to a global scratch run (dst_g).  base: the digit's first slot (LDS path: the
 // chunk's exclusive digit prefix; global path: cursor[d]).  Ends with the chunk's digit counts
 // added to cursor (global path).
-__device__ __forceinline__ void sx_rank_chunk(SxShared& sh, const uint32_t (&kr)[kSxMaxR],
-                                              const uint32_t (&vr)[kSxMaxR], int R, uint32_t len, int shift, int db,
-                                              bool global, uint2* dst_g) {
+template <int NT>
+__device__ __forceinline__ void sx_rank_chunk(SxSharedT<NT / 64>& sh, const uint32_t (&kr)[kSxCap / NT],
+                                              const uint32_t (&vr)[kSxCap / NT], int R, uint32_t len, int shift,
+                                              int db, bool global, uint2* dst_g) {
+    constexpr int MR = kSxCap / NT, NW = NT / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int ndig = 1 << db;
     const uint32_t mask = (uint32_t)ndig - 1u;
@@ -472,7 +476,7 @@ __device__ __forceinline__ void sx_rank_chunk(SxShared& sh, const uint32_t (&kr)
     for (int d = lane; d < ndig; d += 64) sh.wcnt[w][d] = 0;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < kSxMaxR; r++)
+    for (int r = 0; r < MR; r++)
         if (r < R && wl + (uint32_t)r * 64 + lane < len) atomicAdd(&sh.wcnt[w][(kr[r] >> shift) & mask], 1u);
     __syncthreads();
     if (w == 0) {  // digits in order, waves in order inside a digit (DPL consecutive digits per lane)
@@ -480,7 +484,8 @@ __device__ __forceinline__ void sx_rank_chunk(SxShared& sh, const uint32_t (&kr)
         uint32_t sum = 0;
         for (int i = 0; i < dpl; i++) {
             const int d = dpl * lane + i;
-            sum += sh.wcnt[0][d] + sh.wcnt[1][d] + sh.wcnt[2][d] + sh.wcnt[3][d];
+#pragma unroll
+            for (int v = 0; v < NW; v++) sum += sh.wcnt[v][d];
         }
         uint32_t incl = sum;
 #pragma unroll
@@ -493,7 +498,7 @@ __device__ __forceinline__ void sx_rank_chunk(SxShared& sh, const uint32_t (&kr)
             const int d = dpl * lane + i;
             uint32_t r2 = global ? sh.cursor[d] : run, tot = 0;
 #pragma unroll
-            for (int v = 0; v < 4; v++) {
+            for (int v = 0; v < NW; v++) {
                 const uint32_t x = sh.wcnt[v][d];
                 sh.wcnt[v][d] = r2;
                 r2 += x;
@@ -506,7 +511,7 @@ __device__ __forceinline__ void sx_rank_chunk(SxShared& sh, const uint32_t (&kr)
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int r = 0; r < kSxMaxR; r++) {
+    for (int r = 0; r < MR; r++) {
         if (r >= R || wl + (uint32_t)r * 64 >= len) continue;  // wave-uniform
         const bool valid = wl + (uint32_t)r * 64 + lane < len;
         const uint32_t d = (kr[r] >> shift) & mask;
@@ -553,10 +558,10 @@ __global__ __launch_bounds__(256) void k_bin_bounds(uint32_t n_host, const uint3
 // Gaussian-index order in place, one thread per group (groups are clones at one position: a few
 // items).  Returns true when a group longer than kTieMax was left for a full index-pass sort.
 constexpr uint32_t kTieMax = 32;
-template <typename KeyAt, typename ValAt, typename SetVal>
+template <int NT, typename KeyAt, typename ValAt, typename SetVal>
 __device__ __forceinline__ bool fix_ties(uint32_t len, KeyAt key_at, ValAt val_at, SetVal set_val) {
     bool big = false;
-    for (uint32_t i = threadIdx.x; i + 1 < len; i += 256) {
+    for (uint32_t i = threadIdx.x; i + 1 < len; i += NT) {
         const uint32_t k = key_at(i);
         if (key_at(i + 1) != k || (i > 0 && key_at(i - 1) == k)) continue;  // not a group's first item
         uint32_t j = i + 2;
@@ -594,15 +599,18 @@ constexpr int kSxBuckets = 2048;  // = the 4 x 512 per-wave digit counters of Sx
 constexpr uint32_t kSxBucketMax = RR_SX_BUCKET_MAX;
 int g_sx_bucket = 1;  // rr_set_tuning "sx_bucket"
 int g_sx_lds_cap = kSxCap;  // rr_set_tuning "sx_lds_cap": longer runs take the global path (tests)
+int g_sx_b_threads = 1024;  // rr_set_tuning "sx_b_threads": phase B's sort-expand workgroup (256 / 1024)
 uint32_t sx_lds_cap() { return (uint32_t)g_sx_lds_cap; }
-__device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&kr)[kSxMaxR],
-                                                const uint32_t (&vr)[kSxMaxR], int R, uint32_t len) {
+template <int NT>
+__device__ __forceinline__ bool bucket_sort_run(SxSharedT<NT / 64>& sh, const uint32_t (&kr)[kSxCap / NT],
+                                                const uint32_t (&vr)[kSxCap / NT], int R, uint32_t len) {
+    constexpr int MR = kSxCap / NT, NW = NT / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t wl = (uint32_t)w * 64 * R;
     uint32_t* hist = &sh.wcnt[0][0];
     uint32_t kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
-    for (int r = 0; r < kSxMaxR; r++)
+    for (int r = 0; r < MR; r++)
         if (r < R && wl + (uint32_t)r * 64 + lane < len) {
             kmin = min(kmin, kr[r]);
             kmax = max(kmax, kr[r]);
@@ -616,22 +624,25 @@ __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&k
         sh.wsum[w][0] = kmin;
         sh.wsum[w][1] = kmax;
     }
-    for (int i = t; i < kSxBuckets; i += 256) hist[i] = 0u;
+    for (int i = t; i < kSxBuckets; i += NT) hist[i] = 0u;
     __syncthreads();
-    kmin = min(min(sh.wsum[0][0], sh.wsum[1][0]), min(sh.wsum[2][0], sh.wsum[3][0]));
-    kmax = max(max(sh.wsum[0][1], sh.wsum[1][1]), max(sh.wsum[2][1], sh.wsum[3][1]));
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        kmin = min(kmin, sh.wsum[i][0]);
+        kmax = max(kmax, sh.wsum[i][1]);
+    }
     const uint32_t span = kmax - kmin;
     // (span >> shift) < kSxBuckets
     const int shift = span < (uint32_t)kSxBuckets ? 0 : 32 - __clz((int)span) - 11;
-    uint32_t bk[kSxMaxR];
+    uint32_t bk[MR];
 #pragma unroll
-    for (int r = 0; r < kSxMaxR; r++) {
+    for (int r = 0; r < MR; r++) {
         bk[r] = (kr[r] - kmin) >> shift;
         if (r < R && wl + (uint32_t)r * 64 + lane < len) atomicAdd(&hist[bk[r]], 1u);
     }
     __syncthreads();
-    // exclusive bucket starts: thread t owns buckets [8t, 8t + 8)
-    constexpr int BPT = kSxBuckets / 256;
+    // exclusive bucket starts: thread t owns buckets [BPT t, BPT t + BPT)
+    constexpr int BPT = kSxBuckets / NT;
     uint32_t c[BPT], sum = 0, mx = 0;
 #pragma unroll
     for (int k = 0; k < BPT; k++) {
@@ -656,7 +667,7 @@ __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&k
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kSxMaxR; r++)
+    for (int r = 0; r < MR; r++)
         if (r < R && wl + (uint32_t)r * 64 + lane < len) {
             const uint32_t pos = atomicAdd(&hist[bk[r]], 1u);
             sh.k[pos] = kr[r];
@@ -668,10 +679,10 @@ __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&k
     // the indices of one bin being distinct — then every item written to its place.  (One thread
     // insertion-sorting each bucket cost 17.5 us of the 90 us ranges stage: the buckets' lengths
     // are skewed and the workgroup waits for the longest; profiles/r05_sortexpand_probe_ab.jsonl.)
-    uint32_t pk[kSxMaxR], pv[kSxMaxR], pr[kSxMaxR];
+    uint32_t pk[MR], pv[MR], pr[MR];
 #pragma unroll
-    for (int r = 0; r < kSxMaxR; r++) {
-        const uint32_t a = (uint32_t)t + 256u * (uint32_t)r;
+    for (int r = 0; r < MR; r++) {
+        const uint32_t a = (uint32_t)t + (uint32_t)NT * (uint32_t)r;
         pr[r] = 0xffffffffu;
         if (r < R && a < len) {
             const uint32_t k = sh.k[a], v = sh.v[a], vi = v & BIN_ID_MASK;
@@ -689,7 +700,7 @@ __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&k
     }
     __syncthreads();  // every read of the bucket order before the first write
 #pragma unroll
-    for (int r = 0; r < kSxMaxR; r++)
+    for (int r = 0; r < MR; r++)
         if (pr[r] != 0xffffffffu) {
             sh.k[pr[r]] = pk[r];
             sh.v[pr[r]] = pv[r];
@@ -704,11 +715,14 @@ __device__ __forceinline__ bool bucket_sort_run(SxShared& sh, const uint32_t (&k
 // through global scratch: the run's own output region of point_list (4 slots per pair = two uint2
 // arrays of len), with the sorted values put back into vals[lo, lo + len) before the tile split
 // overwrites that region — no scratch arrays in the binning buffer.
-__device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int gx, int gy, uint32_t lo, uint32_t len,
+template <int NT>
+__device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64>& sh, int X, int Y, int gx, int gy, uint32_t lo,
+                                               uint32_t len,
                                                const uint32_t* __restrict__ vals, bool lds_vals,
                                                const uint32_t* __restrict__ depth_keys, bool wide, int ipasses,
                                                uint32_t out_base, uint32_t* __restrict__ point_list,
                                                uint2* __restrict__ ranges, uint32_t lds_cap, bool bucket) {
+    constexpr int MR = kSxCap / NT, NW = NT / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // The depth key: 27 bits in 3 passes of 9, wider frames in 4 of 8.  A run in no particular order
     // (ipasses > 0: the phase-B pairs of the gather path) needs index order among equal depth keys:
@@ -721,41 +735,41 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
     auto key_of = [&](int p, uint32_t v) { return p < ip ? (v & BIN_ID_MASK) : depth_keys[v & BIN_ID_MASK]; };
     bool global = false;  // the sorted run is back in vals[lo, lo + len)
     if (len > 1 && len <= lds_cap) {
-        const int R = (int)((len + 255) / 256);
+        const int R = (int)((len + NT - 1) / NT);
         const uint32_t wl = (uint32_t)w * 64 * R;
-        uint32_t kr[kSxMaxR], vr[kSxMaxR];
+        uint32_t kr[MR], vr[MR];
         // every round's loads unconditional, the index clamped into the run: a condition (per lane or
         // on R) made the compiler branch and wait around each load; the clamped extra loads hit the
         // cache line of the run's last item and are never used (items past len are not ranked)
         if (lds_vals) {  // gathered into sh.v by the caller
 #pragma unroll
-            for (int r = 0; r < kSxMaxR; r++) vr[r] = sh.v[min(wl + (uint32_t)r * 64 + lane, len - 1)];
+            for (int r = 0; r < MR; r++) vr[r] = sh.v[min(wl + (uint32_t)r * 64 + lane, len - 1)];
             __syncthreads();  // every read of the gathered run before the first pass writes sh.v
         } else {
 #pragma unroll
-            for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + min(wl + (uint32_t)r * 64 + lane, len - 1)];
+            for (int r = 0; r < MR; r++) vr[r] = vals[lo + min(wl + (uint32_t)r * 64 + lane, len - 1)];
         }
         bool sorted = false;
         if (bucket) {
 #ifdef RR_SX_TIMING_NO_GATHER  // timing experiment only (wrong order): the depth-key gathers' cost
 #pragma unroll
-            for (int r = 0; r < kSxMaxR; r++) kr[r] = vr[r] & BIN_ID_MASK;
+            for (int r = 0; r < MR; r++) kr[r] = vr[r] & BIN_ID_MASK;
 #else
 #pragma unroll
-            for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
+            for (int r = 0; r < MR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
 #endif
-            sorted = bucket_sort_run(sh, kr, vr, R, len);  // block-uniform
+            sorted = bucket_sort_run<NT>(sh, kr, vr, R, len);  // block-uniform
         }
         for (int attempt = 0; !sorted; attempt++) {
             const int passes = ip + (wide ? 4 : 3);
 #pragma unroll
-            for (int r = 0; r < kSxMaxR; r++) kr[r] = key_of(0, vr[r]);  // all gathers in flight
+            for (int r = 0; r < MR; r++) kr[r] = key_of(0, vr[r]);  // all gathers in flight
             for (int p = 0; p < passes; p++) {
-                sx_rank_chunk(sh, kr, vr, R, len, shift_of(p), db_of(p), false, nullptr);
+                sx_rank_chunk<NT>(sh, kr, vr, R, len, shift_of(p), db_of(p), false, nullptr);
                 if (p + 1 < passes) {
                     const bool rekey = p + 1 == ip;  // index order done: the depth keys from here on
 #pragma unroll
-                    for (int r = 0; r < kSxMaxR; r++) {
+                    for (int r = 0; r < MR; r++) {
                         const uint32_t i = wl + (uint32_t)r * 64 + lane;
                         if (r < R && i < len) {
                             kr[r] = sh.k[i];
@@ -764,20 +778,20 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
                     }
                     if (rekey)
 #pragma unroll
-                        for (int r = 0; r < kSxMaxR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];
+                        for (int r = 0; r < MR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];
                     __syncthreads();  // every read of this pass's order before the next pass's writes
                 }
             }
             if (ipasses == 0 || attempt > 0) break;
             // unordered run sorted by depth alone: equal keys put in index order in place, or (a long
             // group) the full sort with the index passes first
-            if (!fix_ties(
+            if (!fix_ties<NT>(
                     len, [&](uint32_t i) { return sh.k[i]; }, [&](uint32_t i) { return sh.v[i]; },
                     [&](uint32_t i, uint32_t v) { sh.v[i] = v; }))
                 break;  // block-uniform
             ip = ipasses;
 #pragma unroll
-            for (int r = 0; r < kSxMaxR; r++) vr[r] = sh.v[min(wl + (uint32_t)r * 64 + lane, len - 1)];
+            for (int r = 0; r < MR; r++) vr[r] = sh.v[min(wl + (uint32_t)r * 64 + lane, len - 1)];
             __syncthreads();  // every read of the depth order before the index passes write sh.v
         }
     } else if (RR_SX_GLOBAL && len > lds_cap) {
@@ -797,9 +811,9 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
             uint2* dst = (p & 1) ? scr1 : scr0;
             const bool fresh = src == nullptr || p == ip;  // keys recomputed from the values
             // digit totals of the whole run -> each digit's first slot
-            for (int d = t; d < ndig; d += 256) sh.cursor[d] = 0;
+            for (int d = t; d < ndig; d += NT) sh.cursor[d] = 0;
             __syncthreads();
-            for (uint32_t i = t; i < len; i += 256) {
+            for (uint32_t i = t; i < len; i += NT) {
                 const uint32_t k = fresh ? key_of(p, src ? src[i].y : vals[lo + i]) : src[i].x;
                 atomicAdd(&sh.cursor[(k >> shift) & mask], 1u);
             }
@@ -824,24 +838,24 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
             __syncthreads();
             for (uint32_t c0 = 0; c0 < len; c0 += kSxCap) {
                 const uint32_t clen = min((uint32_t)kSxCap, len - c0);
-                const int R = (int)((clen + 255) / 256);
+                const int R = (int)((clen + NT - 1) / NT);
                 const uint32_t wl = (uint32_t)w * 64 * R;
-                uint32_t kr[kSxMaxR], vr[kSxMaxR];
+                uint32_t kr[MR], vr[MR];
                 if (src) {
 #pragma unroll
-                    for (int r = 0; r < kSxMaxR; r++) {  // clamped, unconditional loads (see above)
+                    for (int r = 0; r < MR; r++) {  // clamped, unconditional loads (see above)
                         const uint2 e = src[c0 + min(wl + (uint32_t)r * 64 + lane, clen - 1)];
                         kr[r] = e.x;
                         vr[r] = e.y;
                     }
                 } else {
 #pragma unroll
-                    for (int r = 0; r < kSxMaxR; r++) vr[r] = vals[lo + c0 + min(wl + (uint32_t)r * 64 + lane, clen - 1)];
+                    for (int r = 0; r < MR; r++) vr[r] = vals[lo + c0 + min(wl + (uint32_t)r * 64 + lane, clen - 1)];
                 }
                 if (fresh)
 #pragma unroll
-                    for (int r = 0; r < kSxMaxR; r++) kr[r] = key_of(p, vr[r]);
-                sx_rank_chunk(sh, kr, vr, R, clen, shift, db, true, dst);
+                    for (int r = 0; r < MR; r++) kr[r] = key_of(p, vr[r]);
+                sx_rank_chunk<NT>(sh, kr, vr, R, clen, shift, db, true, dst);
             }
             __syncthreads();
         }
@@ -849,7 +863,7 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
         if (ipasses == 0 || attempt > 0) break;
         uint2* sg = const_cast<uint2*>(sorted_g);
         __threadfence_block();
-        if (!fix_ties(
+        if (!fix_ties<NT>(
                 len, [&](uint32_t i) { return sg[i].x; }, [&](uint32_t i) { return sg[i].y; },
                 [&](uint32_t i, uint32_t v) { sg[i].y = v; }))
             break;
@@ -858,7 +872,7 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
       }
         // the sorted values back over the run's input (read only by pass 0), freeing the region
         uint32_t* const vw = const_cast<uint32_t*>(vals) + lo;
-        for (uint32_t i = t; i < len; i += 256) vw[i] = sorted_g[i].y;
+        for (uint32_t i = t; i < len; i += NT) vw[i] = sorted_g[i].y;
         __syncthreads();
         global = true;
     }
@@ -867,7 +881,7 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t dst0 = out_base + 4u * lo;
     uint32_t carry[4] = {0u, 0u, 0u, 0u};
-    for (uint32_t r0 = 0; r0 < len; r0 += 256) {
+    for (uint32_t r0 = 0; r0 < len; r0 += NT) {
         const uint32_t j = r0 + (uint32_t)t;
         uint32_t v = 0u;
         if (j < len) v = (global || (len <= 1 && !lds_vals)) ? vals[lo + j] : sh.v[j];
@@ -884,7 +898,7 @@ __device__ __forceinline__ void sortexpand_run(SxShared& sh, int X, int Y, int g
         for (int b = 0; b < 4; b++) {
             uint32_t pre = carry[b], tot = 0;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
+            for (int i = 0; i < NW; i++) {
                 pre += i < w ? sh.wsum[i][b] : 0u;
                 tot += sh.wsum[i][b];
             }
@@ -1004,8 +1018,8 @@ __global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ k
 #define RR_SX_OCC 1  // a minimum of 6 workgroups per CU (69 VGPRs instead of 81) measured neutral:
                      // ranges 0.0925 vs 0.0919 ms/step (profiles/r05_dup_big_sx_occ_ab.jsonl)
 #endif
-template <typename K>
-__global__ __launch_bounds__(256, RR_SX_OCC) void k_sortexpand(const uint2* __restrict__ bounds,
+template <typename K, int NT>
+__global__ __launch_bounds__(NT, NT == 256 ? RR_SX_OCC : 1) void k_sortexpand(const uint2* __restrict__ bounds,
                                                     const K* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ depth_keys,
                                                     const FrameTotals* __restrict__ ft, int gx, int gy,
@@ -1015,7 +1029,7 @@ __global__ __launch_bounds__(256, RR_SX_OCC) void k_sortexpand(const uint2* __re
                                                     uint32_t* report,
                                                     int ipasses, const uint32_t* __restrict__ out_base_dev,
                                                     int bucket) {
-    __shared__ SxShared sh;
+    __shared__ SxSharedT<NT / 64> sh;
     const int bgx = bins_x(gx);
     const int bin = blockIdx.x;
     const int X = bin % bgx, Y = bin / bgx;
@@ -1037,7 +1051,7 @@ __global__ __launch_bounds__(256, RR_SX_OCC) void k_sortexpand(const uint2* __re
     const uint32_t lo = run.y ? ~run.x : 0u;
     // out_base_dev: the lists start after the 4 slots per pair of an earlier phase (compact layout)
     const uint32_t ob = out_base_dev ? out_base + 4u * *out_base_dev : out_base;
-    sortexpand_run(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
+    sortexpand_run<NT>(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
                    ob, point_list, ranges, lds_cap, bucket != 0);
 }
 
@@ -1049,7 +1063,7 @@ void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const u
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0) return;
     if (L > 0 && !bounds_ready) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
-    k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
+    k_sortexpand<K, 256><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
                                         open_bits, sx_lds_cap(), n_dev, n_dev ? report : nullptr, 0, nullptr,
                                         g_sx_bucket);
 }
@@ -1061,6 +1075,7 @@ template void launch_sortexpand<uint32_t>(uint32_t, const uint32_t*, const uint3
                                           uint2*, bool, uint32_t*, hipStream_t);
 
 void set_sx_bucket(bool on) { g_sx_bucket = on ? 1 : 0; }
+void set_sx_b_threads(int n) { g_sx_b_threads = n == 256 ? 256 : 1024; }
 void set_sx_lds_cap(int cap) { g_sx_lds_cap = (cap >= 1 && cap <= kSxCap) ? cap : kSxCap; }
 
 int index_passes(int P) {  // 9-bit passes covering the Gaussian indices [0, P)
@@ -1080,9 +1095,16 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
     const int wk = sizeof(K) == 4;
     k_bin_count<<<kBinGroups, 1024, 0, st>>>(keys, wk, n_dev, nb, bin_cnt);
     k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, bounds, vals_sorted, kept);
-    k_sortexpand<K><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list, ranges,
-                                        open_bits, sx_lds_cap(), n_dev, report, index_passes(P), out_base_dev,
-                                        g_sx_bucket);
+    // phase B (open_bits): few bins hold pairs, so a bin's latency sets the launch's time — 1024
+    // threads per bin (rr_set_tuning "sx_b_threads" 256: the phase-A shape)
+    if (open_bits && g_sx_b_threads == 1024)
+        k_sortexpand<K, 1024><<<nb, 1024, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base,
+                                                   point_list, ranges, open_bits, sx_lds_cap(), n_dev, report,
+                                                   index_passes(P), out_base_dev, g_sx_bucket);
+    else
+        k_sortexpand<K, 256><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base,
+                                                 point_list, ranges, open_bits, sx_lds_cap(), n_dev, report,
+                                                 index_passes(P), out_base_dev, g_sx_bucket);
     return true;
 }
 template bool launch_sortexpand_small<uint16_t>(int, const uint16_t*, const uint32_t*, const uint32_t*, uint32_t*,
