@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--tune", action="append", default=[], help="rr_set_tuning key=value (repeatable)")
     ap.add_argument("--no-fuse-next", action="store_true",
                     help="the next frame's preprocess as its own launch (Trainer.fuse_next = False)")
+    ap.add_argument("--skew-state", type=int, default=0,
+                    help="re-place each Adam moment at an offset of this many KiB (+ 1/2 MiB steps) from "
+                         "its parameter's alignment (HBM channel-placement probe)")
     ap.add_argument("--ssim-band", type=int, default=0,
                     help="rl_l1_ssim_forward_backward as one band walk of this many rows (rl_set_fused_band)")
     ap.add_argument("--loss-split", action="store_true",
@@ -77,6 +80,23 @@ def main():
     for _ in range(10):
         tr.step(it)
         it += 1
+    if a.skew_state:
+        # each moment in a fresh buffer at a non-power-of-two offset, so that element i of a
+        # parameter and of its two moments no longer share an address modulo the allocator's 2 MiB
+        # alignment
+        keep = []
+        for k, p in enumerate(g.params()):
+            st = g.optimizer.state[p]
+            for j, name in enumerate(("exp_avg", "exp_avg_sq")):
+                off = (j + 1) * (262144 + a.skew_state * 256)  # floats: (j+1) x (1 MiB + skew KiB)
+                buf = torch.empty(p.numel() + off, device=dev)
+                buf[off:].copy_(st[name].reshape(-1))
+                st[name] = buf[off:].view_as(p)
+                keep.append(buf)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            tr.step(it)
+            it += 1
     _native.Profiler.collect()
     with _native.Profiler():
         for _ in range(20):
