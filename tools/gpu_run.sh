@@ -89,7 +89,8 @@ for STEP in "$@"; do
         SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
         --kernel-trace -d ${OUT}_stall -o run --output-format csv -- python3 tools/pmc_workload.py \
         > ${OUT}_stall.log 2>&1 || { tail -20 ${OUT}_stall.log; exit 1; }
-      python3 tools/pmc_stalls.py ${OUT}_stall --match "${STEP#stalls=}" | tee ${OUT}_stalls.txt ;;
+      python3 tools/pmc_stalls.py ${OUT}_stall --match "${STEP#stalls=}" | tee ${OUT}_stalls.txt
+      python3 tools/pmc_stalls.py ${OUT}_stall --match "${STEP#stalls=}" --min-us 30 > ${OUT}_stalls_long.txt ;;
     pmc)
       bash tools/profile_round.sh ${OUT}_pmcdir pmc-only || exit 1
       head -60 ${OUT}_pmcdir/pmc_traffic.json ;;

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--match", default="")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--min-us", type=float, default=0.0, help="only dispatches at least this long")
     a = ap.parse_args()
     per = {}
     for fn in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
@@ -46,7 +47,7 @@ def main():
         rows = []
         for d in disp.values():
             dur = d["dur_ns"]
-            if dur <= 0:
+            if dur <= 0 or dur < a.min_us * 1e3:
                 continue
             clk = d.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 / dur if d.get("GRBM_GUI_ACTIVE") else 2.1
             cyc = dur * clk
