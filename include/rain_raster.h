@@ -411,11 +411,14 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *   "split_marks" 0/1     windowed duplicate: window starts marked by the split scan when the
  *                         sort unit is 2048 pairs (default 1) or computed by their own launch,
  *   "sx_b_threads" n      phase B's per-bin sort-expand workgroup: 1024 threads (default) or 256,
- *   "sx_lds_cap" n        per-bin runs of more than n pairs (1..2048, default 2048) depth-sorted
- *                         through their own point_list region instead of LDS,
+ *   "sx_lds_cap" n        per-bin runs of more than n pairs (1..2048; default: 2048 in phase A,
+ *                         4096 in phase B's 1024-thread sort-expand) depth-sorted through their
+ *                         own point_list region instead of LDS,
  *   "forward_clear" 0/1   rr_set_forward_workspace registrations honoured (default 1) or dropped,
  *   "dup_b_reserve" 0/1   phase-B gather: one walk per Gaussian with its pair count reserved as an
  *                         upper bound (default 1) or a counting walk first,
+ *   "dup_b_rows" 0/1      phase-B gather, frames up to 128 x 256 tiles: open tiles as per-row
+ *                         bit masks, walks over the open bins only (default 1), or the flat mask,
  *   "dup_big_bins" n      phase-B gather: Gaussians spanning more than n bins (default 32) emitted
  *                         by their whole workgroup, 256 bins at a time; 0: each by its own thread,
  *   "cut_in_scan" 0/1     the early-stop depth cut computed by every workgroup of the split scan's

@@ -1316,6 +1316,10 @@ int rr_set_tuning(const char* key, int value) {
         set_dup_b_reserve(value != 0);
         return RR_OK;
     }
+    if (key && std::string(key) == "dup_b_rows") {
+        set_dup_b_rows(value != 0);
+        return RR_OK;
+    }
     if (key && std::string(key) == "dup_big_bins") {
         set_dup_big_bins(value);
         return RR_OK;

@@ -568,7 +568,8 @@ __global__ __launch_bounds__(NT, NT == 256 ? RR_SX_OCC : 1) void k_sortexpand(co
                                                     uint32_t* report,
                                                     int ipasses, const uint32_t* __restrict__ out_base_dev,
                                                     int bucket) {
-    __shared__ SxSharedT<NT / 64> sh;
+    constexpr int CAP = NT == 1024 ? kSxCapB : kSxCap;
+    __shared__ SxSharedT<NT / 64, CAP> sh;
     const int bgx = bins_x(gx);
     const int bin = blockIdx.x;
     const int X = bin % bgx, Y = bin / bgx;
@@ -590,8 +591,8 @@ __global__ __launch_bounds__(NT, NT == 256 ? RR_SX_OCC : 1) void k_sortexpand(co
     const uint32_t lo = run.y ? ~run.x : 0u;
     // out_base_dev: the lists start after the 4 slots per pair of an earlier phase (compact layout)
     const uint32_t ob = out_base_dev ? out_base + 4u * *out_base_dev : out_base;
-    sortexpand_run<NT>(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
-                   ob, point_list, ranges, lds_cap, bucket != 0);
+    sortexpand_run<NT, CAP>(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
+                            ob, point_list, ranges, lds_cap, bucket != 0);
 }
 
 template <typename K>
@@ -636,9 +637,11 @@ bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const u
     k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, bounds, vals_sorted, kept);
     // phase B (open_bits): few bins hold pairs, so a bin's latency sets the launch's time — 1024
     // threads per bin (rr_set_tuning "sx_b_threads" 256: the phase-A shape)
+    // (its LDS runs hold kSxCapB pairs; a lowered "sx_lds_cap" applies to it too)
     if (open_bits && g_sx_b_threads == 1024)
         k_sortexpand<K, 1024><<<nb, 1024, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base,
-                                                   point_list, ranges, open_bits, sx_lds_cap(), n_dev, report,
+                                                   point_list, ranges, open_bits,
+                                                   g_sx_lds_cap == kSxCap ? (uint32_t)kSxCapB : sx_lds_cap(), n_dev, report,
                                                    index_passes(P), out_base_dev, g_sx_bucket);
     else
         k_sortexpand<K, 256><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base,

@@ -386,9 +386,29 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
 namespace {
 int g_dup_big_bins = 32;
 int g_dup_b_reserve = 1;  // rr_set_tuning "dup_b_reserve": phase B reserves the pair count (one walk)
+int g_dup_b_rows = 1;     // rr_set_tuning "dup_b_rows": phase B's open tiles as row masks (frames <= 128 tiles wide)
+constexpr int kDupReserve = 1, kDupRows = 2;  // k_dup_gather opts bits
+// bit i of the result: bit 2i or 2i+1 of x (tile columns -> bin columns)
+__device__ __forceinline__ uint32_t pair_bits(uint64_t x) {
+    x = (x | (x >> 1)) & 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+    return (uint32_t)x;
 }
+// bits [a - base, b - base) clipped to [0, 64)
+__device__ __forceinline__ uint64_t span_bits(int a, int b, int base) {
+    a = max(a - base, 0);
+    b = min(b - base, 64);
+    if (a >= b) return 0ull;
+    return (b == 64 ? ~0ull : (1ull << b) - 1ull) & ~((1ull << a) - 1ull);
+}
+}  // namespace
 void set_dup_big_bins(int n) { g_dup_big_bins = n >= 0 ? n : 32; }
 void set_dup_b_reserve(bool on) { g_dup_b_reserve = on ? 1 : 0; }
+void set_dup_b_rows(bool on) { g_dup_b_rows = on ? 1 : 0; }
 template <typename K, bool PHASE_B>
 __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restrict__ tiles,
                                                     const uint32_t* __restrict__ depth_keys,
@@ -403,7 +423,8 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
                                                     uint32_t* __restrict__ order_flag, int order_T,
                                                     const uint32_t* __restrict__ list_n,
                                                     const uint32_t* __restrict__ list_idx, int big_bins,
-                                                    int reserve_n) {
+                                                    int opts) {
+    const bool reserve_n = (opts & kDupReserve) != 0;
     if (PHASE_B && order_out && blockIdx.x == 0) {
         tile_order_body256(order_T, order_cost, open_bits, order_out);
         if (threadIdx.x == 0) *order_flag = (uint32_t)order_T;
@@ -427,7 +448,13 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
     // Gaussian s of the frame filtered by the depth cut
     uint32_t n = 0u, g = 0u;
     bool in_phase;
-    if (list_idx) {
+    if (list_idx && PHASE_B) {
+        // the list holds only Gaussians with pairs; phase B reserves from the rect alone (its open
+        // bins, or its bins), so the pair count is not loaded: one dependent load less per Gaussian
+        in_phase = s < (int)*list_n;
+        if (in_phase) g = list_idx[s];
+        n = 0xffffffffu;
+    } else if (list_idx) {
         if (s < (int)*list_n) {
             g = list_idx[s];
             n = tiles[g].x;
@@ -443,21 +470,93 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         }
         in_phase = n > 0u && (PHASE_B ? key >= cut : key < cut);
     }
+    // phase B: the open tiles' bounding box [ox0, ox1) x [oy0, oy1) (phase A leaves a few tiles open,
+    // usually in one corner): every Gaussian's rect is clipped to it first, so most are rejected
+    // without a mask walk, and the walks and reservations cover only the clipped rect (the clipped
+    // spans are the full ones intersected with the box; the tiles cut off are closed)
+    int ox0 = 0, oy0 = 0, ox1 = gx, oy1 = gy;
     if (PHASE_B) {
-        bool any_open = false;
+        __shared__ int s_box[4][4];
+        int bx0 = gx, by0 = gy, bx1 = 0, by1 = 0;
         for (int i = t; i < (gx * gy + 31) / 32; i += 256) {
             const uint32_t word = open_bits[i];
             if (mask_lds) s_open[i] = word;
-            any_open = any_open || word != 0u;
+            for (uint32_t m = word; m; m &= m - 1u) {
+                const int tile = 32 * i + __builtin_ctz(m), ty = tile / gx, tx = tile - ty * gx;
+                bx0 = min(bx0, tx);
+                bx1 = max(bx1, tx + 1);
+                by0 = min(by0, ty);
+                by1 = max(by1, ty + 1);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            bx0 = min(bx0, __shfl_xor(bx0, o));
+            bx1 = max(bx1, __shfl_xor(bx1, o));
+            by0 = min(by0, __shfl_xor(by0, o));
+            by1 = max(by1, __shfl_xor(by1, o));
+        }
+        if (lane == 0) {
+            s_box[w][0] = bx0;
+            s_box[w][1] = by0;
+            s_box[w][2] = bx1;
+            s_box[w][3] = by1;
         }
         // phase A closed every tile (about half the bench frames): nothing to emit, no record loads
-        if (!__syncthreads_or(any_open)) return;
+        if (!__syncthreads_or(bx1 > 0)) return;
+        ox0 = min(min(s_box[0][0], s_box[1][0]), min(s_box[2][0], s_box[3][0]));
+        oy0 = min(min(s_box[0][1], s_box[1][1]), min(s_box[2][1], s_box[3][1]));
+        ox1 = max(max(s_box[0][2], s_box[1][2]), max(s_box[2][2], s_box[3][2]));
+        oy1 = max(max(s_box[0][3], s_box[1][3]), max(s_box[2][3], s_box[3][3]));
     }
+    // phase B, frames up to 128 tiles wide and 256 tall (opts kDupRows): the open tiles also as two
+    // 64-bit words per tile row (s_trow) and one per bin row (s_brow, bit X: bin column X holds an
+    // open tile), so a rect's open test is one masked word pair per tile row and the walk visits
+    // only the bins holding an open tile
+    const bool rowm = PHASE_B && mask_lds && (opts & kDupRows) && gx <= 128 && gy <= 256;
+    __shared__ uint64_t s_trow[PHASE_B ? 512 : 1];
+    __shared__ uint64_t s_brow[PHASE_B ? 128 : 1];
+    if (rowm) {  // block-uniform
+        const uint32_t nw = (uint32_t)(gx * gy + 31) / 32;
+        for (int r = t; r < 2 * gy; r += 256) {
+            const int y = r >> 1, h = r & 1, nbits = min(64, gx - 64 * h);
+            uint64_t v = 0ull;
+            if (nbits > 0) {
+                const uint32_t o = (uint32_t)(y * gx + 64 * h), wi = o >> 5, sh = o & 31;
+                const uint64_t w01 = (uint64_t)s_open[wi] | ((wi + 1 < nw ? (uint64_t)s_open[wi + 1] : 0ull) << 32);
+                const uint64_t w2 = wi + 2 < nw ? (uint64_t)s_open[wi + 2] : 0ull;
+                v = (w01 >> sh) | (sh ? w2 << (64 - sh) : 0ull);
+                if (nbits < 64) v &= (1ull << nbits) - 1ull;
+            }
+            s_trow[r] = v;
+        }
+        __syncthreads();
+        for (int Y = t; Y < bins_y(gy); Y += 256) {
+            uint64_t lo = s_trow[4 * Y], hi = s_trow[4 * Y + 1];
+            if (2 * Y + 1 < gy) {
+                lo |= s_trow[4 * Y + 2];
+                hi |= s_trow[4 * Y + 3];
+            }
+            s_brow[Y] = (uint64_t)pair_bits(lo) | ((uint64_t)pair_bits(hi) << 32);
+        }
+        __syncthreads();
+    }
+    auto clip = [&](int& x0, int& y0, int& x1, int& y1) {
+        x0 = max(x0, ox0);
+        y0 = max(y0, oy0);
+        x1 = min(x1, ox1);
+        y1 = min(y1, oy1);
+    };
     auto is_open = [&](uint32_t tile) -> bool {
         const uint32_t word = mask_lds ? s_open[tile >> 5] : open_bits[tile >> 5];
         return ((word >> (tile & 31)) & 1u) != 0;
     };
     auto open4 = [&](int X, int Y) -> uint32_t {
+        if (rowm) {  // tile columns 2X, 2X + 1: two adjacent bits of one word (2X even, < 128)
+            const int c = 2 * X, hw = c >> 6, b = c & 63;
+            const uint64_t r0 = s_trow[4 * Y + hw], r1 = 2 * Y + 1 < gy ? s_trow[4 * Y + 2 + hw] : 0ull;
+            return (uint32_t)((r0 >> b) & 3ull) | ((uint32_t)((r1 >> b) & 3ull) << 2);
+        }
         uint32_t m = 0;
 #pragma unroll
         for (int b = 0; b < 4; b++) {
@@ -467,6 +566,12 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         return m;
     };
     auto rect_open = [&](int x0, int y0, int x1, int y1) -> bool {
+        if (rowm) {
+            const uint64_t mlo = span_bits(x0, x1, 0), mhi = span_bits(x0, x1, 64);
+            for (int y = y0; y < y1; y++)
+                if ((s_trow[2 * y] & mlo) | (s_trow[2 * y + 1] & mhi)) return true;
+            return false;
+        }
         for (int y = y0; y < y1; y++) {
             const uint32_t lo = (uint32_t)(y * gx + x0), hi = (uint32_t)(y * gx + x1);  // bits [lo, hi)
             for (uint32_t wd = lo >> 5; wd <= (hi - 1) >> 5; wd++) {
@@ -478,10 +583,19 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         }
         return false;
     };
+    // row masks: the bins of the rect's bin rows and columns holding an open tile — an upper bound
+    // on the pairs the walk keeps (0: none)
+    auto open_bins = [&](int x0, int y0, int x1, int y1) -> uint32_t {
+        const uint64_t bm = span_bits(x0 >> 1, (x1 + 1) >> 1, 0);
+        uint32_t c = 0;
+        for (int Y = y0 >> 1; Y < (y1 + 1) >> 1; Y++) c += (uint32_t)__popcll(s_brow[Y] & bm);
+        return c;
+    };
     const int bgx = bins_x(gx);
     uint32_t cnt = 0;
     CullEll ell{};
-    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    int x0 = 0, y0 = 0, x1 = 0, y1 = 0, nbins = 0;
+    uint32_t bound = 0;  // phase B: pairs reserved (reserve_n)
     bool live = false;
     if (in_phase) {
         const int r = radii[g];
@@ -489,20 +603,62 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         const float4 Bv = splats[g].b;
         asm volatile("" ::"v"(r), "v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(Bv.x), "v"(Bv.w));
         tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
-        const int nbins = (((x1 + 1) >> 1) - (x0 >> 1)) * (((y1 + 1) >> 1) - (y0 >> 1));
+        if (PHASE_B) clip(x0, y0, x1, y1);
+        nbins = (((x1 + 1) >> 1) - (x0 >> 1)) * (((y1 + 1) >> 1) - (y0 >> 1));
+#if defined(RR_DUP_PROBE) && RR_DUP_PROBE == 1  // timing probe only (drops pairs): the big path's cost
+        if (PHASE_B && big_bins > 0 && x0 < x1 && y0 < y1 && nbins > big_bins) {
+        } else
+#elif defined(RR_DUP_PROBE) && RR_DUP_PROBE == 2  // timing probe only: the open-tile tests and walks
+        if (PHASE_B) {
+        } else
+#endif
         if (PHASE_B && big_bins > 0 && x0 < x1 && y0 < y1 && nbins > big_bins) {
             s_big[atomicAdd(&s_nbig, 1u)] = g;  // one thread's walk would hold up its workgroup
-        } else if (x0 < x1 && y0 < y1 && (!PHASE_B || rect_open(x0, y0, x1, y1))) {
+        } else if (x0 < x1 && y0 < y1 &&
+                   (!PHASE_B || (rowm ? (bound = open_bins(x0, y0, x1, y1)) > 0u : true) && rect_open(x0, y0, x1, y1))) {
             float ccx, ccy, ccz;
             splat_conic(A, Bv, ccx, ccy, ccz);
             ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
             live = true;
         }
     }
+    // Pair i of the workgroup's reservation (at s_base): with the row masks, the first kStage go
+    // through LDS (the flat mask's words, no longer read) and out in coalesced rows — each thread's
+    // pairs are contiguous, so direct stores scatter 64 runs per instruction — the rest directly
+    constexpr uint32_t kStage = PHASE_B ? 1024u : 0u;
+    uint32_t* const st_val = s_open;
+    uint32_t* const st_key = s_open + kStage;
+    auto put = [&](uint32_t i, K key, uint32_t val) {
+        if (rowm && i < kStage) {
+            st_key[i] = (uint32_t)key;
+            st_val[i] = val;
+        } else {
+            keys[s_base + i] = key;
+            vals[s_base + i] = val;
+        }
+    };
     // the kept pairs, in the duplicate's enumeration (bin rows, then bin columns); phase B: pass 0
     // counts, pass 1 writes; phase A writes its n pairs (never more: the reservation's bound)
     auto walk = [&](bool emit, uint32_t pos, uint32_t cap) {
         uint32_t c = 0;
+        if (rowm) {  // block-uniform: only the bin columns of each row that hold an open tile
+            const uint64_t bm = span_bits(x0 >> 1, (x1 + 1) >> 1, 0);
+            for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && c < cap; Y++) {
+                const uint64_t cand = s_brow[Y] & bm;
+                if (!cand) continue;
+                int l0, h0, l1, h1, Xa, Xb;
+                bin_row_spans(ell, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
+                bin_cols(l0, h0, l1, h1, Xa, Xb);
+                for (uint64_t cm = cand & span_bits(Xa, Xb, 0); cm && c < cap; cm &= cm - 1ull) {
+                    const int X = __builtin_ctzll(cm);
+                    const uint32_t m = bin_mask(X, l0, h0, l1, h1) & open4(X, Y);
+                    if (!m) continue;
+                    if (emit) put(pos + c, (K)(Y * bgx + X), g | (m << BIN_SHIFT));
+                    c++;
+                }
+            }
+            return c;
+        }
         for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && c < cap; Y++) {
             // phase B: a bin row whose two tile rows hold no open tile in [x0, x1) emits nothing
             // (skipped before its culling spans are evaluated)
@@ -514,19 +670,18 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
                 uint32_t m = bin_mask(X, l0, h0, l1, h1);
                 if (PHASE_B) m &= open4(X, Y);
                 if (!m) continue;
-                if (emit) {
-                    keys[pos + c] = (K)(Y * bgx + X);
-                    vals[pos + c] = g | (m << BIN_SHIFT);
-                }
+                if (emit) put(pos + c, (K)(Y * bgx + X), g | (m << BIN_SHIFT));
                 c++;
             }
         }
         return c;
     };
-    // phase B: the kept pairs counted by a first walk, or (reserve_n) the Gaussian's pair count
-    // reserved as an upper bound, the slots the one walk leaves filled with a key past the last bin
-    // (the bin count and scatter skip them): one walk per Gaussian instead of two
-    if (live) cnt = (PHASE_B && !reserve_n) ? walk(false, 0u, 0xffffffffu) : n;
+    // phase B: the kept pairs counted by a first walk, or (reserve_n) an upper bound reserved (the
+    // clipped rect's open bins or bins, or the Gaussian's pair count if fewer and known), the slots the one walk leaves
+    // filled with a key past the last bin (the bin count and scatter skip them): one walk per
+    // Gaussian instead of two
+    if (live)
+        cnt = !PHASE_B ? n : !reserve_n ? walk(false, 0u, 0xffffffffu) : min(n, rowm ? bound : (uint32_t)nbins);
     // the workgroup's kept pairs: wave prefix sums, one reservation
     uint32_t incl = cnt;
 #pragma unroll
@@ -546,14 +701,18 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         if (t == 0) s_base = atomicAdd(n_total, tot);
         __syncthreads();
         if (cnt) {
-            const uint32_t pos = s_base + pre + incl - cnt;
+            const uint32_t pos = pre + incl - cnt;  // in the workgroup's reservation
             // phase A: the walk and the preprocess's count are the same closed form on the same
             // record (rr_preprocess.hpp); should they ever disagree, the reserved slots left over get
             // an empty tile mask, which the per-bin split writes to no tile list
             const K fill = (PHASE_B && reserve_n) ? (K)(bgx * bins_y(gy)) : (K)0;
-            for (uint32_t c = walk(true, pos, cnt); c < cnt; c++) {
-                keys[pos + c] = fill;
-                vals[pos + c] = g;
+            for (uint32_t c = walk(true, pos, cnt); c < cnt; c++) put(pos + c, fill, g);
+        }
+        if (rowm) {  // block-uniform
+            __syncthreads();
+            for (uint32_t i = t; i < min(tot, kStage); i += 256) {
+                keys[s_base + i] = (K)st_key[i];
+                vals[s_base + i] = st_val[i];
             }
         }
     }
@@ -569,6 +728,7 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
             const float4 Bv = splats[gb].b;
             int bx0, by0, bx1, by1;
             tile_rect(A.x, A.y, rb, gx, gy, bx0, by0, bx1, by1);
+            clip(bx0, by0, bx1, by1);  // non-empty: it was queued on the clipped rect
             float ccx, ccy, ccz;
             splat_conic(A, Bv, ccx, ccy, ccz);
             const CullEll eb = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
@@ -683,7 +843,8 @@ void launch_dup_gather(const DupArgs<K>& d, bool phase_b, hipStream_t st) {
     k_dup_gather<K, true><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
         d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits,
         d.n_total, ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T,
-        d.idx ? d.n_list : nullptr, d.idx, g_dup_big_bins, g_dup_b_reserve);
+        d.idx ? d.n_list : nullptr, d.idx, g_dup_big_bins,
+        (g_dup_b_reserve ? kDupReserve : 0) | (g_dup_b_rows ? kDupRows : 0));
 }
 template void launch_dup_gather<uint16_t>(const DupArgs<uint16_t>&, bool, hipStream_t);
 template void launch_dup_gather<uint32_t>(const DupArgs<uint32_t>&, bool, hipStream_t);

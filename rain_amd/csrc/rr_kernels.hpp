@@ -373,8 +373,9 @@ void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
 void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
 int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
 void set_sx_bucket(bool on);  // rr_bin.hip: per-bin bucket sort (default) or LSD passes only
-void set_sx_lds_cap(int cap);
+void set_sx_lds_cap(int cap);  // runs longer than cap (1..2048; other values: the default) take the global path
 void set_sx_b_threads(int n);  // phase B's sort-expand workgroup: 1024 threads (default) or 256
-void set_dup_big_bins(int n);
-void set_dup_b_reserve(bool on);  // phase-B gather: one walk, the pair count reserved (fill keys skipped)  // rr_forward.hip: phase-B Gaussians over n bins emitted per workgroup (0: none)  // runs longer than cap (1..2048; other values: 2048) take the global path
+void set_dup_big_bins(int n);  // rr_forward.hip: phase-B Gaussians over n bins emitted per workgroup (0: none)
+void set_dup_b_reserve(bool on);  // phase-B gather: one walk, the pair count reserved (fill keys skipped)
+void set_dup_b_rows(bool on);     // phase-B gather: open tiles as row masks (frames <= 128 x 256 tiles)
 }  // namespace rr

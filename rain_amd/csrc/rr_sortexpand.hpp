@@ -13,25 +13,32 @@ namespace rr {
 // bits, or 4 of 8 when a visible key needs more than 27 bits) makes it (depth, index) order — the
 // reference's per-tile order (rasterizer_impl.cu:292-300) — and the run is then split stably into
 // its tiles' lists (one ballot per mask bit), written at out_base + 4 lo + b len with the tile's
-// range (rasterizer_impl.cu:105-127).  Runs of up to kSxCap pairs are sorted in LDS, longer ones
-// pass through the scratch arrays in chunks of kSxCap (same ranking, one global digit scan per
+// range (rasterizer_impl.cu:105-127).  Runs of up to CAP pairs are sorted in LDS, longer ones
+// pass through the scratch arrays in chunks of CAP (same ranking, one global digit scan per
 // pass).  Ranking (rr_sort.hip's): wave w owns the contiguous items [w 64 R, (w + 1) 64 R) in
 // rounds of 64; lanes holding the same digit find each other with one ballot per digit bit.
 #ifndef RR_SX_CAP
 #define RR_SX_CAP 2048  // 4096: ranges stage 0.110 vs 0.095 ms/step (profiles/r04h_sortexpand_cap_ab.jsonl)
 #endif
 constexpr int kSxCap = RR_SX_CAP;
-constexpr int kSxMaxR = kSxCap / 256;  // rounds of 64 items per wave at 256 threads (NT threads: kSxCap / NT)
+// Phase B's 1024-thread sort-expand holds runs of up to kSxCapB in LDS (66 KB, two workgroups per
+// CU): its bins' runs are a few open tiles' whole tails, often over 2048 pairs, and the global path
+// cost those frames ~30 us more (tools/phaseb_profile.py)
+#ifndef RR_SX_CAP_B
+#define RR_SX_CAP_B 4096
+#endif
+constexpr int kSxCapB = RR_SX_CAP_B;
 #ifndef RR_SX_GLOBAL
 #define RR_SX_GLOBAL 1  // 0: ISA inspection builds without the long-run path
 #endif
 
-// NW waves per workgroup (4: 256 threads; 16: the 1024-thread phase-B sort-expand)
-template <int NW>
+// NW waves per workgroup (4: 256 threads; 16: the 1024-thread phase-B sort-expand), runs of up to
+// CAP items in LDS
+template <int NW, int CAP>
 struct SxSharedT {
-    uint32_t k[kSxCap];
-    uint32_t v[kSxCap];
-    uint32_t wcnt[NW][512];  // per-wave digit counts, then per-wave cursors (>= the 2048 buckets)
+    uint32_t k[CAP];
+    uint32_t v[CAP];
+    uint32_t wcnt[NW][512];  // per-wave digit counts, then per-wave cursors (also the NW 512 buckets)
     uint32_t cursor[512];    // global path: next slot of each digit across the chunks
     uint32_t wsum[NW][4];
 };
@@ -41,11 +48,11 @@ struct SxSharedT {
 // (dst_lds) or to a global scratch run (dst_g).  base: the digit's first slot (LDS path: the
 // chunk's exclusive digit prefix; global path: cursor[d]).  Ends with the chunk's digit counts
 // added to cursor (global path).
-template <int NT>
-__device__ __forceinline__ void sx_rank_chunk(SxSharedT<NT / 64>& sh, const uint32_t (&kr)[kSxCap / NT],
-                                              const uint32_t (&vr)[kSxCap / NT], int R, uint32_t len, int shift,
+template <int NT, int CAP>
+__device__ __forceinline__ void sx_rank_chunk(SxSharedT<NT / 64, CAP>& sh, const uint32_t (&kr)[CAP / NT],
+                                              const uint32_t (&vr)[CAP / NT], int R, uint32_t len, int shift,
                                               int db, bool global, uint2* dst_g) {
-    constexpr int MR = kSxCap / NT, NW = NT / 64;
+    constexpr int MR = CAP / NT, NW = NT / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int ndig = 1 << db;
     const uint32_t mask = (uint32_t)ndig - 1u;
@@ -144,24 +151,26 @@ __device__ __forceinline__ bool fix_ties(uint32_t len, KeyAt key_at, ValAt val_a
     return __syncthreads_or(big);
 }
 
-// Bucket sort of a run of len <= kSxCap items (depth keys kr / values vr in registers, R rounds per
+// Bucket sort of a run of len <= CAP items (depth keys kr / values vr in registers, R rounds per
 // wave as in sx_rank_chunk) into (depth key, Gaussian index) order — the reference's per-tile order —
-// in sh.k / sh.v, whatever order the run arrived in: one counting pass over kSxBuckets buckets
+// in sh.k / sh.v, whatever order the run arrived in: one counting pass over NW 512 buckets
 // spanning the run's own key range [kmin, kmax], then each bucket (a few items) insertion-sorted by
 // one thread on (key, index).  One histogram, one scan and one scatter instead of the three 9-bit
 // LSD passes (each a histogram, a 512-digit scan and a ballot ranking), and equal depths need no
 // extra index passes.  Returns false, with nothing written to sh.k / sh.v, when a bucket holds more
 // than kSxBucketMax items (strongly clustered depths, many exact copies): the caller then sorts
 // with the LSD passes.
-constexpr int kSxBuckets = 2048;  // = the 4 x 512 per-wave digit counters of SxShared
 #ifndef RR_SX_BUCKET_MAX
 #define RR_SX_BUCKET_MAX 16
 #endif
 constexpr uint32_t kSxBucketMax = RR_SX_BUCKET_MAX;
-template <int NT>
-__device__ __forceinline__ bool bucket_sort_run(SxSharedT<NT / 64>& sh, const uint32_t (&kr)[kSxCap / NT],
-                                                const uint32_t (&vr)[kSxCap / NT], int R, uint32_t len) {
-    constexpr int MR = kSxCap / NT, NW = NT / 64;
+template <int NT, int CAP>
+__device__ __forceinline__ bool bucket_sort_run(SxSharedT<NT / 64, CAP>& sh, const uint32_t (&kr)[CAP / NT],
+                                                const uint32_t (&vr)[CAP / NT], int R, uint32_t len) {
+    constexpr int MR = CAP / NT, NW = NT / 64;
+    constexpr int kSxBuckets = NW * 512;  // the per-wave digit counters of SxSharedT
+    constexpr int kLg = 9 + (NW >= 2) + (NW >= 4) + (NW >= 8) + (NW >= 16);  // log2(kSxBuckets)
+    static_assert((1 << kLg) == kSxBuckets, "bucket count");
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t wl = (uint32_t)w * 64 * R;
     uint32_t* hist = &sh.wcnt[0][0];
@@ -190,7 +199,7 @@ __device__ __forceinline__ bool bucket_sort_run(SxSharedT<NT / 64>& sh, const ui
     }
     const uint32_t span = kmax - kmin;
     // (span >> shift) < kSxBuckets
-    const int shift = span < (uint32_t)kSxBuckets ? 0 : 32 - __clz((int)span) - 11;
+    const int shift = span < (uint32_t)kSxBuckets ? 0 : 32 - __clz((int)span) - kLg;
     uint32_t bk[MR];
 #pragma unroll
     for (int r = 0; r < MR; r++) {
@@ -268,18 +277,18 @@ __device__ __forceinline__ bool bucket_sort_run(SxSharedT<NT / 64>& sh, const ui
 
 // One bin's run of `len` (bin, Gaussian) pairs in index order -> depth order -> its four tiles'
 // lists at out_base + 4 lo + b len, and the tiles' ranges.  The run is vals[lo, lo + len) or, with
-// lds_vals (len <= kSxCap), already in sh.v.  Runs longer than lds_cap (<= kSxCap) are sorted
+// lds_vals (len <= CAP), already in sh.v.  Runs longer than lds_cap (<= CAP) are sorted
 // through global scratch: the run's own output region of point_list (4 slots per pair = two uint2
 // arrays of len), with the sorted values put back into vals[lo, lo + len) before the tile split
 // overwrites that region — no scratch arrays in the binning buffer.
-template <int NT>
-__device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64>& sh, int X, int Y, int gx, int gy, uint32_t lo,
+template <int NT, int CAP>
+__device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64, CAP>& sh, int X, int Y, int gx, int gy, uint32_t lo,
                                                uint32_t len,
                                                const uint32_t* __restrict__ vals, bool lds_vals,
                                                const uint32_t* __restrict__ depth_keys, bool wide, int ipasses,
                                                uint32_t out_base, uint32_t* __restrict__ point_list,
                                                uint2* __restrict__ ranges, uint32_t lds_cap, bool bucket) {
-    constexpr int MR = kSxCap / NT, NW = NT / 64;
+    constexpr int MR = CAP / NT, NW = NT / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     // The depth key: 27 bits in 3 passes of 9, wider frames in 4 of 8.  A run in no particular order
     // (ipasses > 0: the phase-B pairs of the gather path) needs index order among equal depth keys:
@@ -315,14 +324,14 @@ __device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64>& sh, int X, in
 #pragma unroll
             for (int r = 0; r < MR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
 #endif
-            sorted = bucket_sort_run<NT>(sh, kr, vr, R, len);  // block-uniform
+            sorted = bucket_sort_run<NT, CAP>(sh, kr, vr, R, len);  // block-uniform
         }
         for (int attempt = 0; !sorted; attempt++) {
             const int passes = ip + (wide ? 4 : 3);
 #pragma unroll
             for (int r = 0; r < MR; r++) kr[r] = key_of(0, vr[r]);  // all gathers in flight
             for (int p = 0; p < passes; p++) {
-                sx_rank_chunk<NT>(sh, kr, vr, R, len, shift_of(p), db_of(p), false, nullptr);
+                sx_rank_chunk<NT, CAP>(sh, kr, vr, R, len, shift_of(p), db_of(p), false, nullptr);
                 if (p + 1 < passes) {
                     const bool rekey = p + 1 == ip;  // index order done: the depth keys from here on
 #pragma unroll
@@ -352,7 +361,7 @@ __device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64>& sh, int X, in
             __syncthreads();  // every read of the depth order before the index passes write sh.v
         }
     } else if (RR_SX_GLOBAL && len > lds_cap) {
-        // chunks of kSxCap in order; pass p reads run p - 1 (pass 0: the run's values with their
+        // chunks of CAP in order; pass p reads run p - 1 (pass 0: the run's values with their
         // keys) and writes scratch p % 2 (halves of the run's point_list region, 8-B aligned:
         // out_base is a multiple of 4 slots)
         uint2* const scr0 = reinterpret_cast<uint2*>(point_list + out_base + 4u * lo);
@@ -393,8 +402,8 @@ __device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64>& sh, int X, in
                 }
             }
             __syncthreads();
-            for (uint32_t c0 = 0; c0 < len; c0 += kSxCap) {
-                const uint32_t clen = min((uint32_t)kSxCap, len - c0);
+            for (uint32_t c0 = 0; c0 < len; c0 += CAP) {
+                const uint32_t clen = min((uint32_t)CAP, len - c0);
                 const int R = (int)((clen + NT - 1) / NT);
                 const uint32_t wl = (uint32_t)w * 64 * R;
                 uint32_t kr[MR], vr[MR];
@@ -412,7 +421,7 @@ __device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64>& sh, int X, in
                 if (fresh)
 #pragma unroll
                     for (int r = 0; r < MR; r++) kr[r] = key_of(p, vr[r]);
-                sx_rank_chunk<NT>(sh, kr, vr, R, clen, shift, db, true, dst);
+                sx_rank_chunk<NT, CAP>(sh, kr, vr, R, clen, shift, db, true, dst);
             }
             __syncthreads();
         }

@@ -39,6 +39,7 @@ PATHS = {
     "cut_kernel": {"cut_in_scan": (0, 1)},  # the depth cut by its own one-workgroup launch
     "dup_big_serial": {"dup_big_bins": (0, 32)},  # every phase-B Gaussian by its own thread
     "dup_b_count_walk": {"dup_b_reserve": (0, 1)},  # phase B counts its kept pairs first
+    "dup_b_flat_mask": {"dup_b_rows": (0, 1)},  # phase B tests the flat open-tile mask (wide frames' path)
     "sx_b_256": {"sx_b_threads": (256, 1024)},  # phase B's sort-expand in 256-thread workgroups
     "global_runs_b1024": {"sx_lds_cap": (64, 0), "sx_b_threads": (1024, 1024)},
     "dup_big_all": {"dup_big_bins": (1, 32)},  # every phase-B Gaussian of > 1 bin per workgroup

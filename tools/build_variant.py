@@ -3,10 +3,12 @@
 gpurun_variants/<name>.so (git-ignored; travels to the GPU box with the snapshot).
 
     python tools/build_variant.py nostage -DRR_STAGE_SH=0
+    python tools/build_variant.py prev --rev HEAD      (the sources of a git revision)
 """
 import os
 import subprocess
 import sys
+import tempfile
 from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,15 +19,24 @@ from rain_amd import _build as B  # noqa: E402
 
 def main():
     name, flags = sys.argv[1], sys.argv[2:]
+    csrc = B.CSRC
+    if flags[:1] == ["--rev"]:
+        rev, flags = flags[1], flags[2:]
+        tmp = tempfile.mkdtemp(prefix="rr_rev_")
+        arc = subprocess.run(["git", "-C", ROOT, "archive", rev, "rain_amd/csrc", "include"],
+                             capture_output=True, check=True).stdout
+        subprocess.run(["tar", "-x", "-C", tmp], input=arc, check=True)
+        csrc, inc = os.path.join(tmp, "rain_amd", "csrc"), os.path.join(tmp, "include")
+    pre = ["-I", inc, "-I", csrc] if csrc != B.CSRC else []  # ahead of the tree's own include dirs
     out = os.path.join(ROOT, "gpurun_variants")
     objdir = os.path.join(out, name + "_obj")
     os.makedirs(objdir, exist_ok=True)
     srcs = B.LIBS["librain_raster.so"]
 
     def cc(s):
-        src = os.path.join(B.CSRC, s)
+        src = os.path.join(csrc, s)
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
-        cmd = [B.HIPCC, *B.CXXFLAGS, *B.EXTRA.get(s, []), *flags, "-c", src, "-o", obj]
+        cmd = [B.HIPCC, *pre, *B.CXXFLAGS, *B.EXTRA.get(s, []), *flags, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             raise SystemExit(r.stderr)

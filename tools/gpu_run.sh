@@ -15,6 +15,7 @@
 #   abv=V1,V2[,..]        the same over librain_raster.so variants (tools/build_variant.py names)
 #   prof                  rocprofv3 kernel trace + stats of the default bench, timed-window summary
 #   stalls=PATTERN        one SQ stall-counter pass, summarised for the kernels matching PATTERN
+#   pbprof                phase-B kernel durations per view vs the open-tile region (tools/phaseb_profile.py)
 #   owner                 owner-kernel time of the sharded step for N = 1, 2, 4, 8 (tools/owner_bench.py)
 #   pmc                   PMC passes (tools/profile_round.sh without the trace) -> pmc_traffic.json
 # Output: gpurun_out/TAG_*.
@@ -70,6 +71,15 @@ for STEP in "$@"; do
       timeout -k 10 300 python3 -u tools/bin_stats.py > ${OUT}_bin_stats.json 2> ${OUT}_bin_stats.err \
         || { tail -20 ${OUT}_bin_stats.err; exit 1; }
       cat ${OUT}_bin_stats.json ;;
+    pbprof|pbprof=*)
+      # phase-B kernel durations per view against the open-tile region (tools/phaseb_profile.py);
+      # pbprof=V: with the library variant gpurun_variants/V.so
+      V=""; P=${OUT}_pbp; [ "$STEP" != pbprof ] && { V=gpurun_variants/${STEP#pbprof=}.so; P=${OUT}_pbp_${STEP#pbprof=}; }
+      RAIN_RASTER_LIB=$V timeout -k 10 300 rocprofv3 --kernel-trace -d $P -o run --output-format csv \
+        -- python3 tools/phaseb_profile.py run --views 64 > ${P}_views.jsonl 2> ${P}.err \
+        || { tail -20 ${P}.err; exit 1; }
+      python3 tools/phaseb_profile.py join $P ${P}_views.jsonl > ${P}_profile.jsonl
+      grep -v '"open_tiles": 0,' ${P}_profile.jsonl | head -40 ;;
     owner)
       # owner-kernel time of the Gaussian-sharded step by N (tools/owner_bench.py)
       timeout -k 10 400 python3 -u tools/owner_bench.py > ${OUT}_owner.jsonl 2> ${OUT}_owner.err \
