@@ -236,6 +236,19 @@ typedef struct rr_next_frame {
  * backward, with RR_FLAG_WORKSPACE_REGISTERED).  The caller must not write the workspace in
  * between.  NULL: drop a registration. */
 int rr_set_forward_workspace(void* workspace, size_t workspace_bytes);
+
+/* Early-stop phase A as a point a second stream can wait for (the training step runs the loss of
+ * the image rows phase A finished while phase B renders the rest, rain_loss.h
+ * rl_l1_ssim_forward_backward_part).  rr_set_phase_a_event(1): this thread's renders record an event
+ * (a hipEvent_t, rr_phase_a_event) right after the phase-A blend launch — from then on every pixel
+ * of a tile whose bit in the frame's open-tile mask is 0 is final — or, on a path without one (a
+ * single-phase frame: every bit 0), after all of the render's work.  0: no event (default).
+ * rr_frame_open_tiles: the frame's open-tile mask in its image buffer (bit ty * tiles_x + tx, 16 x
+ * 16-px tiles; written by phase A's blend, read-only after it). */
+int rr_set_phase_a_event(int on);
+void* rr_phase_a_event(void);
+int rr_frame_open_tiles(const rr_frame* f, const void* image_buffer, const void** bits, int* tiles_x, int* tiles_y);
+
 int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                 const void* geom_buffer, const void* image_buffer, const void* binning_buffer,
                 int num_rendered, const float* dL_dpix, void* workspace, size_t workspace_bytes,
@@ -399,10 +412,11 @@ int rr_set_blend_config(int fwd_waves, int bwd_waves);
  *                         the totals in one workgroup first (3 launches); default 512, <0 resets,
  *   "wide_bin_keys" 0/1   32-bit bin keys even when the bins fit 16 bits (default 0: only frames
  *                         with more than 65536 bins of 32x32 px use them),
- *   "phase_a_gather" 0/1/2  phase A (or a single-phase frame): 0 (default) windowed duplicate over
+ *   "phase_a_gather" 0..3  phase A (or a single-phase frame): 0 (default) windowed duplicate over
  *                         the split scan's index-ordered list + stable bin sort; the gather path —
  *                         one thread per Gaussian emitting its pairs, per-bin count / scan /
- *                         scatter — over every Gaussian of the frame (1) or over the list (2),
+ *                         scatter — over every Gaussian of the frame (1) or over the list (2); the
+ *                         windowed duplicate + per-bin count / scan / scatter (3),
  *   "phase_b_gather" -1/0/1/2  phase B: the gather path over the list (1, default) or over every
  *                         Gaussian (2), the windowed path (0), or by the last frame's phase-B size (-1),
  *   "sx_bucket" 0/1       per-bin order by one bucket pass + per-bucket insertion sort (default 1)

@@ -100,7 +100,8 @@ RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name", "rr_host_wait_stats", "rr_geometry_layout",
                   "rr_preprocess_rows", "rr_preprocess_rows_views", "rr_unpack_rows", "rr_forward_from_geometry",
                   "rr_forward_render_geometry",
-                  "rr_backward_records", "rr_gauss_backward_views", "rr_set_forward_workspace"]
+                  "rr_backward_records", "rr_gauss_backward_views", "rr_set_forward_workspace",
+                  "rr_set_phase_a_event", "rr_phase_a_event", "rr_frame_open_tiles"]
 
 _raster = None
 _knn = None
@@ -155,6 +156,13 @@ def raster():
         L.rr_profile_enable.argtypes = [ci]
         L.rr_set_forward_workspace.restype = ci
         L.rr_set_forward_workspace.argtypes = [vp, sz]
+        L.rr_set_phase_a_event.restype = ci
+        L.rr_set_phase_a_event.argtypes = [ci]
+        L.rr_phase_a_event.restype = vp
+        L.rr_phase_a_event.argtypes = []
+        L.rr_frame_open_tiles.restype = ci
+        L.rr_frame_open_tiles.argtypes = [ctypes.POINTER(RRFrame), vp, ctypes.POINTER(vp), ctypes.POINTER(ci),
+                                          ctypes.POINTER(ci)]
         L.rr_set_tuning.restype = ci
         L.rr_set_tuning.argtypes = [ctypes.c_char_p, ci]
         L.rr_debug_set_fwd_trace.restype = ci
@@ -193,7 +201,7 @@ def raster():
 
 LOSS_LIB = os.environ.get("RAIN_LOSS_LIB") or os.path.join(LIB_DIR, "librain_loss.so")
 LOSS_SYMBOLS = ["rl_workspace_bytes", "rl_l1_ssim_forward", "rl_l1_ssim_backward", "rl_l1_ssim_forward_backward",
-                "rl_set_fused_band", "rl_last_error"]
+                "rl_l1_ssim_forward_backward_part", "rl_set_fused_band", "rl_last_error"]
 _loss = None
 
 
@@ -213,6 +221,9 @@ def loss_lib():
         L.rl_l1_ssim_forward_backward.restype = ci
         L.rl_l1_ssim_forward_backward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, ctypes.c_size_t, vp,
                                                   vp, vp, vp, vp]
+        L.rl_l1_ssim_forward_backward_part.restype = ci
+        L.rl_l1_ssim_forward_backward_part.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp,
+                                                       ctypes.c_size_t, vp, vp, vp, vp, vp, ci, ci, ci, vp, vp]
         L.rl_last_error.restype = ctypes.c_char_p
         _loss = L
     return _loss

@@ -61,6 +61,40 @@ struct Win {
     float w[11];
 };
 
+// The loss split around the rasterizer's early-stop phase B (rl_l1_ssim_forward_backward_part):
+// part 1 takes the bands whose rows phase A already finished, part 2 the others (part 0: all).
+// bits: rain_raster's open-tile bitmask of the frame (bit ty * tgx + tx, 16 x 16-px tiles).
+struct Split {
+    const uint32_t* bits;
+    int tgx, tgy, part;
+};
+constexpr int kTilePx = 16;  // the rasterizer's tile (rr_common.hpp TILE_X / TILE_Y)
+// Image rows [r0, r1) (clipped to the image) hold a tile phase A left open.  Wave-uniform.
+__device__ __forceinline__ bool rows_open(const Split& sp, int H, int r0, int r1) {
+    r0 = max(r0, 0);
+    r1 = min(r1, H);
+    if (r0 >= r1) return false;
+    const int ty0 = r0 / kTilePx, ty1 = min((r1 - 1) / kTilePx, sp.tgy - 1);
+    const uint32_t lo = (uint32_t)(ty0 * sp.tgx), hi = (uint32_t)((ty1 + 1) * sp.tgx);  // bits [lo, hi)
+    bool any = false;
+    for (uint32_t wd = (lo >> 5) + threadIdx.x; wd <= (hi - 1) >> 5; wd += 64) {
+        uint32_t m = sp.bits[wd];
+        if (wd == lo >> 5) m &= ~0u << (lo & 31);
+        if (wd == (hi - 1) >> 5) m &= ~0u >> (31 - ((hi - 1) & 31));
+        any = any || m != 0u;
+    }
+    return __ballot(any) != 0ull;
+}
+// forward band y (output rows [y TH_FWD, (y + 1) TH_FWD)) in part 1: its input rows are final
+__device__ __forceinline__ bool fwd_band_early(const Split& sp, int H, int y, int th_fwd) {
+    return !rows_open(sp, H, y * th_fwd - 5, (y + 1) * th_fwd + 5);
+}
+// backward band y in part 1: every forward band whose derivative rows it reads is in part 1
+__device__ __forceinline__ bool bwd_band_early(const Split& sp, int H, int y, int th_bwd, int th_fwd) {
+    const int fmin = max(0, y * th_bwd - 5) / th_fwd, fmax = min(H - 1, (y + 1) * th_bwd + 4) / th_fwd;
+    return !rows_open(sp, H, fmin * th_fwd - 5, (fmax + 1) * th_fwd + 5);
+}
+
 // 1/x: v_rcp_f32 (1 ulp) plus one Newton step
 __device__ __forceinline__ float rcp_nr(float x) {
     const float r = __builtin_amdgcn_rcpf(x);
@@ -172,7 +206,8 @@ template <int TH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_ssim_fwd(const float* __restrict__ img, const float* __restrict__ gt, int H,
                                                  int W, float lambda, float inv_n, Win win, float* __restrict__ g1,
                                                  float* __restrict__ g11, float* __restrict__ g12,
-                                                 float2* __restrict__ partial) {
+                                                 float2* __restrict__ partial, Split split) {
+    if (split.part && (split.part == 1) != fwd_band_early(split, H, blockIdx.y, TH)) return;  // block-uniform
     __shared__ float sp[2][NR][PW];
     const int c = blockIdx.z;
     const int x0 = blockIdx.x * TW - R, y0 = blockIdx.y * TH - R;
@@ -355,11 +390,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                                  const float* __restrict__ g1, const float* __restrict__ g11,
                                                  const float* __restrict__ g12, const float* __restrict__ grad_loss,
                                                  float* __restrict__ dimg, const float2* __restrict__ partial,
-                                                 int nb, float* __restrict__ loss, float* __restrict__ parts) {
+                                                 int nb, float* __restrict__ loss, float* __restrict__ parts,
+                                                 Split split) {
     if (loss && blockIdx.x == gridDim.x - 1) {  // the extra column (block-uniform): the forward's finalize
         if (blockIdx.y == 0 && blockIdx.z == 0) loss_finalize_one_wave(partial, nb, lambda, inv_n, loss, parts);
         return;
     }
+    if (split.part && (split.part == 1) != bwd_band_early(split, H, blockIdx.y, TH, TH_FWD)) return;
     __shared__ float sg[3][NR][PW];
     const int c = blockIdx.z;
     const int x0 = blockIdx.x * TW - R, y0 = blockIdx.y * TH - R;
@@ -584,6 +621,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RL_WPE_FUSED
 }
 
 int nblocks(int C, int H, int W) { return ((W + TW - 1) / TW) * ((H + TH_FWD - 1) / TH_FWD) * C; }
+
+// The two-pass forward + backward (the backward grid's extra column finalizes the loss, bitwise
+// rl_l1_ssim_forward's, when `loss` is given), over the bands of `sp`'s part (part 0: all).
+void launch_fwd_bwd(const float* img, const float* gt, int C, int H, int W, float lambda, const Win& win, float* g1,
+                    float2* partial, float* loss, float* parts, const float* grad_loss, float* dimg, const Split& sp,
+                    hipStream_t st) {
+    const size_t n = (size_t)C * H * W;
+    const float inv_n = (float)(1.0 / (double)n);
+    const dim3 gf((W + TW - 1) / TW, (H + TH_FWD - 1) / TH_FWD, C);
+    k_ssim_fwd<TH_FWD><<<gf, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, partial, sp);
+    const dim3 gb((W + TW - 1) / TW + (loss ? 1 : 0), (H + TH_BWD - 1) / TH_BWD, C);
+    k_ssim_bwd<TH_BWD><<<gb, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg,
+                                          partial, nblocks(C, H, W), loss, parts, sp);
+}
 int g_fused_band = 0;  // rows per block of the one-walk form; 0: the two passes
 int nblocks_fused(int C, int H, int W, int th) { return ((W + TWF - 1) / TWF) * ((H + th - 1) / th) * C; }
 
@@ -631,7 +682,7 @@ int rl_l1_ssim_forward(const float* img, const float* gt, int C, int H, int W, f
     const float inv_n = (float)(1.0 / (double)n);
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((W + TW - 1) / TW, (H + TH_FWD - 1) / TH_FWD, C);
-    k_ssim_fwd<TH_FWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g11, g12, partial);
+    k_ssim_fwd<TH_FWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g11, g12, partial, Split{});
     k_loss_finalize<<<1, kFinT, 0, st>>>(partial, nblocks(C, H, W), lambda, inv_n, loss, parts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -659,7 +710,7 @@ int rl_l1_ssim_backward(const float* img, const float* gt, int C, int H, int W, 
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((W + TW - 1) / TW, (H + TH_BWD - 1) / TH_BWD, C);
     k_ssim_bwd<TH_BWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg,
-                                            nullptr, 0, nullptr, nullptr);
+                                            nullptr, 0, nullptr, nullptr, Split{});
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("rl_l1_ssim_backward: ") + hipGetErrorString(e);
@@ -709,15 +760,56 @@ int rl_l1_ssim_forward_backward(const float* img, const float* gt, int C, int H,
         }
         return 0;
     }
-    const dim3 gf((W + TW - 1) / TW, (H + TH_FWD - 1) / TH_FWD, C);
-    k_ssim_fwd<TH_FWD><<<gf, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, partial);
-    // one extra column of the backward grid finalizes the loss (bitwise rl_l1_ssim_forward's)
-    const dim3 gb((W + TW - 1) / TW + 1, (H + TH_BWD - 1) / TH_BWD, C);
-    k_ssim_bwd<TH_BWD><<<gb, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg,
-                                          partial, nblocks(C, H, W), loss, parts);
+    launch_fwd_bwd(img, gt, C, H, W, lambda, win, g1, partial, loss, parts, grad_loss, dimg, Split{}, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("rl_l1_ssim_forward_backward: ") + hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+int rl_l1_ssim_forward_backward_part(const float* img, const float* gt, int C, int H, int W, float lambda,
+                                     const float* window, void* workspace, size_t workspace_bytes, float* loss,
+                                     float* parts, const float* grad_loss, float* dimg, const void* open_bits,
+                                     int tiles_x, int tiles_y, int part, void* wait_event, void* stream) {
+    if (!img || !gt || !window || !workspace || !grad_loss || !dimg || C <= 0 || H <= 0 || W <= 0 || !open_bits ||
+        (part != 1 && part != 2) || (part == 2 && !loss) || tiles_x * kTilePx < W || tiles_y * kTilePx < H ||
+        (tiles_x - 1) * kTilePx >= W || (tiles_y - 1) * kTilePx >= H) {
+        g_err = "rl_l1_ssim_forward_backward_part: bad argument";
+        return 1;
+    }
+    if (g_fused_band) {
+        g_err = "rl_l1_ssim_forward_backward_part: the one-band-walk form (rl_set_fused_band) has no split";
+        return 1;
+    }
+    if ((size_t)H * W * 4 >= (size_t)kOOB) {
+        g_err = "rl_l1_ssim_forward_backward_part: image plane larger than 2^30 bytes";
+        return 1;
+    }
+    if (workspace_bytes < rl_workspace_bytes(C, H, W) || nblocks(C, H, W) > NB_MAX) {
+        g_err = "rl_l1_ssim_forward_backward_part: workspace too small";
+        return 3;
+    }
+    Win win;
+    for (int i = 0; i < 11; i++) win.w[i] = window[i];
+    const size_t n = (size_t)C * H * W;
+    float* g1 = static_cast<float*>(workspace);
+    float2* partial = reinterpret_cast<float2*>(g1 + 3 * n);
+    hipStream_t st = (hipStream_t)stream;
+    if (wait_event) {
+        const hipError_t w = hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0);
+        if (w != hipSuccess) {
+            g_err = std::string("rl_l1_ssim_forward_backward_part: ") + hipGetErrorString(w);
+            return 2;
+        }
+    }
+    const Split sp{static_cast<const uint32_t*>(open_bits), tiles_x, tiles_y, part};
+    launch_fwd_bwd(img, gt, C, H, W, lambda, win, g1, partial, part == 2 ? loss : nullptr, parts, grad_loss, dimg, sp,
+                   st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = std::string("rl_l1_ssim_forward_backward_part: ") + hipGetErrorString(e);
         return 2;
     }
     return 0;

@@ -161,8 +161,9 @@ constexpr uint32_t kEarlyDen = 3, kEarlyMin = 1u << 16;
 uint32_t g_early_den = kEarlyDen, g_early_min = kEarlyMin;
 
 // Binning paths (count_pairs below).  g_a_gather: phase A by the windowed duplicate + stable bin sort
-// (0, default), by the gather path over the split scan's phase-A list (2) or over every Gaussian of
-// the frame (1, no split scan then if phase B does without it too).  g_b_gather: phase B by the
+// (0, default), by the windowed duplicate + per-bin count / scatter and the per-bin sort on
+// unordered runs (3), by the gather path over the split scan's phase-A list (2) or over every
+// Gaussian of the frame (1, no split scan then if phase B does without it too).  g_b_gather: phase B by the
 // gather path over the phase-B list (1, default) or over every Gaussian (2), by the windowed path (0),
 // or by the last frame's phase-B size (-1).
 int g_a_gather = 0;
@@ -170,8 +171,9 @@ int g_b_gather = 1;
 constexpr int kGatherMaxBins = 16384;  // rr_bin.hip kBinScanMax
 bool gather_bins_fit(int W, int H) { return bins_x(grid_x(W)) * bins_y(grid_y(H)) <= kGatherMaxBins; }
 // Both phases always by the gather paths: the compact binning layout (carve_bin).
+bool a_gather_dup() { return g_a_gather == 1 || g_a_gather == 2; }  // phase A's duplicate by the gather path
 bool compact_binning(int W, int H) {
-    return g_a_gather != 0 && (g_b_gather == 1 || g_b_gather == 2) && gather_bins_fit(W, H);
+    return a_gather_dup() && (g_b_gather == 1 || g_b_gather == 2) && gather_bins_fit(W, H);
 }
 
 struct Bin {
@@ -599,6 +601,9 @@ thread_local WsRange g_fwd_ws, g_ws_clean;
 // (its order array): the backward then needs no prologue at all once the workspace is clean.
 thread_local const uint32_t* g_order_ready = nullptr;
 int g_fwd_clear = 1;  // rr_set_tuning "forward_clear" 0: registrations are dropped (A/B)
+// rr_set_phase_a_event: an event recorded after each render's phase-A blend (this thread's renders)
+thread_local hipEvent_t g_phase_a_ev = nullptr;
+thread_local bool g_phase_a_done = false;
 
 // The windowed duplicate's window starts from the split scan's marks (default) or from a
 // window-starts launch (rr_set_tuning "split_marks" 0)
@@ -622,7 +627,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     d.tiles = gm.tiles; d.depth_keys = gm.depth_keys; d.ft = gm.ft;
     const PhaseHints h = phase_hints(L, early);
     const bool fit = gather_bins_fit(W, H);
-    const bool gather_a = fit && g_a_gather;
+    const bool gather_a = fit && a_gather_dup();
+    const bool count_a = fit && g_a_gather == 3;  // windowed duplicate, count / scatter bin sort
     const bool gather = early && fit && phase_b_gather();
     if (bn.compact != (gather_a && (gather || !early)) && bn.compact)
         return fail(RR_ERR_ARG, "binning path changed between carving and rendering");
@@ -657,7 +663,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         d.n_list = &gm.ft->GA; d.idx = gm.lists.idx_a; d.off = gm.lists.off_a;
         d.first = marks_a ? gm.lists.first_a : bn.first;
         d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L_dev = &gm.ft->LA;
-        d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
+        // (count_a: the windows' digit counts are not read; one digit keeps their histogram trivial)
+        d.keys = keys; d.vals = bn.vals; d.dbits = count_a ? 0 : pa.dbits0; d.counts = pa.counts;
         d.starts_done = marks_a;
         if (early && !gather && !marks_a && !marks_b) {
             d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
@@ -667,6 +674,12 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         d.first_b = nullptr; d.nwin_b = 0; d.starts_done = false;
     }
     RR_STAGE_CHECK("duplicate");
+    if (count_a) {  // the windows' pairs (dense, [0, LA)) counted and scattered into their bins
+        StageTimer tm(RR_STAGE_RANGES, st);
+        launch_sortexpand_small<K>(P, keys, bn.vals, &gm.ft->LA, im.bin_cnt_a, bn.vals_sorted, gm.depth_keys, gm.ft,
+                                   gx, gy, 0u, bn.point_list, im.ranges, nullptr, im.bounds_a, nullptr, st);
+        RR_STAGE_CHECK("sort-expand (count / scatter)");
+    } else {
     {
         StageTimer tm(RR_STAGE_TILE_SORT, st);
         RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.vals_sorted, L, 0, bn.bits,
@@ -681,6 +694,7 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     }
     RR_STAGE_CHECK("sort-expand");
     }
+    }
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = early ? kBlendPhaseA : kBlendSingle;
@@ -691,6 +705,10 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         launch_blend_fwd(b, st);
         b.clear = nullptr;
         b.clear_n4 = 0;
+        if (g_phase_a_ev) {  // the rows of every tile phase A finished are final from here on
+            RR_CHECK(hipEventRecord(g_phase_a_ev, st), "phase-A event");
+            g_phase_a_done = true;
+        }
     }
     RR_STAGE_CHECK("blend forward");
     if (!early) return RR_OK;
@@ -834,9 +852,9 @@ int rr_forward_render_aux(const rr_frame* f, const rr_camera* cam, const rr_gaus
 namespace {
 
 // Binning + blend of a frame whose geometry buffer holds the sorted, scanned per-Gaussian arrays.
-int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
-                 void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
-                 float* out_normal, void* stream) {
+int render_frame_body(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
+                      void* image_buffer, void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color,
+                      float* out_depth, float* out_normal, void* stream) {
     const int P = f->P, W = f->width, H = f->height, L = num_pairs;
     const int cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
     // a workspace registration is used by this render (or dropped by it) either way
@@ -877,6 +895,21 @@ int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void
     const bool early = !(f->flags & RR_FLAG_FULL_BINNING) && g_early_den > 1 && (uint32_t)L >= g_early_min;
     return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
                    : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
+}
+
+// rr_set_phase_a_event: the render records the event right after phase A's blend launch
+// (render_tiles) or, on any path without one, after all its work — a waiter never sees it early.
+int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
+                 void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
+                 float* out_normal, void* stream) {
+    g_phase_a_done = false;
+    const int rc = render_frame_body(f, cam, radii, geom_buffer, image_buffer, binning_buffer, binning_bytes,
+                                     num_pairs, out_color, out_depth, out_normal, stream);
+    if (g_phase_a_ev && !g_phase_a_done) {
+        const hipError_t e = hipEventRecord(g_phase_a_ev, (hipStream_t)stream);
+        if (e != hipSuccess && rc == RR_OK) return fail(RR_ERR_HIP, std::string("phase-A event: ") + hipGetErrorString(e));
+    }
+    return rc;
 }
 
 }  // namespace
@@ -1261,7 +1294,7 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     out->l_eff = s;
     // phase A's pairs, and the phase-B pairs kept for the tiles phase A left open (the binning path
     // the frame took: the tuning in force now, as at its render)
-    const bool gather_a = g_a_gather && gather_bins_fit(W, H);
+    const bool gather_a = a_gather_dup() && gather_bins_fit(W, H);
     const bool gather_b = phase_b_gather() && gather_bins_fit(W, H);
     out->num_binned = (gather_a ? (int64_t)cnt[2] : (int64_t)ft.LA) + (gather_b ? cnt[3] : cnt[0]);
     return RR_OK;
@@ -1300,6 +1333,32 @@ int rr_set_forward_workspace(void* workspace, size_t bytes) {
     if (workspace && (((uintptr_t)workspace & 15u) != 0 || bytes % 16 != 0))
         return fail(RR_ERR_ARG, "workspace must be 16-byte aligned and a multiple of 16 bytes");
     g_fwd_ws = workspace && bytes ? WsRange{workspace, bytes} : WsRange{};
+    return RR_OK;
+}
+
+int rr_set_phase_a_event(int on) {
+    if (on && !g_phase_a_ev) {
+        const hipError_t e = hipEventCreateWithFlags(&g_phase_a_ev, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            g_phase_a_ev = nullptr;
+            return fail(RR_ERR_HIP, std::string("phase-A event: ") + hipGetErrorString(e));
+        }
+    } else if (!on && g_phase_a_ev) {
+        (void)hipEventDestroy(g_phase_a_ev);
+        g_phase_a_ev = nullptr;
+    }
+    return RR_OK;
+}
+
+void* rr_phase_a_event(void) { return g_phase_a_ev; }
+
+int rr_frame_open_tiles(const rr_frame* f, const void* image_buffer, const void** bits, int* tiles_x, int* tiles_y) {
+    if (!f || !image_buffer || !bits || !tiles_x || !tiles_y) return fail(RR_ERR_ARG, "null argument");
+    if (f->width <= 0 || f->height <= 0) return fail(RR_ERR_ARG, "empty frame");
+    const Img im = carve_img(const_cast<void*>(image_buffer), f->width, f->height);
+    *bits = im.open_bits;
+    *tiles_x = grid_x(f->width);
+    *tiles_y = grid_y(f->height);
     return RR_OK;
 }
 
@@ -1349,7 +1408,7 @@ int rr_set_tuning(const char* key, int value) {
         return RR_OK;
     }
     if (key && std::string(key) == "phase_a_gather") {
-        g_a_gather = value == 1 || value == 2 ? value : 0;
+        g_a_gather = value >= 1 && value <= 3 ? value : 0;
         return RR_OK;
     }
     if (set_tuning(key, value) != 0) return fail(RR_ERR_ARG, std::string("unknown tuning key: ") + (key ? key : "(null)"));

@@ -26,6 +26,8 @@ PATHS = {
     "gather_a_all": {"phase_a_gather": (1, 0), "phase_b_gather": (2, 1)},
     "gather_a_list": {"phase_a_gather": (2, 0)},
     "gather_a_list_lsd": {"phase_a_gather": (2, 0), "sx_bucket": (0, 1)},
+    "count_a": {"phase_a_gather": (3, 0)},  # windowed duplicate, count / scatter bin sort
+    "count_a_global_runs": {"phase_a_gather": (3, 0), "sx_lds_cap": (64, 0)},
     "windowed_b": {"phase_b_gather": (0, 1)},
     "bin_bounds_launch": {"bounds_in_sort": (0, 1)},
     # units of kSplitWin (2048) pairs at these sizes: window starts from the split scan's marks

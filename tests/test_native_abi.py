@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared(header):
     src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|size_t|char\s*\*|char)\s*\*?\s*(r[rlt]_\w+|sk_\w+)\s*\(", src,
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|size_t|char\s*\*|char|void\s*\*)\s*\*?\s*(r[rlt]_\w+|sk_\w+)\s*\(", src,
                                  flags=re.M)))
 
 

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--api", action="store_true", help="also time the reference-API step (Trainer(fused=False))")
     ap.add_argument("--pack", action="store_true", help="parameters and moments in three flat buffers (pack_flat_state)")
     ap.add_argument("--tune", action="append", default=[], help="rr_set_tuning key=value (repeatable)")
+    ap.add_argument("--overlap-loss", action="store_true",
+                    help="the loss of phase A's rows on a side stream during phase B (Trainer.overlap_loss)")
     ap.add_argument("--no-fuse-next", action="store_true",
                     help="the next frame's preprocess as its own launch (Trainer.fuse_next = False)")
     ap.add_argument("--skew-state", type=int, default=0,
@@ -73,6 +75,8 @@ def main():
     tr = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(seed=0), scene_extent=4.4)
     if a.no_fuse_next:
         tr.fuse_next = False
+    if a.overlap_loss:
+        tr.overlap_loss = True
     if a.pack:
         g.optimizer.fused_step(g)  # creates the moment state the packing moves
         g.pack_flat_state(1)
