@@ -33,6 +33,14 @@ namespace rr {
 #ifndef RR_BWD_BF
 #define RR_BWD_BF 0
 #endif
+// RR_BWD_GLDS: the next round's records go global -> LDS directly (global_load_lds_dwordx4 into the
+// other half of a double-buffered stage) instead of through 12 prefetch VGPRs and a ds_write:
+// 159 -> 121 VGPRs, 3 -> 4 waves per SIMD; blend backward 0.2427 / 0.2449 -> 0.2384 / 0.2401 ms,
+// step 1.0600 / 1.0597 -> 1.0523 / 1.0527 ms (profiles/r05_bwd_glds_ab.jsonl).  (The same staging
+// in the forward blend measured slower, 0.188 vs 0.170 ms: profiles/r05_fwd_glds_ab.jsonl.)
+#ifndef RR_BWD_GLDS
+#define RR_BWD_GLDS 1
+#endif
 
 // OCC: minimum waves per SIMD requested from the register allocator.  The default 3 leaves the
 // compiler its 132 VGPRs without spills; 4 caps it at 128 with 96 B/lane of scratch in the
@@ -54,10 +62,17 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
     const int py0 = ty * TILE_Y + (lane >> 4) + 4 * w * PPL;
     const float pfx = (float)px;
 
+#if RR_BWD_GLDS
+    __shared__ float4 s_a2[2][B];
+    __shared__ float4 s_b2[2][B];
+    __shared__ float4 s_c2[2][B];
+    __shared__ uint32_t s_id2[2][B];
+#else
     __shared__ float4 s_a[B];
     __shared__ float4 s_b[B];
     __shared__ float4 s_c[B];
     __shared__ uint32_t s_id[B];
+#endif
     __shared__ float s_g[NW][B * NGRAD];
 
     const size_t HW = (size_t)a.H * a.W;
@@ -92,6 +107,38 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
     const float ddelx_dx = 0.5f * a.W;
     const float ddely_dy = 0.5f * a.H;
 
+#if RR_BWD_GLDS
+    // round r's records land in stage r & 1: issued (global -> LDS) one round ahead; each wave
+    // writes its 64 lanes' records contiguously, which is the stage's layout (record t at [t])
+    auto glds_round = [&](int buf, uint32_t id) {
+        typedef __attribute__((address_space(1))) const void* gp;
+        typedef __attribute__((address_space(3))) void* lp;
+        const float4* src = reinterpret_cast<const float4*>(a.splats) + 3 * (size_t)id;
+        __builtin_amdgcn_global_load_lds((gp)(src + 0), (lp)&s_a2[buf][64 * w], 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gp)(src + 1), (lp)&s_b2[buf][64 * w], 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gp)(src + 2), (lp)&s_c2[buf][64 * w], 16, 0, 0);
+    };
+    // ids: lanes past the list load record 0 (staged, never read); the next round's id is loaded
+    // a round ahead of its records
+    uint32_t cid = t < nmax ? a.point_list[pair_at(nmax - 1 - t)] : 0u;
+    glds_round(0, cid);
+    uint32_t nid = B + t < nmax ? a.point_list[pair_at(nmax - 1 - (B + t))] : 0u;
+    for (int base = 0, cur = 0; base < nmax; base += B, cur ^= 1) {
+        float4* const s_a = s_a2[cur];
+        float4* const s_b = s_b2[cur];
+        float4* const s_c = s_c2[cur];
+        uint32_t* const s_id = s_id2[cur];
+        s_id[t] = cid;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this round's records are in LDS
+        __syncthreads();
+        if (base + B < nmax) {  // block-uniform: the next round's records and the one after's ids
+            glds_round(cur ^ 1, nid);
+            cid = nid;
+            const int k3 = base + 2 * B + t;
+            nid = k3 < nmax ? a.point_list[pair_at(nmax - 1 - k3)] : 0u;
+        }
+        const int cnt = min(B, nmax - base);
+#else
     uint32_t nid = 0;
     float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
     if (t < nmax) {
@@ -112,6 +159,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             load_splat(a.splats, nid, na, nb, nc);
         }
         const int cnt = min(B, nmax - base);
+#endif
 #if RR_BWD_DEFER
         // Software-pipelined by hand: the block after pair j's branched pixel bodies holds pair
         // j's nine per-lane sums, the LDS record reads and the four exp2 chains of pair j + 1, and
