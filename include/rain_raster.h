@@ -394,7 +394,8 @@ int rr_profile_enable(int enable);
 int rr_profile_select(unsigned stage_mask);
 
 /* Tuning knob (diagnostics / A-B tests): wave64s per 16x16 tile used by the forward and backward
- * blend kernels (1, 2 or 4; 0 restores the default).  Results are identical for every choice. */
+ * blend kernels (1, 2 or 4; 0 restores the default; backward 3: one wave per tile compiled for 3
+ * instead of 4 waves per SIMD).  Results are identical for every choice. */
 int rr_set_blend_config(int fwd_waves, int bwd_waves);
 
 /* Runtime tuning knobs (A/B tests; defaults are the measured best):

@@ -41,6 +41,17 @@ namespace rr {
 #ifndef RR_BWD_GLDS
 #define RR_BWD_GLDS 1
 #endif
+// RR_BWD_PAIR2: two pairs' gradient components reduced across the wave together (wave_sum18, 48
+// instead of 56 VALU per two pairs, bitwise the same sums), with the default kernel held at 4 waves
+// per SIMD (RR_BWD_OCC: 128 VGPRs, 20 B/lane of scratch): blend backward 0.2383 / 0.2361 ->
+// 0.2260 / 0.2276 ms, step 1.0514 / 1.0499 -> 1.0406 / 1.0415 ms; at 3 waves (134 VGPRs) 0.2333 /
+// 0.2339 (profiles/r05_bwd_pair2_ab.jsonl)
+#ifndef RR_BWD_OCC
+#define RR_BWD_OCC 4  // the default kernel's minimum waves per SIMD (launch bounds)
+#endif
+#ifndef RR_BWD_PAIR2
+#define RR_BWD_PAIR2 1
+#endif
 
 // OCC: minimum waves per SIMD requested from the register allocator.  The default 3 leaves the
 // compiler its 132 VGPRs without spills; 4 caps it at 128 with 96 B/lane of scratch in the
@@ -247,6 +258,106 @@ __global__ __launch_bounds__(64 * NW, OCC) void k_blend_bwd(BlendBwdArgs a) {
             float t0, t1, t2;
             wave_sum9(p0, p1, p2, p3, p4, p5, g6, g7, g8, t0, t1, t2);
             red9_store(&s_g[w][j * NGRAD], lane, t0, t1, t2);
+        }
+#elif RR_BWD_PAIR2
+        // two pairs per reduction (wave_sum18): each pair's pixel work as in the loop below, in
+        // order (T and R advance pair by pair), then one interleaved reduction of their 18 sums
+        auto pair_grads = [&](int j, float (&g)[NGRAD]) -> bool {
+            const int contributor = nmax - 1 - (base + j);
+            const float4 A = s_a[j];
+            const float4 Bv = s_b[j];
+            float g0, g1, g2, g3, g4, g5, g6 = 0.f, g7 = 0.f, g8 = 0.f;
+            bool any = false;
+            // The conic-side terms are linear in v = e * dL/dalpha with e = opacity G (the unclamped
+            // alpha), and a lane's PPL pixels share its column (dx): per pixel only S_v, S_v.dy,
+            // S_v.dy^2 are accumulated, and the six components follow once per lane and pair
+            // (g0 = S_v dx, g1 = S_vdy, g2 = dx g0, g3 = dx g1, g4 = S_vdy2, g5 = S_v / opacity):
+            // 5 VALU per pixel instead of 11.
+            const float dx = A.x - pfx;
+            const P2X px2 = blend_p2_x(A.z, A.w, Bv.y, dx);  // identical to the forward's values
+            float sv = 0.f, svdy = 0.f, svdy2 = 0.f;
+            const float4 Cc = s_c[j];  // once per pair (not per active row)
+            // every pixel's alpha first, in one basic block, so that the PPL exp chains interleave
+            // instead of each waiting behind the previous pixel's branched body (LLVM sinks each
+            // back into its pixel's block without the opaque uses): blend bwd 0.2453 -> 0.2435 ms
+            // per step in an interleaved A/B; the reciprocals hoisted too (paid for inactive pixels
+            // as well) measured 0.2491 (profiles/r03_blend_bwd_hoist_ab.jsonl)
+            float ev[PPL], av[PPL];
+            bool acv[PPL];
+#pragma unroll
+            for (int q = 0; q < PPL; q++) {
+                const float dy = A.y - (float)(py0 + 4 * q);
+                const float e2 = blend_e2(px2, Bv.x, dy);
+                ev[q] = __builtin_amdgcn_exp2f(e2);  // o G
+                av[q] = fminf(0.99f, ev[q]);
+                acv[q] = contributor < last[q] && e2 <= Bv.y && av[q] >= 1.0f / 255.0f;
+            }
+#pragma unroll
+            for (int q = 0; q < PPL; q++) asm volatile("" : "+v"(ev[q]), "+v"(av[q]));
+#pragma unroll
+            for (int q = 0; q < PPL; q++) {
+                const float dy = A.y - (float)(py0 + 4 * q);
+                const float e = ev[q], alpha = av[q];
+                const bool act = acv[q];
+                if (act) {
+                    any = true;
+                    // both divisions by (1 - alpha) share one reciprocal; the Newton step keeps T's
+                    // recovery within an ulp per pair over lists of thousands of pairs (the bare
+                    // v_rcp_f32 measured 2 % faster on this kernel, 0.238 vs 0.243 ms)
+                    const float inv = rcp_nr(1.f - alpha);
+                    T[q] = T[q] * inv;                // T_i, the transmittance in front of this Gaussian
+                    const float dchannel_dcolor = alpha * T[q];
+                    const float cdp = Cc.x * dp0[q] + Cc.y * dp1[q] + Cc.z * dp2[q];
+                    g6 += dchannel_dcolor * dp0[q];
+                    g7 += dchannel_dcolor * dp1[q];
+                    g8 += dchannel_dcolor * dp2[q];
+                    const float d = cdp - R[q];  // R: accum_rec . dL/dpix in front of this Gaussian
+                    // dL/dalpha = T_i (c - accum_rec) . dL/dpix - T_final (bg . dL/dpix) / (1 - alpha)
+                    const float dL_dalpha = d * T[q] + tfbg[q] * inv;
+                    // the reference's next accum_rec update (last_alpha = alpha, last_color = c),
+                    // applied now instead of at the next contributing pair: the same fma on the
+                    // same values, without carrying last_alpha / last_color
+                    R[q] = __builtin_fmaf(alpha, d, R[q]);
+                    const float v = e * dL_dalpha;
+                    const float vdy = v * dy;
+                    sv += v;
+                    svdy += vdy;
+                    svdy2 = __builtin_fmaf(vdy, dy, svdy2);
+                }
+            }
+            // unconditionally: with no active pixel the sums are 0 and so are these (a branch here
+            // costs a zero-initialising move per component and pair)
+            g0 = sv * dx;
+            g1 = svdy;
+            g2 = g0 * dx;
+            g3 = g1 * dx;
+            g4 = svdy2;
+            g5 = sv * s_c[j].w;  // 1 / opacity
+            g[0] = g0;
+            g[1] = g1;
+            g[2] = g2;
+            g[3] = g3;
+            g[4] = g4;
+            g[5] = g5;
+            g[6] = g6;
+            g[7] = g7;
+            g[8] = g8;
+            return any;
+        };
+        for (int j = 0; j < cnt; j += 2) {
+            float ga[NGRAD], gb[NGRAD];
+            const bool anya = pair_grads(j, ga);
+            const bool has_b = j + 1 < cnt;  // block-uniform
+            bool anyb = false;
+            if (has_b) {
+                anyb = pair_grads(j + 1, gb);
+            } else {
+#pragma unroll
+                for (int k = 0; k < NGRAD; k++) gb[k] = 0.f;
+            }
+            float t[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+            if (__ballot(anya || anyb) != 0ull) wave_sum18(ga, gb, t);
+            red18_store(&s_g[w][j * NGRAD], lane, t, has_b);
         }
 #else
         for (int j = 0; j < cnt; j++) {
@@ -518,9 +629,9 @@ void launch_blend_bwd(const BlendBwdArgs& a, hipStream_t st) {
     const int nw = g_bwd_waves ? g_bwd_waves : env_waves("RAIN_BLEND_BWD_WAVES", kBwdWavesDefault);
     switch (nw) {
         case 2: k_blend_bwd<2, 1><<<T, 128, 0, st>>>(a); break;
-        case 3: k_blend_bwd<1, 4><<<T, 64, 0, st>>>(a); break;  // A/B variant: 1 wave capped at 128 VGPRs
+        case 3: k_blend_bwd<1, 3><<<T, 64, 0, st>>>(a); break;  // A/B variant: 1 wave, up to 168 VGPRs
         case 4: k_blend_bwd<4, 1><<<T, 256, 0, st>>>(a); break;
-        default: k_blend_bwd<1, 3><<<T, 64, 0, st>>>(a); break;
+        default: k_blend_bwd<1, RR_BWD_OCC><<<T, 64, 0, st>>>(a); break;
     }
 }
 

@@ -483,6 +483,30 @@ __device__ __forceinline__ void wave_sum9(float v0, float v1, float v2, float v3
     t1 = row16_sum(swap16_add(r2, r3));
     t2 = row16_sum(swap16_add(r4, 0.f));
 }
+// Two pairs' nine components (a, b) at once: 48 VALU ops instead of 2 x 28 — the swap stages pair
+// a's and b's components instead of two of one pair's, so the row sums run on 5 registers, not 6.
+// The same adds on the same values as two wave_sum9 calls (bitwise the same sums).  Result: lane
+// 16r+15 holds component 2i + (r & 1) of pair r >> 1 in t[i] (i < 4), and lanes 15 / 47 hold
+// component 8 of a / b in t[4] (see red18_store).
+__device__ __forceinline__ void wave_sum18(const float (&a)[NGRAD], const float (&b)[NGRAD], float (&t)[5]) {
+    float r[NGRAD];
+#pragma unroll
+    for (int k = 0; k < NGRAD; k++) r[k] = swap32_add(a[k], b[k]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) t[i] = row16_sum(swap16_add(r[2 * i], r[2 * i + 1]));
+    t[4] = row16_sum(swap16_add(r[8], 0.f));
+}
+__device__ __forceinline__ void red18_store(float* dst, int lane, const float (&t)[5], bool has_b) {
+    if ((lane & 15) == 15) {
+        const int row = lane >> 4, sel = row >> 1, odd = row & 1;
+        if (sel == 0 || has_b) {
+            float* d = dst + sel * NGRAD;
+#pragma unroll
+            for (int i = 0; i < 4; i++) d[2 * i + odd] = t[i];
+            if (!odd) d[8] = t[4];
+        }
+    }
+}
 __device__ __forceinline__ void red9_store(float* dst, int lane, float t0, float t1, float t2) {
     if ((lane & 15) == 15) {
         const int row = lane >> 4;
