@@ -3,7 +3,9 @@
 (BASELINE.json metric; configs[2] at N=1, configs[3] view-sharded at N>1).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py ...)
+    (N>1 under a launcher: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
+     127.0.0.1 ... bench.py --gpus N ...; WORLD_SIZE must equal --gpus.  N>1 without one: bench.py starts
+     that launcher itself as a child process, before anything touches the GPU, and exits with its code)
 
 A "step" is one iteration of the reference's train.py loop (train.py:71-147) on every rank:
 lr update, render forward, L1+SSIM loss, backward through the MI355X rasterizer, (gradient
@@ -29,6 +31,7 @@ Extra objects on the JSON line:
                 overall (step_dominant)
   cpu_baseline  the CPU oracle (oracle/raster_oracle.c, "port") on the same frame, timed on rank 0
                 at every N (--no-cpu-baseline skips it)
+  sync_loss_*   the timed step with the reference's per-iteration `loss.item()` read-back (train.py:120)
 """
 from __future__ import annotations
 
@@ -46,9 +49,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 VALU_PEAK_TFLOPS = 157.3
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU).  N > 1 without a torch.distributed.run environment: this "
+                        "process starts `python -m torch.distributed.run --nproc-per-node N ... bench.py` as "
+                        "a child and exits with its code; under a launcher it must equal WORLD_SIZE")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--points", type=int, default=1_000_000)
@@ -67,7 +73,59 @@ def parse():
     p.add_argument("--force-dist", action="store_true",
                    help="init the RCCL process group and run the sharded exchange path even at world 1 "
                         "(rehearses the multi-GPU code path on one GPU; not the headline configuration)")
-    return p.parse_args()
+    p.add_argument("--sync-loss-steps", type=int, default=20,
+                   help="steps of the extra leg that reads the loss back every iteration (train.py:120)")
+    return p.parse_args(argv)
+
+
+def launch_plan(gpus, env):
+    """What this invocation does with `--gpus`: ("run", world) runs the benchmark in this process as
+    one rank of `world`; ("spawn", n) starts n ranks through torch.distributed.run as a child process;
+    ("error", msg) refuses.  Pure (no torch, no GPU), so the parent of a spawn never touches the GPU
+    before the ranks do (an exec from a GPU-initialised process is forbidden on the box, and a
+    parent holding the device would count against the box's per-card process limit)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        try:
+            world = int(ws)
+        except ValueError:
+            return ("error", f"WORLD_SIZE={ws!r} is not an integer")
+        if gpus is not None and gpus != world:
+            return ("error", f"--gpus {gpus} does not match WORLD_SIZE={world} from the launcher")
+        return ("run", world)
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        return ("error", f"--gpus {n}: need at least one GPU")
+    return ("spawn", n) if n > 1 else ("run", 1)
+
+
+def spawn_command(n, argv, port, script=None):
+    """The child command line of a spawn: one rank per GPU on this node, rendezvous on 127.0.0.1,
+    bench.py with the same arguments (WORLD_SIZE from the launcher then equals --gpus)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", script or os.path.join(ROOT, "bench.py"), *argv]
+
+
+def _spawn(n, argv, script=None):
+    """Run the N ranks as a child process (subprocess, not exec), its stdout / stderr inherited, so
+    rank 0's JSON line is this process's output; a SIGTERM / SIGINT to this process is passed on."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    child = subprocess.Popen(spawn_command(n, argv, port, script), env=env)
+
+    def forward(sig, _frame):
+        child.send_signal(sig)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    return child.wait()
 
 
 MODELED = ("preprocess", "scan", "duplicate", "tile_sort", "ranges", "blend_fwd", "blend_bwd", "gauss_bwd")
@@ -122,11 +180,18 @@ def gauss_bwd_bytes(P, V, K, M, fused_adam=True, next_frame=False):
 
 def main():
     args = parse()
+    what, val = launch_plan(args.gpus, os.environ)
+    if what == "error":
+        print(f"bench.py: {val}", file=sys.stderr)
+        return 2
+    if what == "spawn":
+        rc = _spawn(val, sys.argv[1:])
+        return rc if rc >= 0 else 128 - rc
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = val
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     force = args.force_dist
@@ -254,6 +319,12 @@ def main():
     # the reference's share (1 densify/prune iteration in 100) on top of the measured steps
     ms_1in100 = ms_per_step + densify_extra_ms / 100.0 if n_densify == 0 else ms_per_step
 
+    # the same step with the reference's per-iteration loss read-back (train.py:120 `loss.item()`,
+    # a device -> host sync every iteration), which the timed loop leaves out: its cost, measured
+    sync_it0 = _clear_window(end_iter + 1, 3 + args.sync_loss_steps)
+    sync_ms = _timed_steps(trainer, sync_it0, args.sync_loss_steps, world, dev, sync_loss=True)
+    sync_end = sync_it0 + 3 + args.sync_loss_steps - 1
+
     # the reference's own timing bracket (train.py:71-117: iter_start before render, iter_end after
     # loss.backward()): render forward + L1/SSIM + backward, no optimizer step, no densification
     bracket_ms = _bracket(trainer, cams, gts, K if K < 50 else 50, world, dev)
@@ -264,7 +335,7 @@ def main():
 
     # the same iteration through the reference's own API (what an unchanged train.py:109-147 runs):
     # render() -> GaussianRasterizer autograd -> getters' autograd -> torch.optim.Adam
-    api_it0 = (end_iter // 100 + 1) * 100 + 1
+    api_it0 = (sync_end // 100 + 1) * 100 + 1
     api_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0, K if K < 30 else 30, world, dev,
                       torch_adam=False)
     api_ta_ms = _api_leg(gauss, cams, gts, opt, pipe, extent, api_it0 + 40, K if K < 30 else 30, world, dev)
@@ -401,6 +472,10 @@ def main():
                    "parallelism": (f"dp{world} (view-parallel, Gaussian-sharded: RCCL all-to-all of per-view "
                                    f"records)" if world > 1 else "dp1 (RCCL exchange forced)" if force else "dp1"),
                    "iterations": [start_iter, end_iter], "densify_events_in_window": n_densify},
+        # the timed step plus the reference's per-iteration `loss.item()` host read-back (train.py:120)
+        "sync_loss_iters_per_s": round(world * 1000.0 / sync_ms, 3),
+        "sync_loss_ms_per_step": round(sync_ms, 4),
+        "sync_loss_window": [sync_it0 + 3, sync_end],
         "densify_iter_ms": round(one_ms[D1], 3),
         "ordinary_iter_ms_alone": round(one_ms[D1 - 1], 3),
         "densify_extra_ms": round(densify_extra_ms, 3),
@@ -433,6 +508,38 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1 or force:
         dist.destroy_process_group()
+
+
+def _clear_window(start, n):
+    """First iteration s >= start such that s .. s+n-1 holds no densify / reset iteration (no
+    multiple of 100: train.py:136-143)."""
+    s = start
+    while any(i % 100 == 0 for i in range(s, s + n)):
+        s = (s // 100 + 1) * 100 + 1
+    return s
+
+
+def _timed_steps(trainer, it0, n, world, dev, sync_loss=False):
+    """ms per training step over iterations it0+3 .. it0+2+n (three untimed first), max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    for it in range(it0, it0 + 3):
+        trainer.step(it, sync_loss=sync_loss)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for it in range(it0 + 3, it0 + 3 + n):
+        info = trainer.step(it, sync_loss=sync_loss)
+        assert not sync_loss or info.loss is not None
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([t], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        t = float(e.item())
+    return 1000.0 * t / n
 
 
 def _bracket(trainer, cams, gts, n, world, dev, low_pass=None):
@@ -681,4 +788,4 @@ def _cpu_baseline(gauss, cam, bg, D, threads, views=3):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

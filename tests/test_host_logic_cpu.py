@@ -57,3 +57,64 @@ def test_gauss_bwd_byte_models():
     assert b.algorithmic_bytes("gauss_bwd", st, P, 1920, 1080, K) == single
     assert b.algorithmic_bytes("gauss_bwd", st, P, 1920, 1080, K, 1, True) == b.gauss_bwd_views_bytes(P, K, M, 1)
     assert b.algorithmic_bytes("gauss_bwd", st, P, 1920, 1080, K, 8) == b.gauss_bwd_views_bytes(P, K, M, 8)
+
+
+@pytest.mark.parametrize("gpus,env,plan", [
+    (None, {}, ("run", 1)),                         # the driver's default: one rank, this process
+    (1, {}, ("run", 1)),
+    (8, {}, ("spawn", 8)),                          # `bench.py --gpus 8` with no launcher: spawn 8 ranks
+    (2, {"WORLD_SIZE": "2"}, ("run", 2)),           # under torch.distributed.run
+    (None, {"WORLD_SIZE": "4"}, ("run", 4)),
+])
+def test_bench_launch_plan(gpus, env, plan):
+    assert _bench().launch_plan(gpus, env) == plan
+
+
+@pytest.mark.parametrize("gpus,env", [(4, {"WORLD_SIZE": "2"}), (1, {"WORLD_SIZE": "8"}), (0, {}),
+                                      (2, {"WORLD_SIZE": "x"})])
+def test_bench_launch_plan_refuses(gpus, env):
+    what, msg = _bench().launch_plan(gpus, env)
+    assert what == "error" and msg
+
+
+def test_bench_refuses_gpus_world_mismatch_before_torch():
+    """A launcher's WORLD_SIZE that differs from --gpus ends bench.py with a non-zero code, before
+    torch is imported (so nothing has touched a GPU)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-X", "importtime", os.path.join(ROOT, "bench.py"), "--gpus", "4"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "does not match WORLD_SIZE=2" in r.stderr
+    assert " torch" not in "\n".join(l for l in r.stderr.splitlines() if "import time" in l)
+
+
+def test_bench_spawn_runs_n_ranks(tmp_path):
+    """--gpus N without a launcher: torch.distributed.run starts N ranks as a child process whose
+    rank 0 prints the line, and the child's exit code is returned (a stub stands in for bench.py)."""
+    import subprocess
+    import sys
+
+    stub = tmp_path / "stub.py"
+    stub.write_text(
+        "import json, os, sys\n"
+        "if os.environ['RANK'] == '0':\n"
+        "    print(json.dumps({'world': int(os.environ['WORLD_SIZE']), 'argv': sys.argv[1:],\n"
+        "                      'addr': os.environ['MASTER_ADDR']}), flush=True)\n"
+        "sys.exit(int(sys.argv[-1]))\n")
+    b = _bench()
+    cmd = b.spawn_command(3, ["--gpus", "3", "0"], 29555, str(stub))
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=3" in cmd
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    code = ("import importlib.util, sys\n"
+            f"spec = importlib.util.spec_from_file_location('b', {os.path.join(ROOT, 'bench.py')!r})\n"
+            "m = importlib.util.module_from_spec(spec); spec.loader.exec_module(m)\n"
+            f"sys.exit(m._spawn(3, ['--gpus', '3', sys.argv[1]], {str(stub)!r}))\n")
+    r = subprocess.run([sys.executable, "-c", code, "0"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and '"world": 3' in lines[0] and '"addr": "127.0.0.1"' in lines[0]
+    r = subprocess.run([sys.executable, "-c", code, "3"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
