@@ -237,18 +237,6 @@ typedef struct rr_next_frame {
  * between.  NULL: drop a registration. */
 int rr_set_forward_workspace(void* workspace, size_t workspace_bytes);
 
-/* Early-stop phase A as a point a second stream can wait for (the training step runs the loss of
- * the image rows phase A finished while phase B renders the rest, rain_loss.h
- * rl_l1_ssim_forward_backward_part).  rr_set_phase_a_event(1): this thread's renders record an event
- * (a hipEvent_t, rr_phase_a_event) right after the phase-A blend launch — from then on every pixel
- * of a tile whose bit in the frame's open-tile mask is 0 is final — or, on a path without one (a
- * single-phase frame: every bit 0), after all of the render's work.  0: no event (default).
- * rr_frame_open_tiles: the frame's open-tile mask in its image buffer (bit ty * tiles_x + tx, 16 x
- * 16-px tiles; written by phase A's blend, read-only after it). */
-int rr_set_phase_a_event(int on);
-void* rr_phase_a_event(void);
-int rr_frame_open_tiles(const rr_frame* f, const void* image_buffer, const void** bits, int* tiles_x, int* tiles_y);
-
 int rr_backward(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g, const int* radii,
                 const void* geom_buffer, const void* image_buffer, const void* binning_buffer,
                 int num_rendered, const float* dL_dpix, void* workspace, size_t workspace_bytes,
@@ -355,6 +343,8 @@ typedef struct rr_frame_stats {
     int64_t tiles;         /* T */
     int64_t num_pairs;     /* pairs emitted by exact tile culling (before early-stop binning) */
     int64_t num_binned;    /* pairs actually sorted into tile lists (phase A + phase B) */
+    int64_t phase_b_pairs; /* pairs of the Gaussians behind the early-stop cut (0: one phase) */
+    int64_t phase_b_slots; /* phase-B slots the duplicate reserved (<= phase_b_pairs: its region's size) */
 } rr_frame_stats;
 int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* image_buffer, rr_frame_stats* out,
                         void* stream);
@@ -393,54 +383,30 @@ enum rr_stage {
 int rr_profile_enable(int enable);
 int rr_profile_select(unsigned stage_mask);
 
-/* Tuning knob (diagnostics / A-B tests): wave64s per 16x16 tile used by the forward and backward
- * blend kernels (1, 2 or 4; 0 restores the default; backward 3: one wave per tile compiled for 3
- * instead of 4 waves per SIMD).  Results are identical for every choice. */
-int rr_set_blend_config(int fwd_waves, int bwd_waves);
-
-/* Runtime tuning knobs (A/B tests; defaults are the measured best):
- *   "bwd_tile_order" 0/1  backward blend dispatches tiles heaviest first (default 1;
- *                         env RAIN_BWD_TILE_ORDER),
- *   "fwd_tile_order" 0/1  forward blends dispatch tiles longest list first (default 0;
- *                         env RAIN_FWD_TILE_ORDER),
- *   "fwd_waves" / "bwd_waves" as rr_set_blend_config,
- *   "fwd_b_waves"    0/1  phase-B forward blend on 4 waves per tile (default 1),
- *   "sort_min_units" n    radix sorts pick the largest unit with >= n units (default 128; 0 resets),
- *   "sort_min_units_tile" n  the same for the bin sorts (<= 16-bit keys; default 1024),
- *   "sort_max_rounds" r   cap on 64-item rounds per wave in a sort unit, 1..16 (default 16),
+/* Runtime tuning knobs: each forces a product path that larger frames or scenes take onto the
+ * small frames of the tests (every setting gives the same lists, images and gradients).  Kept per
+ * HIP device (the device current at the call); a CPU-only process sets those of device 0.
  *   "pair_scan_direct_blocks" n  pair-count scans of up to n blocks of 2048 Gaussians let every
  *                         block sum the earlier block totals itself (2 launches); larger ones scan
  *                         the totals in one workgroup first (3 launches); default 512, <0 resets,
  *   "wide_bin_keys" 0/1   32-bit bin keys even when the bins fit 16 bits (default 0: only frames
  *                         with more than 65536 bins of 32x32 px use them),
- *   "phase_a_gather" 0..3  phase A (or a single-phase frame): 0 (default) windowed duplicate over
- *                         the split scan's index-ordered list + stable bin sort; the gather path —
- *                         one thread per Gaussian emitting its pairs, per-bin count / scan /
- *                         scatter — over every Gaussian of the frame (1) or over the list (2); the
- *                         windowed duplicate + per-bin count / scan / scatter (3),
- *   "phase_b_gather" -1/0/1/2  phase B: the gather path over the list (1, default) or over every
- *                         Gaussian (2), the windowed path (0), or by the last frame's phase-B size (-1),
- *   "sx_bucket" 0/1       per-bin order by one bucket pass + per-bucket insertion sort (default 1)
- *                         or by 9-bit LSD passes only,
- *   "bounds_in_sort" 0/1  windowed paths: bin runs from the bin sort's last scatter (default 1),
- *   "split_marks" 0/1     windowed duplicate: window starts marked by the split scan when the
- *                         sort unit is 2048 pairs (default 1) or computed by their own launch,
- *   "sx_b_threads" n      phase B's per-bin sort-expand workgroup: 1024 threads (default) or 256,
- *   "sx_lds_cap" n        per-bin runs of more than n pairs (1..2048; default: 2048 in phase A,
- *                         4096 in phase B's 1024-thread sort-expand) depth-sorted through their
- *                         own point_list region instead of LDS,
- *   "forward_clear" 0/1   rr_set_forward_workspace registrations honoured (default 1) or dropped,
- *   "dup_b_reserve" 0/1   phase-B gather: one walk per Gaussian with its pair count reserved as an
- *                         upper bound (default 1) or a counting walk first,
- *   "dup_b_rows" 0/1      phase-B gather, frames up to 128 x 256 tiles: open tiles as per-row
- *                         bit masks, walks over the open bins only (default 1), or the flat mask,
+ *   "phase_b_gather" 0/1  phase B by the gather path when the bins fit one workgroup's count
+ *                         (default 1) or always by the windowed path (frames of > 16384 bins),
+ *   "dup_b_rows" 0/1      phase-B gather on frames up to 128 x 256 tiles: open tiles as per-row bit
+ *                         masks (default 1), or the flat mask of wider frames,
  *   "dup_big_bins" n      phase-B gather: Gaussians spanning more than n bins (default 32) emitted
- *                         by their whole workgroup, 256 bins at a time; 0: each by its own thread,
- *   "cut_in_scan" 0/1     the early-stop depth cut computed by every workgroup of the split scan's
- *                         first launch (default 1) or by its own one-workgroup launch,
+ *                         by their whole workgroup; 0: each by its own thread; <0 resets,
+ *   "sx_bucket" 0/1       per-bin order by one bucket pass + per-bucket insertion sort (default 1)
+ *                         or by the 9-bit LSD passes of crowded buckets only,
+ *   "sx_lds_cap" n        per-bin runs of more than n pairs (default, 0: 2048 in phase A, 4096 in
+ *                         phase B's 1024-thread sort-expand) depth-sorted through their own
+ *                         point_list region instead of LDS,
+ *   "sort_min_units" n / "sort_min_units_tile" n  radix sorts pick the largest unit with >= n units
+ *                         (defaults 128 / 1024 for the bin sorts; 0 resets),
+ *   "sort_max_rounds" r   cap on 64-item rounds per wave in a sort unit: 1, 2, 4, 8 (16 otherwise),
  *   "early_den" n         early-stop split: phase A holds ~1/n of the pairs (default 3).
- * Frames of more than 16384 bins always take the windowed paths.
- * Results are identical for every setting.  Unknown keys return RR_ERR_ARG. */
+ * Unknown keys return RR_ERR_ARG. */
 int rr_set_tuning(const char* key, int value);
 /* Diagnostics: device buffer of >= 8 * 8 * tiles u32 receiving one timing record per forward-blend
  * wave (start / end s_memrealtime, tile, pairs walked, list length, phase) — only builds compiled

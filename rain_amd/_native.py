@@ -84,7 +84,8 @@ RR_MAX_VIEWS = 16
 
 class RRFrameStats(ctypes.Structure):
     _fields_ = [("num_rendered", ctypes.c_int64), ("num_visible", ctypes.c_int64), ("l_eff", ctypes.c_int64),
-                ("tiles", ctypes.c_int64), ("num_pairs", ctypes.c_int64), ("num_binned", ctypes.c_int64)]
+                ("tiles", ctypes.c_int64), ("num_pairs", ctypes.c_int64), ("num_binned", ctypes.c_int64),
+                ("phase_b_pairs", ctypes.c_int64), ("phase_b_slots", ctypes.c_int64)]
 
 
 class RRDebugViews(ctypes.Structure):
@@ -95,13 +96,11 @@ class RRDebugViews(ctypes.Structure):
 # every symbol include/rain_raster.h declares (tests check the .so exports all of them)
 RASTER_SYMBOLS = ["rr_geometry_bytes", "rr_image_bytes", "rr_binning_bytes", "rr_backward_workspace_bytes",
                   "rr_forward_geometry", "rr_forward_render", "rr_forward_render_aux", "rr_forward", "rr_backward", "rr_mark_visible", "rr_last_error",
-                  "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_blend_config",
-                  "rr_set_binning_config", "rr_set_tuning", "rr_debug_set_fwd_trace", "rr_profile_enable",
+                  "rr_version", "rr_read_frame_stats", "rr_debug_get_views", "rr_set_binning_config", "rr_set_tuning", "rr_debug_set_fwd_trace", "rr_profile_enable",
                   "rr_profile_select", "rr_profile_collect", "rr_stage_name", "rr_host_wait_stats", "rr_geometry_layout",
                   "rr_preprocess_rows", "rr_preprocess_rows_views", "rr_unpack_rows", "rr_forward_from_geometry",
                   "rr_forward_render_geometry",
-                  "rr_backward_records", "rr_gauss_backward_views", "rr_set_forward_workspace",
-                  "rr_set_phase_a_event", "rr_phase_a_event", "rr_frame_open_tiles"]
+                  "rr_backward_records", "rr_gauss_backward_views", "rr_set_forward_workspace"]
 
 _raster = None
 _knn = None
@@ -148,21 +147,12 @@ def raster():
         L.rr_read_frame_stats.argtypes = [fp, vp, vp, ctypes.POINTER(RRFrameStats), vp]
         L.rr_debug_get_views.restype = ci
         L.rr_debug_get_views.argtypes = [fp, vp, vp, vp, ci, ctypes.POINTER(RRDebugViews)]
-        L.rr_set_blend_config.restype = ci
-        L.rr_set_blend_config.argtypes = [ci, ci]
         L.rr_host_wait_stats.restype = ci
         L.rr_host_wait_stats.argtypes = [ci, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         L.rr_profile_enable.restype = ci
         L.rr_profile_enable.argtypes = [ci]
         L.rr_set_forward_workspace.restype = ci
         L.rr_set_forward_workspace.argtypes = [vp, sz]
-        L.rr_set_phase_a_event.restype = ci
-        L.rr_set_phase_a_event.argtypes = [ci]
-        L.rr_phase_a_event.restype = vp
-        L.rr_phase_a_event.argtypes = []
-        L.rr_frame_open_tiles.restype = ci
-        L.rr_frame_open_tiles.argtypes = [ctypes.POINTER(RRFrame), vp, ctypes.POINTER(vp), ctypes.POINTER(ci),
-                                          ctypes.POINTER(ci)]
         L.rr_set_tuning.restype = ci
         L.rr_set_tuning.argtypes = [ctypes.c_char_p, ci]
         L.rr_debug_set_fwd_trace.restype = ci
@@ -201,7 +191,7 @@ def raster():
 
 LOSS_LIB = os.environ.get("RAIN_LOSS_LIB") or os.path.join(LIB_DIR, "librain_loss.so")
 LOSS_SYMBOLS = ["rl_workspace_bytes", "rl_l1_ssim_forward", "rl_l1_ssim_backward", "rl_l1_ssim_forward_backward",
-                "rl_l1_ssim_forward_backward_part", "rl_set_fused_band", "rl_last_error"]
+                "rl_last_error"]
 _loss = None
 
 
@@ -212,8 +202,6 @@ def loss_lib():
         vp, ci, cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         L.rl_workspace_bytes.restype = ctypes.c_size_t
         L.rl_workspace_bytes.argtypes = [ci, ci, ci]
-        L.rl_set_fused_band.restype = ci
-        L.rl_set_fused_band.argtypes = [ci]
         L.rl_l1_ssim_forward.restype = ci
         L.rl_l1_ssim_forward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, ctypes.c_size_t, vp, vp, vp]
         L.rl_l1_ssim_backward.restype = ci
@@ -221,9 +209,6 @@ def loss_lib():
         L.rl_l1_ssim_forward_backward.restype = ci
         L.rl_l1_ssim_forward_backward.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp, ctypes.c_size_t, vp,
                                                   vp, vp, vp, vp]
-        L.rl_l1_ssim_forward_backward_part.restype = ci
-        L.rl_l1_ssim_forward_backward_part.argtypes = [vp, vp, ci, ci, ci, cf, ctypes.POINTER(cf), vp,
-                                                       ctypes.c_size_t, vp, vp, vp, vp, vp, ci, ci, ci, vp, vp]
         L.rl_last_error.restype = ctypes.c_char_p
         _loss = L
     return _loss

@@ -61,40 +61,6 @@ struct Win {
     float w[11];
 };
 
-// The loss split around the rasterizer's early-stop phase B (rl_l1_ssim_forward_backward_part):
-// part 1 takes the bands whose rows phase A already finished, part 2 the others (part 0: all).
-// bits: rain_raster's open-tile bitmask of the frame (bit ty * tgx + tx, 16 x 16-px tiles).
-struct Split {
-    const uint32_t* bits;
-    int tgx, tgy, part;
-};
-constexpr int kTilePx = 16;  // the rasterizer's tile (rr_common.hpp TILE_X / TILE_Y)
-// Image rows [r0, r1) (clipped to the image) hold a tile phase A left open.  Wave-uniform.
-__device__ __forceinline__ bool rows_open(const Split& sp, int H, int r0, int r1) {
-    r0 = max(r0, 0);
-    r1 = min(r1, H);
-    if (r0 >= r1) return false;
-    const int ty0 = r0 / kTilePx, ty1 = min((r1 - 1) / kTilePx, sp.tgy - 1);
-    const uint32_t lo = (uint32_t)(ty0 * sp.tgx), hi = (uint32_t)((ty1 + 1) * sp.tgx);  // bits [lo, hi)
-    bool any = false;
-    for (uint32_t wd = (lo >> 5) + threadIdx.x; wd <= (hi - 1) >> 5; wd += 64) {
-        uint32_t m = sp.bits[wd];
-        if (wd == lo >> 5) m &= ~0u << (lo & 31);
-        if (wd == (hi - 1) >> 5) m &= ~0u >> (31 - ((hi - 1) & 31));
-        any = any || m != 0u;
-    }
-    return __ballot(any) != 0ull;
-}
-// forward band y (output rows [y TH_FWD, (y + 1) TH_FWD)) in part 1: its input rows are final
-__device__ __forceinline__ bool fwd_band_early(const Split& sp, int H, int y, int th_fwd) {
-    return !rows_open(sp, H, y * th_fwd - 5, (y + 1) * th_fwd + 5);
-}
-// backward band y in part 1: every forward band whose derivative rows it reads is in part 1
-__device__ __forceinline__ bool bwd_band_early(const Split& sp, int H, int y, int th_bwd, int th_fwd) {
-    const int fmin = max(0, y * th_bwd - 5) / th_fwd, fmax = min(H - 1, (y + 1) * th_bwd + 4) / th_fwd;
-    return !rows_open(sp, H, fmin * th_fwd - 5, (fmax + 1) * th_fwd + 5);
-}
-
 // 1/x: v_rcp_f32 (1 ulp) plus one Newton step
 __device__ __forceinline__ float rcp_nr(float x) {
     const float r = __builtin_amdgcn_rcpf(x);
@@ -206,8 +172,7 @@ template <int TH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_ssim_fwd(const float* __restrict__ img, const float* __restrict__ gt, int H,
                                                  int W, float lambda, float inv_n, Win win, float* __restrict__ g1,
                                                  float* __restrict__ g11, float* __restrict__ g12,
-                                                 float2* __restrict__ partial, Split split) {
-    if (split.part && (split.part == 1) != fwd_band_early(split, H, blockIdx.y, TH)) return;  // block-uniform
+                                                 float2* __restrict__ partial) {
     __shared__ float sp[2][NR][PW];
     const int c = blockIdx.z;
     const int x0 = blockIdx.x * TW - R, y0 = blockIdx.y * TH - R;
@@ -390,13 +355,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                                  const float* __restrict__ g1, const float* __restrict__ g11,
                                                  const float* __restrict__ g12, const float* __restrict__ grad_loss,
                                                  float* __restrict__ dimg, const float2* __restrict__ partial,
-                                                 int nb, float* __restrict__ loss, float* __restrict__ parts,
-                                                 Split split) {
+                                                 int nb, float* __restrict__ loss, float* __restrict__ parts) {
     if (loss && blockIdx.x == gridDim.x - 1) {  // the extra column (block-uniform): the forward's finalize
         if (blockIdx.y == 0 && blockIdx.z == 0) loss_finalize_one_wave(partial, nb, lambda, inv_n, loss, parts);
         return;
     }
-    if (split.part && (split.part == 1) != bwd_band_early(split, H, blockIdx.y, TH, TH_FWD)) return;
     __shared__ float sg[3][NR][PW];
     const int c = blockIdx.z;
     const int x0 = blockIdx.x * TW - R, y0 = blockIdx.y * TH - R;
@@ -460,183 +423,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
 }
 
-// Forward and backward in ONE band walk (rl_l1_ssim_forward_backward's default, rl_set_fused_band):
-// the derivative maps never leave the chip.  Block = one wave64 and one channel; lane l owns G
-// column ox0 - R + l (the SSIM map and its three derivative maps G1, G11, G12 are formed for 64
-// columns: the 54 output columns [ox0, ox0 + 54) of the block and a 5-column halo each side) and,
-// for l < 54, output column ox0 + l.  The band's TH + 4R input rows stream through the LDS ring as
-// in k_ssim_fwd; once the moment ring is full every input row completes one G row (the forward's
-// arithmetic), which goes through a 2-row LDS ring for the backward's horizontal 11-tap pass into
-// an 11-row register ring; once that is full every G row completes one output row of dimg (the
-// backward's arithmetic).  G outside the image is 0 (the two-pass backward reads the stored maps
-// with zero padding), so dimg equals the two-pass result up to FMA contraction; the loss sums S and
-// |x - y| over the block's own output pixels (a different block partition than k_ssim_fwd's, so
-// the loss agrees with rl_l1_ssim_forward to float rounding, not bitwise).  Per output pixel: the
-// same VALU work as the two passes, one launch and ~75 MB/frame of HBM traffic instead of ~270.
-constexpr int TWF = TW - 2 * R;  // 54 output columns per fused block
-#ifndef RL_LA_FUSED
-#define RL_LA_FUSED 2
-#endif
-#ifndef RL_WPE_FUSED
-#define RL_WPE_FUSED 3
-#endif
-template <int TH>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RL_WPE_FUSED))) void k_ssim_fused(
-    const float* __restrict__ img, const float* __restrict__ gt, int H, int W, float lambda, float inv_n, Win win,
-    const float* __restrict__ grad_loss, float* __restrict__ dimg, float2* __restrict__ partial) {
-    __shared__ float sp[2][NR][PW];   // input rows (x, y)
-    __shared__ float sgr[3][NR][PW];  // G rows (G1, G11, G12): 64 columns + 10 zero columns
-    __shared__ float sbr[3][11][64];  // the horizontally blurred G rows: each lane's own column
-                                      // (an LDS ring instead of 33 registers: 3 waves/SIMD, no spill)
-    const int c = blockIdx.z;
-    const int ox0 = blockIdx.x * TWF, oy0 = blockIdx.y * TH;
-    const int x0 = ox0 - 2 * R, y0 = oy0 - 2 * R;  // input patch origin
-    const size_t plane = (size_t)H * W;
-    const int lane = threadIdx.x;
-    constexpr int PH = TH + 4 * R;  // input rows per band
-    constexpr int LA = RL_LA_FUSED;
-    const Rsrc rs[2] = {plane_rsrc(img + c * plane, 4 * (int)plane), plane_rsrc(gt + c * plane, 4 * (int)plane)};
-    const Rsrc ds = plane_rsrc(dimg + c * plane, 4 * (int)plane);
-    const Band bd(x0, y0, H, W, lane);
-    PatchRow<2> q[LA + 1];
-    if (lane < PW - 64)
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-#pragma unroll
-            for (int s = 0; s < NR; s++) sgr[k][s][64 + lane] = 0.f;
-    prime<2, LA, PH>(rs, bd, sp, q, lane);
-    const int gxc = ox0 - R + lane;  // this lane's G column
-    const bool gcol_in = gxc >= 0 && gxc < W;
-    const bool own_col = lane >= R && lane < R + TWF && gxc < W;  // an output column of this block
-    const int ocol = ox0 + lane;
-    const int vo_out = (lane < TWF && ocol < W) ? 4 * ocol : kOOB;
-    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
-    const float k = -lambda * inv_n;
-    const float gl = grad_loss[0];
-    const float l1k = (1.f - lambda) * inv_n;
-    float r0[11], r1[11], r2[11], r3[11], r4[11];  // moment rows (forward)
-    float s_val = 0.f, l1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < PH; r++) {
-        queue_issue<2, LA, PH>(rs, bd, q, r);
-        const int slot = r % NR;
-        const lds_ptr px = row_base(&sp[0][slot][lane]);
-        const lds_ptr py = px + NR * PW;
-        float a = 0.f, b = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
-#pragma unroll
-        for (int j = 0; j < 11; j++) {
-            const float xv = px[j], yv = py[j], wj = win.w[j];
-            a += wj * xv;
-            b += wj * yv;
-            aa += wj * (xv * xv);
-            bb += wj * (yv * yv);
-            ab += wj * (xv * yv);
-        }
-        pin(a);
-        pin(b);
-        pin(aa);
-        pin(bb);
-        pin(ab);
-        // L1 at this row's centre pixel when it is one of the block's output pixels
-        if (r >= 2 * R && r < TH + 2 * R) l1 += (own_col && y0 + r < H) ? fabsf(px[R] - py[R]) : 0.f;
-        queue_retire<2, LA, PH>(sp, q, r, lane);
-        r0[r % 11] = a;
-        r1[r % 11] = b;
-        r2[r % 11] = aa;
-        r3[r % 11] = bb;
-        r4[r % 11] = ab;
-        if (r >= 2 * R) {
-            const int g = r - 2 * R;       // G row of the band
-            const int gy = oy0 - R + g;    // its image row
-            float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
-#pragma unroll
-            for (int i = 0; i < 11; i++) {
-                const int qs = (g + i) % 11;
-                const float wi = win.w[i];
-                m1 += wi * r0[qs];
-                m2 += wi * r1[qs];
-                e11 += wi * r2[qs];
-                e22 += wi * r3[qs];
-                e12 += wi * r4[qs];
-            }
-            const float m1s = m1 * m1, m2s = m2 * m2, m12 = m1 * m2;
-            const float s11 = e11 - m1s, s22 = e22 - m2s, s12 = e12 - m12;
-            const float A = 2.f * m12 + C1, B = 2.f * s12 + C2;
-            const float Cd = m1s + m2s + C1, Dd = s11 + s22 + C2;
-            const float inv_cd = rcp_nr(Cd), inv_dd = rcp_nr(Dd);
-            const float cdd = inv_cd * inv_dd;
-            const float S = (A * B) * cdd;
-            if (g >= R && g < TH + R) s_val += (own_col && gy < H) ? S : 0.f;
-            const bool gin = gcol_in && gy >= 0 && gy < H;
-            const int gs = g % NR;
-            sgr[0][gs][lane] = gin ? k * (2.f * m2 * (B - A) * cdd - 2.f * m1 * S * (inv_cd - inv_dd)) : 0.f;
-            sgr[1][gs][lane] = gin ? k * (-S * inv_dd) : 0.f;
-            sgr[2][gs][lane] = gin ? k * (2.f * A * cdd) : 0.f;
-            __syncthreads();  // the G row in LDS before the horizontal pass reads its neighbours
-            const lds_ptr pg = row_base(&sgr[0][gs][lane]);
-            float h1 = 0.f, h11 = 0.f, h12 = 0.f;
-#pragma unroll
-            for (int j = 0; j < 11; j++) {
-                const float wj = win.w[j];
-                h1 += wj * pg[j];
-                h11 += wj * pg[NR * PW + j];
-                h12 += wj * pg[2 * NR * PW + j];
-            }
-            pin(h1);
-            pin(h11);
-            pin(h12);
-            sbr[0][g % 11][lane] = h1;
-            sbr[1][g % 11][lane] = h11;
-            sbr[2][g % 11][lane] = h12;
-            if (g >= 2 * R) {
-                const int o = g - 2 * R;  // output row of the block
-                const int gyo = oy0 + o;
-                float v1 = 0.f, v11 = 0.f, v12 = 0.f;
-#pragma unroll
-                for (int i = 0; i < 11; i++) {
-                    const int qs = (o + i) % 11;
-                    const float wi = win.w[i];
-                    v1 += wi * sbr[0][qs][lane];
-                    v11 += wi * sbr[1][qs][lane];
-                    v12 += wi * sbr[2][qs][lane];
-                }
-                const int so = gyo < H ? gyo * 4 * W : kOOB;
-                const float xv = load_f32(rs[0], vo_out, so);
-                const float yv = load_f32(rs[1], vo_out, so);
-                const float dd = xv - yv;
-                const float sgn = dd > 0.f ? 1.f : (dd < 0.f ? -1.f : 0.f);
-                store_f32(gl * (v1 + 2.f * xv * v11 + yv * v12 + l1k * sgn), ds, vo_out, so);
-            }
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s_val += __shfl_xor(s_val, o);
-        l1 += __shfl_xor(l1, o);
-    }
-    if (lane == 0) {
-        const int bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-        partial[bid] = make_float2(s_val, l1);
-    }
-}
-
 int nblocks(int C, int H, int W) { return ((W + TW - 1) / TW) * ((H + TH_FWD - 1) / TH_FWD) * C; }
 
 // The two-pass forward + backward (the backward grid's extra column finalizes the loss, bitwise
-// rl_l1_ssim_forward's, when `loss` is given), over the bands of `sp`'s part (part 0: all).
+// rl_l1_ssim_forward's, when `loss` is given).
 void launch_fwd_bwd(const float* img, const float* gt, int C, int H, int W, float lambda, const Win& win, float* g1,
-                    float2* partial, float* loss, float* parts, const float* grad_loss, float* dimg, const Split& sp,
-                    hipStream_t st) {
+                    float2* partial, float* loss, float* parts, const float* grad_loss, float* dimg, hipStream_t st) {
     const size_t n = (size_t)C * H * W;
     const float inv_n = (float)(1.0 / (double)n);
     const dim3 gf((W + TW - 1) / TW, (H + TH_FWD - 1) / TH_FWD, C);
-    k_ssim_fwd<TH_FWD><<<gf, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, partial, sp);
+    k_ssim_fwd<TH_FWD><<<gf, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, partial);
     const dim3 gb((W + TW - 1) / TW + (loss ? 1 : 0), (H + TH_BWD - 1) / TH_BWD, C);
     k_ssim_bwd<TH_BWD><<<gb, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg,
-                                          partial, nblocks(C, H, W), loss, parts, sp);
+                                          partial, nblocks(C, H, W), loss, parts);
 }
-int g_fused_band = 0;  // rows per block of the one-walk form; 0: the two passes
-int nblocks_fused(int C, int H, int W, int th) { return ((W + TWF - 1) / TWF) * ((H + th - 1) / th) * C; }
 
 }  // namespace
 
@@ -645,17 +445,7 @@ extern "C" {
 const char* rl_last_error(void) { return g_err.c_str(); }
 
 size_t rl_workspace_bytes(int C, int H, int W) {
-    const int nb = std::max(nblocks(C, H, W), nblocks_fused(C, H, W, 16));
-    return (size_t)3 * C * H * W * sizeof(float) + (size_t)nb * sizeof(float2) + 256;
-}
-
-int rl_set_fused_band(int rows) {
-    if (rows != 0 && rows != 16 && rows != 24 && rows != 32 && rows != 48 && rows != 64) {
-        g_err = "rl_set_fused_band: rows must be 0, 16, 24, 32, 48 or 64";
-        return 1;
-    }
-    g_fused_band = rows;
-    return 0;
+    return (size_t)3 * C * H * W * sizeof(float) + (size_t)nblocks(C, H, W) * sizeof(float2) + 256;
 }
 
 int rl_l1_ssim_forward(const float* img, const float* gt, int C, int H, int W, float lambda, const float* window,
@@ -682,7 +472,7 @@ int rl_l1_ssim_forward(const float* img, const float* gt, int C, int H, int W, f
     const float inv_n = (float)(1.0 / (double)n);
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((W + TW - 1) / TW, (H + TH_FWD - 1) / TH_FWD, C);
-    k_ssim_fwd<TH_FWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g11, g12, partial, Split{});
+    k_ssim_fwd<TH_FWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g11, g12, partial);
     k_loss_finalize<<<1, kFinT, 0, st>>>(partial, nblocks(C, H, W), lambda, inv_n, loss, parts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -710,7 +500,7 @@ int rl_l1_ssim_backward(const float* img, const float* gt, int C, int H, int W, 
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((W + TW - 1) / TW, (H + TH_BWD - 1) / TH_BWD, C);
     k_ssim_bwd<TH_BWD><<<grid, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, g1, g1 + n, g1 + 2 * n, grad_loss, dimg,
-                                            nullptr, 0, nullptr, nullptr, Split{});
+                                            nullptr, 0, nullptr, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("rl_l1_ssim_backward: ") + hipGetErrorString(e);
@@ -730,8 +520,7 @@ int rl_l1_ssim_forward_backward(const float* img, const float* gt, int C, int H,
         g_err = "rl_l1_ssim_forward_backward: image plane larger than 2^30 bytes";
         return 1;
     }
-    if (workspace_bytes < rl_workspace_bytes(C, H, W) || nblocks(C, H, W) > NB_MAX ||
-        nblocks_fused(C, H, W, 16) > NB_MAX) {
+    if (workspace_bytes < rl_workspace_bytes(C, H, W) || nblocks(C, H, W) > NB_MAX) {
         g_err = "rl_l1_ssim_forward_backward: workspace too small";
         return 3;
     }
@@ -742,74 +531,10 @@ int rl_l1_ssim_forward_backward(const float* img, const float* gt, int C, int H,
     float2* partial = reinterpret_cast<float2*>(g1 + 3 * n);
     const float inv_n = (float)(1.0 / (double)n);
     hipStream_t st = (hipStream_t)stream;
-    if (g_fused_band) {  // one band walk + the loss finalize
-        const int th = g_fused_band;
-        const dim3 gu((W + TWF - 1) / TWF, (H + th - 1) / th, C);
-        switch (th) {
-            case 16: k_ssim_fused<16><<<gu, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, grad_loss, dimg, partial); break;
-            case 24: k_ssim_fused<24><<<gu, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, grad_loss, dimg, partial); break;
-            case 48: k_ssim_fused<48><<<gu, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, grad_loss, dimg, partial); break;
-            case 64: k_ssim_fused<64><<<gu, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, grad_loss, dimg, partial); break;
-            default: k_ssim_fused<32><<<gu, 64, 0, st>>>(img, gt, H, W, lambda, inv_n, win, grad_loss, dimg, partial); break;
-        }
-        k_loss_finalize<<<1, kFinT, 0, st>>>(partial, nblocks_fused(C, H, W, th), lambda, inv_n, loss, parts);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) {
-            g_err = std::string("rl_l1_ssim_forward_backward: ") + hipGetErrorString(e);
-            return 2;
-        }
-        return 0;
-    }
-    launch_fwd_bwd(img, gt, C, H, W, lambda, win, g1, partial, loss, parts, grad_loss, dimg, Split{}, st);
+    launch_fwd_bwd(img, gt, C, H, W, lambda, win, g1, partial, loss, parts, grad_loss, dimg, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = std::string("rl_l1_ssim_forward_backward: ") + hipGetErrorString(e);
-        return 2;
-    }
-    return 0;
-}
-
-int rl_l1_ssim_forward_backward_part(const float* img, const float* gt, int C, int H, int W, float lambda,
-                                     const float* window, void* workspace, size_t workspace_bytes, float* loss,
-                                     float* parts, const float* grad_loss, float* dimg, const void* open_bits,
-                                     int tiles_x, int tiles_y, int part, void* wait_event, void* stream) {
-    if (!img || !gt || !window || !workspace || !grad_loss || !dimg || C <= 0 || H <= 0 || W <= 0 || !open_bits ||
-        (part != 1 && part != 2) || (part == 2 && !loss) || tiles_x * kTilePx < W || tiles_y * kTilePx < H ||
-        (tiles_x - 1) * kTilePx >= W || (tiles_y - 1) * kTilePx >= H) {
-        g_err = "rl_l1_ssim_forward_backward_part: bad argument";
-        return 1;
-    }
-    if (g_fused_band) {
-        g_err = "rl_l1_ssim_forward_backward_part: the one-band-walk form (rl_set_fused_band) has no split";
-        return 1;
-    }
-    if ((size_t)H * W * 4 >= (size_t)kOOB) {
-        g_err = "rl_l1_ssim_forward_backward_part: image plane larger than 2^30 bytes";
-        return 1;
-    }
-    if (workspace_bytes < rl_workspace_bytes(C, H, W) || nblocks(C, H, W) > NB_MAX) {
-        g_err = "rl_l1_ssim_forward_backward_part: workspace too small";
-        return 3;
-    }
-    Win win;
-    for (int i = 0; i < 11; i++) win.w[i] = window[i];
-    const size_t n = (size_t)C * H * W;
-    float* g1 = static_cast<float*>(workspace);
-    float2* partial = reinterpret_cast<float2*>(g1 + 3 * n);
-    hipStream_t st = (hipStream_t)stream;
-    if (wait_event) {
-        const hipError_t w = hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0);
-        if (w != hipSuccess) {
-            g_err = std::string("rl_l1_ssim_forward_backward_part: ") + hipGetErrorString(w);
-            return 2;
-        }
-    }
-    const Split sp{static_cast<const uint32_t*>(open_bits), tiles_x, tiles_y, part};
-    launch_fwd_bwd(img, gt, C, H, W, lambda, win, g1, partial, part == 2 ? loss : nullptr, parts, grad_loss, dimg, sp,
-                   st);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        g_err = std::string("rl_l1_ssim_forward_backward_part: ") + hipGetErrorString(e);
         return 2;
     }
     return 0;

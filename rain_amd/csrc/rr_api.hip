@@ -7,6 +7,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -17,10 +19,17 @@
 using namespace rr;
 
 namespace rr {
-// rr_set_tuning "wide_bin_keys": 32-bit bin keys even when the bins fit 16 bits (the layout of
-// frames with more than 65536 bins, e.g. above 8K x 8K), so tests reach that path at small sizes
-bool g_wide_bin_keys = false;
-void set_wide_bin_keys(bool on) { g_wide_bin_keys = on; }
+// The tuning record of the current device (rr_kernels.hpp Tuning): a device index outside the
+// table, or no device at all (a CPU-only process setting knobs), uses entry 0.
+Tuning& tuning() {
+    static Tuning per_device[kMaxDevices];
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDevices) {
+        (void)hipGetLastError();
+        d = 0;
+    }
+    return per_device[d];
+}
 }  // namespace rr
 
 namespace {
@@ -110,7 +119,8 @@ struct Img {
     uint32_t* n_contrib;
     uint2* ranges;      // phase-A (or single-phase) lists; ranges_b and counters follow it
     uint2* ranges_b;    // phase-B lists of early-stop binning (all {0,0} otherwise)
-    uint32_t* counters; // [0] phase-B pairs, [1] backward tile order done, [2] phase-A pairs (gather path)
+    uint32_t* counters; // [0] phase-B pairs (gather path: slots reserved), [1] backward tile order done,
+                        // [2] phase B took the gather path, [3] phase-B pairs its bin runs hold
     size_t zero_bytes;  // ranges .. bin_cnt_a: cleared before every render
     uint32_t* tile_max;
     uint8_t* open;      // [T] tile still open after phase A
@@ -150,42 +160,30 @@ Img carve_img(void* buf, int W, int H) {
     return m;
 }
 
-// Early-stop binning split (rr_bin.hip k_early_cut): phase A bins the pairs of the Gaussians nearer
+// Early-stop binning split (rr_bin.hip depth_cut): phase A bins the pairs of the Gaussians nearer
 // than a per-frame depth cut holding ~1/den of the pairs, for every tile; phase B the rest, only for
 // the tiles phase A left open (rr_kernels.hpp BlendPhase).  den = 3: on the bench frames (1M
 // Gaussians, 1080p) most tiles saturate inside the first third (tools/saturation_stats.py; with the
 // depth-rank split of rounds 1-3, tools/step_ab.py --split 2,3,4: 1.509 / 1.491 / 1.525 ms per
-// step).  Frames below kEarlyMin pairs are binned in one phase.  rr_set_binning_config changes both
-// (tests force the split onto small frames).
-constexpr uint32_t kEarlyDen = 3, kEarlyMin = 1u << 16;
-uint32_t g_early_den = kEarlyDen, g_early_min = kEarlyMin;
-
-// Binning paths (count_pairs below).  g_a_gather: phase A by the windowed duplicate + stable bin sort
-// (0, default), by the windowed duplicate + per-bin count / scatter and the per-bin sort on
-// unordered runs (3), by the gather path over the split scan's phase-A list (2) or over every
-// Gaussian of the frame (1, no split scan then if phase B does without it too).  g_b_gather: phase B by the
-// gather path over the phase-B list (1, default) or over every Gaussian (2), by the windowed path (0),
-// or by the last frame's phase-B size (-1).
-int g_a_gather = 0;
-int g_b_gather = 1;
+// step).  Frames below Tuning::early_min pairs are binned in one phase.  rr_set_binning_config
+// changes both (tests force the split onto small frames).
+//
+// Binning paths: phase A (or the single phase) by the windowed duplicate over the split scan's
+// index-ordered list + the stable bin sort; phase B by the gather path (rr_forward.hip k_dup_gather,
+// per-bin count / scatter: few pairs) when the grid's bins fit one workgroup's count (rr_bin.hip
+// kBinScanMax), else by the windowed path (Tuning::b_gather off forces it onto small frames).
 constexpr int kGatherMaxBins = 16384;  // rr_bin.hip kBinScanMax
-bool gather_bins_fit(int W, int H) { return bins_x(grid_x(W)) * bins_y(grid_y(H)) <= kGatherMaxBins; }
-// Both phases always by the gather paths: the compact binning layout (carve_bin).
-bool a_gather_dup() { return g_a_gather == 1 || g_a_gather == 2; }  // phase A's duplicate by the gather path
-bool compact_binning(int W, int H) {
-    return a_gather_dup() && (g_b_gather == 1 || g_b_gather == 2) && gather_bins_fit(W, H);
+bool b_gather(int W, int H) {
+    return tuning().b_gather && bins_x(grid_x(W)) * bins_y(grid_y(H)) <= kGatherMaxBins;
 }
 
 struct Bin {
     // FIRST, so the backward finds it without knowing the pair count: the per-tile lists
     // k_sortexpand writes, 4 slots per (bin, Gaussian) pair.  The host knows only the frame's
-    // total L (the phases' split LA + LB = L stays on the device).  Compact layout (both phases
-    // binned by the gather paths): phase A's lists at [0, 4 LA), phase B's right after them (its
-    // base read on the device), and one region [0, L) of the pair arrays used by phase A and then
-    // again by phase B — 26 B per pair (point_list 16, keys 2, values 4 + 4 sorted).
-    // Otherwise every pair array has a phase-A region [0, L) and a phase-B region [L, 2L)
-    // (point_list: [0, 4L) and [4L, 8L)), plus the bin sort's arrays — 56 B per pair with 16-bit
-    // bin keys (point_list 32, keys 4 + 4 sorted, values 8 + 8 sorted) + ~0.5 B of sort counts.
+    // total L (the phases' split LA + LB = L stays on the device).  Every pair array has a phase-A
+    // region [0, L) and a phase-B region [L, 2L) (point_list: [0, 4L) and [4L, 8L)), plus the bin
+    // sort's arrays — 56 B per pair with 16-bit bin keys (point_list 32, keys 4 + 4 sorted, values
+    // 8 + 8 sorted) + ~0.5 B of sort counts.
     // Bins of more than 2048 pairs are depth-sorted inside their own point_list region (rr_bin.hip
     // sortexpand_run): no scratch arrays.
     uint32_t* point_list;
@@ -198,7 +196,6 @@ struct Bin {
     void* temp;            // bin-sort scratch, shared by the two phases
     size_t temp_bytes;
     bool wide;  // 32-bit bin keys (more than 65536 bins)
-    bool compact;  // compact_binning(): see point_list
     int bits;
     uint32_t L;  // (bin, Gaussian) pairs of both phases
     size_t total;
@@ -210,7 +207,7 @@ struct PhaseHints {
 };
 PhaseHints phase_hints(uint32_t L, bool early) {
     const size_t n = std::max<size_t>(L, 1);
-    const size_t a = std::max<size_t>(n / std::max<uint32_t>(g_early_den, 1u), 1);
+    const size_t a = std::max<size_t>(n / std::max<uint32_t>(tuning().early_den, 1u), 1);
     return early ? PhaseHints{a, std::max<size_t>(n - a, 1)} : PhaseHints{n, n};
 }
 template <typename K>
@@ -223,26 +220,21 @@ Bin carve_bin(void* buf, int L, int W, int H) {
     Carver c(buf);
     Bin b;
     const int NB = bins_x(grid_x(W)) * bins_y(grid_y(H));
-    b.wide = NB > 65536 || g_wide_bin_keys;
+    b.wide = NB > 65536 || tuning().wide_bin_keys;
     b.bits = std::max(1, (int)higher_msb((uint32_t)NB));  // >= 1: the duplicate windows are sort units
     b.L = (uint32_t)std::max(L, 0);
-    b.compact = compact_binning(W, H);
-    const size_t n = (size_t)std::max(L, 1);
-    const size_t np = b.compact ? n : 2 * n;  // entries of each pair array
+    const size_t np = 2 * (size_t)std::max(L, 1);  // entries of each pair array: both phases' regions
     b.point_list = c.take<uint32_t>(4 * np + kPointListPad);
     if (b.wide) {
         b.keys = c.take<uint32_t>(np);
-        b.keys_sorted = b.compact ? nullptr : c.take<uint32_t>(np);
+        b.keys_sorted = c.take<uint32_t>(np);
     } else {
         b.keys = c.take<uint16_t>(np);
-        b.keys_sorted = b.compact ? nullptr : c.take<uint16_t>(np);
+        b.keys_sorted = c.take<uint16_t>(np);
     }
     b.vals = c.take<uint32_t>(np);
     b.vals_sorted = c.take<uint32_t>(np);
-    b.first = b.unit_len = nullptr;
-    b.temp = nullptr;
-    b.temp_bytes = 0;
-    if (!b.compact) {
+    {
         const PhaseHints h = phase_hints(b.L, true);
         auto units = [&](size_t hint) {
             return b.wide ? tile_plan<uint32_t>(nullptr, b.L, b.bits, hint).units
@@ -341,7 +333,7 @@ int check(const rr_frame* f, hipStream_t st, const char* what) {
 // wait has outlasted any frame the stream is queried: a launch / kernel error is reported, and a
 // stream that went idle without the sequence number becoming visible falls back to the plain copy.
 struct Mailbox {
-    uint32_t* host = nullptr;  // [L, rect, seq, wide, -, phase-B pairs of the last frame], coherent pinned
+    uint32_t* host = nullptr;  // [L, rect, seq, wide], coherent pinned
     uint32_t* dev = nullptr;   // device alias of host
     uint32_t seq = 0;
     bool failed = false;       // allocation failed: always use the copy
@@ -474,60 +466,32 @@ PreArgs pre_args(const rr_frame* f, const rr_camera* cam, const rr_gaussians* g)
     return a;
 }
 
-// Binning paths (rr_set_tuning): phase A (or the single phase) by the gather path — one thread per
-// Gaussian emitting its pairs densely (rr_forward.hip k_dup_gather), per-bin count / scan / scatter
-// and the per-bin sort restoring (depth, index) order (rr_bin.hip launch_sortexpand_small) — or by
-// the windowed duplicate over the split scan's index-ordered lists + the stable bin sort
-// ("phase_a_gather" 0).  Phase B likewise ("phase_b_gather": 1 (default) the gather path, 0 the
-// windowed one, -1 the gather path when the last frame's phase B held at most kBGatherMax pairs:
-// the phase-B sort-expand leaves its count in mailbox word 5).  The gather paths need no split scan;
-// grids of more bins than one workgroup's count / scan holds (rr_bin.hip kBinScanMax) always take
-// the windowed path.
-constexpr uint32_t kBGatherMax = 1u << 16;
-bool phase_b_gather() {
-    if (g_b_gather >= 0) return g_b_gather != 0;
-    const Mailbox& mb = g_mailbox;
-    return mb.host && !mb.failed && __atomic_load_n(mb.host + 5, __ATOMIC_RELAXED) <= kBGatherMax;
-}
+// The image buffer whose per-frame block the last pair count of this thread cleared, not yet
+// rendered into: a render consumes it, so that a second render after one pair count (whose gather
+// counters would start where the first one's ended, past their regions) fails instead.
+thread_local const void* g_counted_img = nullptr;
 
-// The depth cut inside the split scan's first launch (default) or by k_early_cut before it
-// (rr_set_tuning "cut_in_scan" 0; always without a split scan)
-int g_cut_in_scan = 1;
-
-// Depth cut (+ the split pair-count scan when a windowed path needs its lists) -> the one
-// device->host read of the forward, over a geometry buffer whose per-Gaussian arrays (splats, tiles,
-// depth keys, block sums) are filled.  No depth sort: the bins' runs are put in depth order by
-// k_sortexpand (rr_bin.hip).  The same launch as the depth-cut samples clears the image buffer's
-// per-frame block (im: the buffer the frame is then rendered into).
+// Depth cut + the split pair-count scan -> the one device->host read of the forward, over a
+// geometry buffer whose per-Gaussian arrays (splats, tiles, depth keys, block sums) are filled.  No
+// depth sort: the bins' runs are put in depth order by k_sortexpand (rr_bin.hip).  The scan's first
+// launch computes the cut and clears the image buffer's per-frame block (im: the buffer the frame
+// is then rendered into).
 int count_pairs(const rr_frame* f, const Geom& gm, const Img& im, int P, hipStream_t st, int* num_rendered,
                 int* num_pairs) {
     PairCountRead rd;
     uint32_t* box = pair_counts_box(gm.ft, rd);
     const bool full = (f->flags & RR_FLAG_FULL_BINNING) != 0;
-    const bool fit = gather_bins_fit(f->width, f->height);
-    // the split scan's lists: the windowed paths and the list-driven gather paths read them (it also
-    // keeps the device busy while the host reads the pair counts)
-    const bool need_lists = !fit || g_a_gather != 1 || (!full && g_b_gather != 2);
+    const Tuning& tu = tuning();
     {
         StageTimer tm(RR_STAGE_SCAN, st);
-        // the image buffer's per-frame block is cleared by the split scan's first launch (many
-        // workgroups) or, without a split scan, by the depth-cut kernel
         uint32_t* zero = reinterpret_cast<uint32_t*>(im.ranges);
         const int nzero = (int)(im.zero_bytes / sizeof(uint32_t));
-        const uint32_t den = full ? 1u : g_early_den;
-        if (need_lists && g_cut_in_scan) {  // the cut computed by every workgroup of the scan's first launch
-            const CutArgs ca{gm.block_sums, gm.block_wide, den, g_early_min, box, rd.seq};
-            launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(), zero,
-                              nzero, st, &ca);
-        } else {
-            launch_early_cut(P, gm.depth_keys, gm.tiles, gm.block_sums, gm.block_wide, den, g_early_min, gm.ft, gm.temp,
-                             box, rd.seq, need_lists ? nullptr : zero, nzero, st);
-            if (need_lists)
-                launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, pair_scan_direct_blocks(),
-                                  zero, nzero, st);
-        }
+        const CutArgs ca{gm.block_sums, gm.block_wide, full ? 1u : tu.early_den, tu.early_min, box, rd.seq};
+        launch_split_scan(gm.tiles, gm.depth_keys, P, gm.lists, gm.ft, gm.temp, tu.pair_scan_direct_blocks, zero,
+                          nzero, ca, st);
         RR_CHECK(hipGetLastError(), "pair-count scan");
     }
+    g_counted_img = im.final_T;
     RR_STAGE_CHECK("scan");
     // the one device->host sync of the forward (rasterizer_impl.cu:273): pairs to bin, and the
     // reference's num_rendered (sum of bounding-rect areas) which the API returns unchanged; the
@@ -586,34 +550,54 @@ int rr_forward_geometry(const rr_frame* f, const rr_camera* cam, const rr_gaussi
 
 namespace {
 
-// The bins' runs from the bin sort's last scatter (default) or from a k_bin_bounds launch over the
-// sorted keys (rr_set_tuning "bounds_in_sort" 0); windowed paths only.
-int g_bounds_in_sort = 1;
 // The backward's accumulator workspace: registered for the next forward render on this thread
-// (rr_set_forward_workspace), which zero-fills it inside its first blend launch and records it as
-// clean; a backward whose workspace is the clean one skips its own clear.
+// (rr_set_forward_workspace), which zero-fills it inside its first blend launch.
 struct WsRange {
     void* ptr = nullptr;
     size_t bytes = 0;
 };
-thread_local WsRange g_fwd_ws, g_ws_clean;
-// The backward's tile order of the last render, when its phase-B duplicate launch computed it
-// (its order array): the backward then needs no prologue at all once the workspace is clean.
-thread_local const uint32_t* g_order_ready = nullptr;
-int g_fwd_clear = 1;  // rr_set_tuning "forward_clear" 0: registrations are dropped (A/B)
-// rr_set_phase_a_event: an event recorded after each render's phase-A blend (this thread's renders)
-thread_local hipEvent_t g_phase_a_ev = nullptr;
-thread_local bool g_phase_a_done = false;
-
-// The windowed duplicate's window starts from the split scan's marks (default) or from a
-// window-starts launch (rr_set_tuning "split_marks" 0)
-int g_split_marks = 1;
+thread_local WsRange g_fwd_ws;
+// What a render leaves for its frame's backward, which may run on another host thread (autograd's
+// device thread): the workspace it zero-filled, and the backward's tile order when its phase-B
+// duplicate launch computed it (the order array).  A backward whose workspace is the clean one
+// skips its clear, and with the order ready it needs no prologue at all.  Process-wide, keyed by
+// the image buffer, the last few renders; the first backward of a frame consumes its entry (a
+// second one, of a retained graph, clears and orders by itself).
+struct FrameFacts {
+    const void* img = nullptr;
+    WsRange clean;
+    const uint32_t* order = nullptr;
+};
+std::mutex g_facts_mu;
+std::deque<FrameFacts> g_facts;
+constexpr size_t kMaxFacts = 16;
+thread_local FrameFacts g_render_facts;  // the facts of the render in progress on this thread
+void publish_facts(const FrameFacts& f) {
+    std::lock_guard<std::mutex> lk(g_facts_mu);
+    for (auto it = g_facts.begin(); it != g_facts.end(); ++it)
+        if (it->img == f.img) {
+            g_facts.erase(it);
+            break;
+        }
+    if (f.clean.ptr || f.order) g_facts.push_back(f);
+    if (g_facts.size() > kMaxFacts) g_facts.pop_front();
+}
+FrameFacts take_facts(const void* img) {
+    std::lock_guard<std::mutex> lk(g_facts_mu);
+    for (auto it = g_facts.begin(); it != g_facts.end(); ++it)
+        if (it->img == img) {
+            const FrameFacts f = *it;
+            g_facts.erase(it);
+            return f;
+        }
+    return FrameFacts{};
+}
 
 // Tile lists for one frame: duplicate -> pairs into their bins -> per-bin depth order + tile lists
 // -> blend, once (single phase) or as the two phases of early-stop binning (rr_kernels.hpp
 // BlendPhase).  The host knows the frame's total L only: phase A's pairs go to region [0, L) of the
 // pair arrays and phase B's to region [L, 2L); every launch is sized for L and reads its phase's
-// count on the device (the gather paths' counters, or FrameTotals LA / LB for the windowed ones).
+// count on the device (FrameTotals LA / LB, or the gather path's counters).
 template <typename K>
 int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn, const int* radii, int P, int W,
                  int H, int cull, bool early, BlendFwdArgs b, hipStream_t st) {
@@ -624,47 +608,22 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
     DupArgs<K> d{};
     d.P = P; d.splats = gm.splats; d.radii = radii;
     d.gx = gx; d.gy = gy; d.cull = cull;
-    d.tiles = gm.tiles; d.depth_keys = gm.depth_keys; d.ft = gm.ft;
+    d.tiles = gm.tiles;
     const PhaseHints h = phase_hints(L, early);
-    const bool fit = gather_bins_fit(W, H);
-    const bool gather_a = fit && a_gather_dup();
-    const bool count_a = fit && g_a_gather == 3;  // windowed duplicate, count / scatter bin sort
-    const bool gather = early && fit && phase_b_gather();
-    if (bn.compact != (gather_a && (gather || !early)) && bn.compact)
-        return fail(RR_ERR_ARG, "binning path changed between carving and rendering");
-    // phase B's region of the pair arrays (compact: phase A's, dead once its sort-expand has run)
-    const uint32_t offB = bn.compact ? 0u : L;
-    uint32_t* report = g_mailbox.failed ? nullptr : g_mailbox.dev;
-    // phase A (or the only phase): its pairs for every tile
-    const RadixPlan pa = bn.compact ? RadixPlan{} : tile_plan<K>(bn.temp, L, bn.bits, h.a);
-    const RadixPlan pb = bn.compact ? RadixPlan{} : tile_plan<K>(bn.temp, L, bn.bits, h.b);  // phase B
+    const bool gather = early && b_gather(W, H);
+    const RadixPlan pa = tile_plan<K>(bn.temp, L, bn.bits, h.a);  // phase A (or the only phase)
+    const RadixPlan pb = tile_plan<K>(bn.temp, L, bn.bits, h.b);  // phase B (windowed path)
     bool starts_b = false;  // phase B's window starts computed with phase A's
     // window starts marked by the split scan (units of kSplitWin pairs), else a window-starts launch
-    const bool marks_a = g_split_marks && pa.unit_items == kSplitWin && (uint32_t)pa.units <= gm.lists.nwin;
-    const bool marks_b = g_split_marks && pb.unit_items == kSplitWin && (uint32_t)pb.units <= gm.lists.nwin;
-    if (gather_a) {
-        {
-            StageTimer tm(RR_STAGE_DUPLICATE, st);
-            d.keys = keys; d.vals = bn.vals; d.n_total = im.counters + 2;
-            d.n_list = &gm.ft->GA; d.idx = g_a_gather == 2 ? gm.lists.idx_a : nullptr;
-            launch_dup_gather<K>(d, false, st);
-            d.n_total = nullptr; d.idx = nullptr;
-        }
-        RR_STAGE_CHECK("duplicate (gather)");
-        {
-            StageTimer tm(RR_STAGE_RANGES, st);
-            launch_sortexpand_small<K>(P, keys, bn.vals, im.counters + 2, im.bin_cnt_a, bn.vals_sorted, gm.depth_keys,
-                                       gm.ft, gx, gy, 0u, bn.point_list, im.ranges, nullptr, im.bounds_a, nullptr, st);
-        }
-        RR_STAGE_CHECK("sort-expand (gather)");
-    } else {
+    const bool marks_a = pa.unit_items == kSplitWin && (uint32_t)pa.units <= gm.lists.nwin;
+    const bool marks_b = pb.unit_items == kSplitWin && (uint32_t)pb.units <= gm.lists.nwin;
+    // phase A (or the only phase): its pairs for every tile
     {
         StageTimer tm(RR_STAGE_DUPLICATE, st);
         d.n_list = &gm.ft->GA; d.idx = gm.lists.idx_a; d.off = gm.lists.off_a;
         d.first = marks_a ? gm.lists.first_a : bn.first;
         d.pair0 = 0; d.win = (uint32_t)pa.unit_items; d.nwin = pa.units; d.L_dev = &gm.ft->LA;
-        // (count_a: the windows' digit counts are not read; one digit keeps their histogram trivial)
-        d.keys = keys; d.vals = bn.vals; d.dbits = count_a ? 0 : pa.dbits0; d.counts = pa.counts;
+        d.keys = keys; d.vals = bn.vals; d.dbits = pa.dbits0; d.counts = pa.counts;
         d.starts_done = marks_a;
         if (early && !gather && !marks_a && !marks_b) {
             d.first_b = bn.first + pa.units; d.pair0_b = 0; d.win_b = (uint32_t)pb.unit_items; d.nwin_b = pb.units;
@@ -674,106 +633,86 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
         d.first_b = nullptr; d.nwin_b = 0; d.starts_done = false;
     }
     RR_STAGE_CHECK("duplicate");
-    if (count_a) {  // the windows' pairs (dense, [0, LA)) counted and scattered into their bins
-        StageTimer tm(RR_STAGE_RANGES, st);
-        launch_sortexpand_small<K>(P, keys, bn.vals, &gm.ft->LA, im.bin_cnt_a, bn.vals_sorted, gm.depth_keys, gm.ft,
-                                   gx, gy, 0u, bn.point_list, im.ranges, nullptr, im.bounds_a, nullptr, st);
-        RR_STAGE_CHECK("sort-expand (count / scatter)");
-    } else {
     {
         StageTimer tm(RR_STAGE_TILE_SORT, st);
         RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys, keys_sorted, bn.vals, bn.vals_sorted, L, 0, bn.bits,
-                                     st, true, nullptr, &gm.ft->LA, h.a, g_bounds_in_sort ? im.bounds_a : nullptr),
+                                     st, true, nullptr, &gm.ft->LA, h.a, im.bounds_a),
                  std::string("bin sort (") + radix_sort_last_error() + ")");
     }
     RR_STAGE_CHECK("bin sort");
     {
         StageTimer tm(RR_STAGE_RANGES, st);
-        launch_sortexpand<K>(L, &gm.ft->LA, keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u,
-                             bn.point_list, im.ranges, nullptr, im.bounds_a, g_bounds_in_sort != 0, nullptr, st);
+        launch_sortexpand<K>(keys_sorted, bn.vals_sorted, gm.depth_keys, gm.ft, gx, gy, 0u, bn.point_list, im.ranges,
+                             nullptr, im.bounds_a, st);
     }
     RR_STAGE_CHECK("sort-expand");
-    }
-    }
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = early ? kBlendPhaseA : kBlendSingle;
-        b.order = fwd_tile_order() ? im.order : nullptr;
-        if (b.order) launch_tile_order_by_length(gx * gy, im.ranges, im.order, st);
         // the registered backward workspace (render_frame), cleared in this launch's drain
-        if (b.clear) g_ws_clean = WsRange{b.clear, b.clear_n4 * sizeof(float4)};
+        if (b.clear) g_render_facts.clean = WsRange{b.clear, b.clear_n4 * sizeof(float4)};
         launch_blend_fwd(b, st);
         b.clear = nullptr;
         b.clear_n4 = 0;
-        if (g_phase_a_ev) {  // the rows of every tile phase A finished are final from here on
-            RR_CHECK(hipEventRecord(g_phase_a_ev, st), "phase-A event");
-            g_phase_a_done = true;
-        }
     }
     RR_STAGE_CHECK("blend forward");
     if (!early) return RR_OK;
-    // phase B: its pairs, only for tiles phase A left open; region [L, 2L) of the pair arrays
+    // phase B: its pairs, only for tiles phase A left open; region [L, 2L) of the pair arrays.  The
+    // backward's tile order is computed on phase A's tile_max by an extra workgroup of the phase-B
+    // duplicate launch (counters[1] = T marks it done)
+    d.open_bits = im.open_bits; d.n_total = im.counters;
+    d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
     if (gather) {
         {
             StageTimer tm(RR_STAGE_DUPLICATE, st);
-            d.keys = keys + offB; d.vals = bn.vals + offB;
-            d.open_bits = im.open_bits; d.n_total = im.counters;
-            d.n_list = &gm.ft->GB; d.idx = g_b_gather == 2 ? nullptr : gm.lists.idx_b;
-            if (bwd_tile_order() && !fwd_tile_order() && dup_tile_order()) {
-                d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
-                if (P > 0) g_order_ready = im.order;  // launch_dup_gather's extra workgroup sorts them
-            }
-            launch_dup_gather<K>(d, true, st);
+            d.keys = keys + L; d.vals = bn.vals + L;
+            d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b;
+            d.gather_mark = im.counters + 2;
+            if (P > 0) g_render_facts.order = im.order;
+            launch_dup_gather<K>(d, st);
         }
         RR_STAGE_CHECK("duplicate (phase B gather)");
         {
             StageTimer tm(RR_STAGE_RANGES, st);
-            // phase B's tile lists right after phase A's (compact: at 4 LA, read on the device)
-            launch_sortexpand_small<K>(P, keys + offB, bn.vals + offB, im.counters, im.bin_cnt, bn.vals_sorted + offB,
-                                       gm.depth_keys, gm.ft, gx, gy, bn.compact ? 0u : 4u * L, bn.point_list,
-                                       im.ranges_b, im.open_bits, im.bounds_b, report, st,
-                                       bn.compact ? im.counters + 2 : nullptr, im.counters + 3);
+            // phase B's tile lists right after phase A's
+            launch_sortexpand_small<K>(P, keys + L, bn.vals + L, im.counters, im.bin_cnt, bn.vals_sorted + L,
+                                       gm.depth_keys, gm.ft, gx, gy, 4u * L, bn.point_list, im.ranges_b, im.open_bits,
+                                       im.bounds_b, im.counters + 3, st);
         }
         RR_STAGE_CHECK("sort-expand (phase B gather)");
     } else {
-    {
-        StageTimer tm(RR_STAGE_DUPLICATE, st);
-        d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b; d.off = gm.lists.off_b;
-        d.first = marks_b ? gm.lists.first_b : bn.first + pa.units;
-        d.pair0 = 0; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units;
-        d.L_dev = &gm.ft->LB;
-        d.keys = keys + L; d.vals = bn.vals + L; d.dbits = pb.dbits0; d.counts = pb.counts;
-        d.open_bits = im.open_bits; d.unit_len = bn.unit_len; d.n_total = im.counters;
-        // the backward's tile order on phase A's tile_max (counters[1] = T marks it done; the forward
-        // blends' own order, when enabled, shares im.order and keeps the prologue's sort instead)
-        if (bwd_tile_order() && !fwd_tile_order() && dup_tile_order()) {
-            d.order_cost = im.tile_max; d.order_out = im.order; d.order_flag = im.counters + 1; d.order_T = gx * gy;
+        {
+            StageTimer tm(RR_STAGE_DUPLICATE, st);
+            d.n_list = &gm.ft->GB; d.idx = gm.lists.idx_b; d.off = gm.lists.off_b;
+            d.first = marks_b ? gm.lists.first_b : bn.first + pa.units;
+            d.pair0 = 0; d.win = (uint32_t)pb.unit_items; d.nwin = pb.units;
+            d.L_dev = &gm.ft->LB;
+            d.keys = keys + L; d.vals = bn.vals + L; d.dbits = pb.dbits0; d.counts = pb.counts;
+            d.unit_len = bn.unit_len;
+            d.zero = nullptr; d.nzero = 0;
+            d.starts_done = starts_b || marks_b;
+            if (P > 0) g_render_facts.order = im.order;
+            launch_duplicate<K>(d, st);
         }
-        d.zero = nullptr; d.nzero = 0;
-        d.starts_done = starts_b || marks_b;
-        launch_duplicate<K>(d, st);
-    }
-    RR_STAGE_CHECK("duplicate (phase B)");
-    {
-        StageTimer tm(RR_STAGE_TILE_SORT, st);
-        RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys + L, keys_sorted + L, bn.vals + L,
-                                     bn.vals_sorted + L, L, 0, bn.bits, st, true, bn.unit_len, im.counters, h.b,
-                                     g_bounds_in_sort ? im.bounds_b : nullptr),
-                 std::string("bin sort, phase B (") + radix_sort_last_error() + ")");
-    }
-    RR_STAGE_CHECK("bin sort (phase B)");
-    {
-        StageTimer tm(RR_STAGE_RANGES, st);
-        launch_sortexpand<K>(L, im.counters, keys_sorted + L, bn.vals_sorted + L, gm.depth_keys, gm.ft, gx, gy,
-                             4u * L, bn.point_list, im.ranges_b, im.open_bits, im.bounds_b, g_bounds_in_sort != 0,
-                             report, st);
-    }
-    RR_STAGE_CHECK("sort-expand (phase B)");
+        RR_STAGE_CHECK("duplicate (phase B)");
+        {
+            StageTimer tm(RR_STAGE_TILE_SORT, st);
+            RR_CHECK(radix_sort_pairs<K>(bn.temp, bn.temp_bytes, keys + L, keys_sorted + L, bn.vals + L,
+                                         bn.vals_sorted + L, L, 0, bn.bits, st, true, bn.unit_len, im.counters, h.b,
+                                         im.bounds_b),
+                     std::string("bin sort, phase B (") + radix_sort_last_error() + ")");
+        }
+        RR_STAGE_CHECK("bin sort (phase B)");
+        {
+            StageTimer tm(RR_STAGE_RANGES, st);
+            launch_sortexpand<K>(keys_sorted + L, bn.vals_sorted + L, gm.depth_keys, gm.ft, gx, gy, 4u * L,
+                                 bn.point_list, im.ranges_b, im.open_bits, im.bounds_b, st);
+        }
+        RR_STAGE_CHECK("sort-expand (phase B)");
     }
     {
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = kBlendPhaseB;
-        if (b.order) launch_tile_order_by_length(gx * gy, im.ranges_b, im.order, st);
         launch_blend_fwd(b, st);
     }
     RR_STAGE_CHECK("blend forward (phase B)");
@@ -781,6 +720,8 @@ int render_tiles(const rr_frame* f, const Geom& gm, const Img& im, const Bin& bn
 }
 
 int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
+                 void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
+                 float* out_normal, void* stream);int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
                  void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
                  float* out_normal, void* stream);
 
@@ -796,13 +737,13 @@ int blend_backward(const rr_frame* f, const rr_camera* cam, const void* geom_buf
     const Bin bn = carve_bin(const_cast<void*>(binning_buffer), 0, W, H);
     const int gx = grid_x(W), gy = grid_y(H);
     const bool blend = L > 0 && binning_buffer;
-    uint32_t* order = blend && bwd_tile_order() ? im.order : nullptr;
+    uint32_t* order = blend ? im.order : nullptr;  // heaviest tiles first
     // the accumulators already zero-filled by the forward (rr_set_forward_workspace): no clear
     const size_t nacc = (size_t)P * GACC_STRIDE;
-    const bool clean = (f->flags & RR_FLAG_WORKSPACE_REGISTERED) && g_ws_clean.ptr == gacc &&
-                       g_ws_clean.bytes >= nacc * sizeof(float);
-    g_ws_clean = WsRange{};  // this backward's accumulation dirties it
-    const bool order_ready = order && g_order_ready == order;
+    const FrameFacts facts = take_facts(im.final_T);  // this backward's accumulation dirties the workspace
+    const bool clean = (f->flags & RR_FLAG_WORKSPACE_REGISTERED) && facts.clean.ptr == gacc &&
+                       facts.clean.bytes >= nacc * sizeof(float);
+    const bool order_ready = order && facts.order == order;
     if (!clean || (order && !order_ready)) {
         StageTimer tm(RR_STAGE_MEMSET, st);
         launch_bwd_prologue(gacc, clean ? 0 : nacc, gx * gy, im.tile_max, order_ready ? nullptr : order,
@@ -851,30 +792,31 @@ int rr_forward_render_aux(const rr_frame* f, const rr_camera* cam, const rr_gaus
 
 namespace {
 
-// Binning + blend of a frame whose geometry buffer holds the sorted, scanned per-Gaussian arrays.
-int render_frame_body(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer,
-                      void* image_buffer, void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color,
-                      float* out_depth, float* out_normal, void* stream) {
+// Binning + blend of a frame whose pairs were just counted (count_pairs) into this image buffer.
+int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
+                 void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
+                 float* out_normal, void* stream) {
     const int P = f->P, W = f->width, H = f->height, L = num_pairs;
     const int cull = (f->flags & RR_FLAG_NO_TILE_CULLING) ? 0 : 1;
     // a workspace registration is used by this render (or dropped by it) either way
-    const WsRange reg = g_fwd_clear ? g_fwd_ws : WsRange{};
+    const WsRange reg = g_fwd_ws;
     g_fwd_ws = WsRange{};
-    g_ws_clean = WsRange{};
-    g_order_ready = nullptr;
     if (P == 0) return RR_OK;
     if (!out_color || !out_depth || !geom_buffer || !image_buffer || (L > 0 && !binning_buffer))
         return fail(RR_ERR_ARG, "null buffer");
     const Geom gm = carve_geom(geom_buffer, P);
     const Img im = carve_img(image_buffer, W, H);
+    if (g_counted_img != im.final_T)
+        return fail(RR_ERR_ARG, "render without a pair count of this image buffer (one render per rr_forward_geometry / "
+                                "rr_forward_from_geometry on this thread)");
+    g_counted_img = nullptr;
+    g_render_facts = FrameFacts{im.final_T, WsRange{}, nullptr};
+    publish_facts(g_render_facts);  // drops an earlier render's facts of this buffer
     const Bin bn = carve_bin(binning_buffer, L, W, H);
     if (L > 0 && binning_bytes < bn.total) return fail(RR_ERR_CAPACITY, "binning buffer too small");
     hipStream_t st = (hipStream_t)stream;
     const int gx = grid_x(W), gy = grid_y(H);
-    if (L == 0) {  // otherwise the first duplicate launch clears them (DupArgs::zero)
-        StageTimer tm(RR_STAGE_RANGES, st);
-        RR_CHECK(hipMemsetAsync(im.ranges, 0, im.zero_bytes, st), "memset ranges");
-    }
+    // (the per-frame block of the image buffer was cleared by count_pairs' split scan)
     BlendFwdArgs b{};
     b.W = W; b.H = H; b.gx = gx; b.gy = gy;
     b.ranges = im.ranges; b.ranges_b = im.ranges_b; b.open = im.open; b.open_bits = im.open_bits;
@@ -888,27 +830,18 @@ int render_frame_body(const rr_frame* f, const rr_camera* cam, const int* radii,
         StageTimer tm(RR_STAGE_BLEND_FWD, st);
         b.phase = kBlendSingle;
         launch_blend_fwd(b, st);
-        return check(f, st, "blend forward");
+        if (b.clear) g_render_facts.clean = WsRange{b.clear, b.clear_n4 * sizeof(float4)};
+        const int rc = check(f, st, "blend forward");
+        if (rc == RR_OK) publish_facts(g_render_facts);
+        return rc;
     }
-    // the split k_early_cut makes (its one-phase conditions but "no sampled pair", which leaves
+    // the split the depth cut makes (its one-phase conditions but "no sampled pair", which leaves
     // phase B empty on the device)
-    const bool early = !(f->flags & RR_FLAG_FULL_BINNING) && g_early_den > 1 && (uint32_t)L >= g_early_min;
-    return bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
-                   : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
-}
-
-// rr_set_phase_a_event: the render records the event right after phase A's blend launch
-// (render_tiles) or, on any path without one, after all its work — a waiter never sees it early.
-int render_frame(const rr_frame* f, const rr_camera* cam, const int* radii, void* geom_buffer, void* image_buffer,
-                 void* binning_buffer, size_t binning_bytes, int num_pairs, float* out_color, float* out_depth,
-                 float* out_normal, void* stream) {
-    g_phase_a_done = false;
-    const int rc = render_frame_body(f, cam, radii, geom_buffer, image_buffer, binning_buffer, binning_bytes,
-                                     num_pairs, out_color, out_depth, out_normal, stream);
-    if (g_phase_a_ev && !g_phase_a_done) {
-        const hipError_t e = hipEventRecord(g_phase_a_ev, (hipStream_t)stream);
-        if (e != hipSuccess && rc == RR_OK) return fail(RR_ERR_HIP, std::string("phase-A event: ") + hipGetErrorString(e));
-    }
+    const Tuning& tu = tuning();
+    const bool early = !(f->flags & RR_FLAG_FULL_BINNING) && tu.early_den > 1 && (uint32_t)L >= tu.early_min;
+    const int rc = bn.wide ? render_tiles<uint32_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st)
+                           : render_tiles<uint16_t>(f, gm, im, bn, radii, P, W, H, cull, early, b, st);
+    if (rc == RR_OK) publish_facts(g_render_facts);
     return rc;
 }
 
@@ -1279,7 +1212,7 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     RR_CHECK(hipMemcpyAsync(&ft, gm.ft, sizeof(ft), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(per.data(), gm.tiles, (size_t)P * sizeof(uint2), hipMemcpyDeviceToHost, st), "stats");
     RR_CHECK(hipMemcpyAsync(tm.data(), im.tile_max, (size_t)T * 4, hipMemcpyDeviceToHost, st), "stats");
-    // [0] phase-B pairs (the gather path: slots reserved), [2] phase-A pairs of the gather path,
+    // [0] phase-B pairs (the gather path: slots reserved), [2] phase B took the gather path,
     // [3] phase-B pairs the gather path's bin runs hold
     uint32_t cnt[4] = {0u, 0u, 0u, 0u};
     RR_CHECK(hipMemcpyAsync(cnt, im.counters, sizeof(cnt), hipMemcpyDeviceToHost, st), "stats");
@@ -1292,11 +1225,11 @@ int rr_read_frame_stats(const rr_frame* f, const void* geom_buffer, const void* 
     int64_t s = 0;
     for (uint32_t v : tm) s += v;
     out->l_eff = s;
-    // phase A's pairs, and the phase-B pairs kept for the tiles phase A left open (the binning path
-    // the frame took: the tuning in force now, as at its render)
-    const bool gather_a = a_gather_dup() && gather_bins_fit(W, H);
-    const bool gather_b = phase_b_gather() && gather_bins_fit(W, H);
-    out->num_binned = (gather_a ? (int64_t)cnt[2] : (int64_t)ft.LA) + (gather_b ? cnt[3] : cnt[0]);
+    // phase A's pairs, and the phase-B pairs kept for the tiles phase A left open (by the path the
+    // frame took: its phase-B duplicate marks the gather path in counters[2])
+    out->num_binned = (int64_t)ft.LA + (cnt[2] ? cnt[3] : cnt[0]);
+    out->phase_b_pairs = (int64_t)ft.LB;
+    out->phase_b_slots = (int64_t)cnt[0];
     return RR_OK;
 }
 
@@ -1315,15 +1248,6 @@ int rr_debug_get_views(const rr_frame* f, const void* geom_buffer, const void* i
     return RR_OK;
 }
 
-int rr_set_blend_config(int fwd_waves, int bwd_waves) {
-    auto ok = [](int v) { return v == 0 || v == 1 || v == 2 || v == 4; };
-    // bwd 3 = one wave per tile without the 4-waves/SIMD register cap (A/B tuning variant)
-    if (!ok(fwd_waves) || !(ok(bwd_waves) || bwd_waves == 3))
-        return fail(RR_ERR_ARG, "waves per tile must be 0, 1, 2 or 4");
-    set_blend_config(fwd_waves, bwd_waves);
-    return RR_OK;
-}
-
 int rr_debug_set_fwd_trace(void* dev_buf) {
     set_fwd_trace(dev_buf);
     return RR_OK;
@@ -1336,89 +1260,33 @@ int rr_set_forward_workspace(void* workspace, size_t bytes) {
     return RR_OK;
 }
 
-int rr_set_phase_a_event(int on) {
-    if (on && !g_phase_a_ev) {
-        const hipError_t e = hipEventCreateWithFlags(&g_phase_a_ev, hipEventDisableTiming);
-        if (e != hipSuccess) {
-            g_phase_a_ev = nullptr;
-            return fail(RR_ERR_HIP, std::string("phase-A event: ") + hipGetErrorString(e));
-        }
-    } else if (!on && g_phase_a_ev) {
-        (void)hipEventDestroy(g_phase_a_ev);
-        g_phase_a_ev = nullptr;
-    }
-    return RR_OK;
-}
-
-void* rr_phase_a_event(void) { return g_phase_a_ev; }
-
-int rr_frame_open_tiles(const rr_frame* f, const void* image_buffer, const void** bits, int* tiles_x, int* tiles_y) {
-    if (!f || !image_buffer || !bits || !tiles_x || !tiles_y) return fail(RR_ERR_ARG, "null argument");
-    if (f->width <= 0 || f->height <= 0) return fail(RR_ERR_ARG, "empty frame");
-    const Img im = carve_img(const_cast<void*>(image_buffer), f->width, f->height);
-    *bits = im.open_bits;
-    *tiles_x = grid_x(f->width);
-    *tiles_y = grid_y(f->height);
-    return RR_OK;
-}
-
 int rr_set_tuning(const char* key, int value) {
-    if (key && std::string(key) == "early_den") {  // early-stop split: phase A ~1/den of the pairs
-        g_early_den = value > 0 ? (uint32_t)value : kEarlyDen;
-        return RR_OK;
-    }
-    if (key && std::string(key) == "sx_b_threads") {
-        set_sx_b_threads(value);
-        return RR_OK;
-    }
-    if (key && std::string(key) == "dup_b_reserve") {
-        set_dup_b_reserve(value != 0);
-        return RR_OK;
-    }
-    if (key && std::string(key) == "dup_b_rows") {
-        set_dup_b_rows(value != 0);
-        return RR_OK;
-    }
-    if (key && std::string(key) == "dup_big_bins") {
-        set_dup_big_bins(value);
-        return RR_OK;
-    }
-    if (key && std::string(key) == "cut_in_scan") {
-        g_cut_in_scan = value != 0;
-        return RR_OK;
-    }
-    if (key && std::string(key) == "sx_lds_cap") {  // runs longer than this: global sort path
-        set_sx_lds_cap(value);
-        return RR_OK;
-    }
-    if (key && std::string(key) == "forward_clear") {
-        g_fwd_clear = value != 0;
-        return RR_OK;
-    }
-    if (key && std::string(key) == "split_marks") {
-        g_split_marks = value != 0;
-        return RR_OK;
-    }
-    if (key && std::string(key) == "bounds_in_sort") {
-        g_bounds_in_sort = value != 0;
-        return RR_OK;
-    }
-    if (key && std::string(key) == "phase_b_gather") {
-        g_b_gather = value < 0 ? -1 : (value > 2 ? 1 : value);
-        return RR_OK;
-    }
-    if (key && std::string(key) == "phase_a_gather") {
-        g_a_gather = value >= 1 && value <= 3 ? value : 0;
-        return RR_OK;
-    }
-    if (set_tuning(key, value) != 0) return fail(RR_ERR_ARG, std::string("unknown tuning key: ") + (key ? key : "(null)"));
+    if (!key) return fail(RR_ERR_ARG, "unknown tuning key: (null)");
+    const std::string k(key);
+    Tuning& tu = tuning();
+    const Tuning dflt{};
+    if (k == "early_den") tu.early_den = value > 0 ? (uint32_t)value : dflt.early_den;
+    else if (k == "pair_scan_direct_blocks") tu.pair_scan_direct_blocks = value >= 0 ? value : dflt.pair_scan_direct_blocks;
+    else if (k == "wide_bin_keys") tu.wide_bin_keys = value != 0;
+    else if (k == "phase_b_gather") tu.b_gather = value != 0;
+    else if (k == "dup_b_rows") tu.dup_b_rows = value != 0;
+    else if (k == "dup_big_bins") tu.dup_big_bins = value >= 0 ? value : dflt.dup_big_bins;
+    else if (k == "sx_bucket") tu.sx_bucket = value != 0;
+    else if (k == "sx_lds_cap") tu.sx_lds_cap = value > 0 ? value : 0;
+    else if (k == "sort_min_units") tu.sort_min_units = value > 0 ? value : dflt.sort_min_units;
+    else if (k == "sort_min_units_tile") tu.sort_min_units_tile = value > 0 ? value : dflt.sort_min_units_tile;
+    else if (k == "sort_max_rounds")
+        tu.sort_max_rounds = (value == 1 || value == 2 || value == 4 || value == 8) ? value : dflt.sort_max_rounds;
+    else return fail(RR_ERR_ARG, "unknown tuning key: " + k);
     return RR_OK;
 }
 
 int rr_set_binning_config(int split_denominator, int min_pairs) {
     if (split_denominator < 0 || min_pairs < 0) return fail(RR_ERR_ARG, "negative binning config");
-    g_early_den = split_denominator == 0 ? kEarlyDen : (uint32_t)split_denominator;
-    g_early_min = min_pairs == 0 ? kEarlyMin : (uint32_t)min_pairs;
+    Tuning& tu = tuning();
+    const Tuning dflt{};
+    tu.early_den = split_denominator == 0 ? dflt.early_den : (uint32_t)split_denominator;
+    tu.early_min = min_pairs == 0 ? dflt.early_min : (uint32_t)min_pairs;
     return RR_OK;
 }
 

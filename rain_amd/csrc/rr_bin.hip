@@ -11,15 +11,16 @@
 //
 // Early-stop binning (rr_kernels.hpp BlendPhase) splits the pairs by DEPTH instead of by depth
 // rank: phase A holds the pairs of the Gaussians nearer than a cut chosen per frame from a sampled,
-// pair-weighted depth histogram (k_early_cut: ~1/den of the pairs), phase B the others.  Each
-// tile's phase-A list is then a prefix of its full depth-ordered list and the B list the rest, which
-// is all the two-phase blend needs (any cut gives the full lists' outputs).
+// pair-weighted depth histogram (~1/den of the pairs), phase B the others.  Each tile's phase-A
+// list is then a prefix of its full depth-ordered list and the B list the rest, which is all the
+// two-phase blend needs (any cut gives the full lists' outputs).
 //
-//   k_early_cut        one workgroup: frame totals from the preprocess block sums, the depth cut
-//                      from sampled {depth key, pairs}
-//   k_early_cut        ... and publishes the frame's total pairs to the host (rr_api.hip mailbox)
-//   k_split_scan_*     inclusive scan of {A pairs, B pairs} per Gaussian in index order; its last
-//                      thread leaves the phases' counts in FrameTotals (device-side only)
+//   k_split_scan_totals  per block of Gaussians: the frame totals from the preprocess block sums
+//                        and the depth cut from sampled {depth key, pairs} (every workgroup, the
+//                        same cut; workgroup 0 publishes the frame's total pairs to the host,
+//                        rr_api.hip mailbox), then the block's {A pairs, B pairs} totals
+//   k_split_scan         inclusive scan of {A pairs, B pairs} per Gaussian in index order; its last
+//                        thread leaves the phases' counts in FrameTotals (device-side only)
 //   k_sortexpand<K>    per bin: depth sort of its run + the split into its four tiles' lists
 #include <algorithm>
 
@@ -36,14 +37,8 @@ namespace rr {
 // den <= 1, a frame below min_pairs pairs or no sampled pair: cut = all ones (one phase).
 constexpr int kCutBuckets = 4096;
 constexpr int kCutShift = kDepthKeyBits - 12;
-// evenly spaced Gaussians: every one up to 4096, ~1 in 245 at 1M (the cut only steers the split's
-// balance; any cut gives the same lists).  Per-bucket sums fit 32 bits: <= 4096 samples of at most
-// 2^18 bins each.
+// Per-bucket sums fit 32 bits: <= 4096 samples of at most 2^18 bins each.
 constexpr int kCutSamples = 4096;
-constexpr int kCutSamplesPerThread = kCutSamples / 1024;
-#ifndef RR_MAILBOX_RELEASE
-#define RR_MAILBOX_RELEASE 0  // 1: the sequence number as a system-scope release store (A/B builds)
-#endif
 
 // Clears the image buffer's per-frame block (tile ranges, counters, open bits, bin runs and counts:
 // rr_api.hip carve_img) in a grid-stride loop, 16 B per store (a carved array: 16-B aligned).
@@ -62,8 +57,8 @@ __device__ __forceinline__ void clear_words(uint32_t* __restrict__ zero, int nze
 // balance, any cut gives the same lists.
 
 // The frame's totals (L, rect, wide: the preprocess block sums) and the depth cut, computed by one
-// workgroup of NT threads: k_early_cut (1024 threads, alone) or every workgroup of k_cut_totals
-// (256, the split scan's first launch, each from the same inputs by the same steps: the same cut).
+// workgroup of NT threads — every workgroup of the split scan's first launch, each from the same
+// inputs by the same steps: the same cut.
 template <int NT>
 struct CutShared {
     uint32_t hist[kCutBuckets];
@@ -196,9 +191,6 @@ __device__ __forceinline__ void publish_cut(const CutResult& r, FrameTotals* ft,
         __hip_atomic_store(box + 1, r.rect > sat ? sat : (uint32_t)r.rect, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(box + 3, r.wide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#if RR_MAILBOX_RELEASE
-        __hip_atomic_store(box + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
         // The host reads only the mailbox words, which the system-scope stores above write
         // through to host memory (sc0 sc1): waiting for their completion orders them before the
         // sequence number.  A release store here would also write back every dirty line of this
@@ -206,29 +198,7 @@ __device__ __forceinline__ void publish_cut(const CutResult& r, FrameTotals* ft,
         // the host reads needs.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(box + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
     }
-}
-
-__global__ __launch_bounds__(1024) void k_early_cut(int P, const uint32_t* __restrict__ keys,
-                                                    const uint2* __restrict__ tiles,
-                                                    const uint2* __restrict__ block_sums,
-                                                    const uint32_t* __restrict__ block_wide, int nb, uint32_t den,
-                                                    uint32_t min_pairs, FrameTotals* __restrict__ ft, uint32_t* box,
-                                                    uint32_t seq, uint32_t* __restrict__ zero, int nzero) {
-    __shared__ CutShared<1024> sh;
-    if (zero) clear_words(zero, nzero);
-    const CutResult r = depth_cut<1024>(sh, P, keys, tiles, block_sums, block_wide, nb, den, min_pairs);
-    if (threadIdx.x == 0) publish_cut(r, ft, box, seq);
-}
-
-void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
-                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, void* temp,
-                      uint32_t* box, uint32_t seq, uint32_t* zero, int nzero, hipStream_t st) {
-    (void)temp;
-    if (P <= 0) return;
-    k_early_cut<<<1, 1024, 0, st>>>(P, keys, tiles, block_sums, block_wide, (P + 255) / 256, den, min_pairs, ft, box,
-                                    seq, zero, nzero);
 }
 
 // ---- the phases' Gaussian lists: scan of {A pairs, B pairs, A rows, B rows} in index order ------
@@ -265,21 +235,17 @@ __device__ __forceinline__ Quad quad_block_sum(Quad x, Quad* s) {
     return quad_add(quad_add(s[0], s[1]), quad_add(s[2], s[3]));
 }
 
-// CUT: the depth cut computed here by every workgroup (depth_cut<256>: the same cut in each) and
-// published by workgroup 0 — k_early_cut's job without its launch; else the cut from ft.  Each
-// workgroup samples kCutScanSamples Gaussians (16 runs of 64: the cut only steers the phases'
-// balance, and the per-workgroup histogram is 4x cheaper than k_early_cut's 4096 samples).
-#ifndef RR_CUT_SCAN_SAMPLES
-#define RR_CUT_SCAN_SAMPLES 1024
-#endif
-constexpr int kCutScanSamples = RR_CUT_SCAN_SAMPLES;
-template <bool CUT>
+// The depth cut computed here by every workgroup (depth_cut<256>: the same cut in each) and
+// published by workgroup 0 (no launch of its own).  Each workgroup samples kCutScanSamples
+// Gaussians (16 runs of 64: the cut only steers the phases' balance, and the per-workgroup
+// histogram is 4x cheaper than 4096 samples).
+constexpr int kCutScanSamples = 1024;
 __global__ __launch_bounds__(256) void k_split_scan_totals(const uint2* __restrict__ tiles,
                                                            const uint32_t* __restrict__ keys, int P,
                                                            FrameTotals* __restrict__ ft, Quad* __restrict__ tot,
                                                            uint32_t* __restrict__ zero, int nzero, CutArgs ca) {
     __shared__ Quad s[4];
-    __shared__ CutShared<CUT ? 256 : 64> sh;
+    __shared__ CutShared<256> sh;
     // this block's items first: their loads overlap the cut's
     constexpr int IPT = kPairScanItems / 256;
     const size_t b0 = (size_t)blockIdx.x * kPairScanItems;
@@ -290,15 +256,10 @@ __global__ __launch_bounds__(256) void k_split_scan_totals(const uint2* __restri
         in[r] = i < (size_t)P ? tiles[i].x : 0u;
         ik[r] = i < (size_t)P ? keys[i] : 0u;
     }
-    uint32_t cut;
-    if constexpr (CUT) {
-        const CutResult r = depth_cut<256, kCutScanSamples>(sh, P, keys, tiles, ca.block_sums, ca.block_wide,
-                                                            (P + 255) / 256, ca.den, ca.min_pairs);
-        if (blockIdx.x == 0 && threadIdx.x == 0) publish_cut(r, ft, ca.box, ca.seq);
-        cut = r.cut;
-    } else {
-        cut = ft->cut;
-    }
+    const CutResult r = depth_cut<256, kCutScanSamples>(sh, P, keys, tiles, ca.block_sums, ca.block_wide,
+                                                        (P + 255) / 256, ca.den, ca.min_pairs);
+    if (blockIdx.x == 0 && threadIdx.x == 0) publish_cut(r, ft, ca.box, ca.seq);
+    const uint32_t cut = r.cut;
     if (zero) clear_words(zero, nzero);
     Quad x{0, 0, 0, 0};
 #pragma unroll
@@ -408,21 +369,17 @@ __global__ __launch_bounds__(256) void k_split_scan(const uint2* __restrict__ ti
     if (blockIdx.x == gridDim.x - 1 && t == 255) store_split(ft, ex);
 }
 
-// the split scan's block totals, or (first) k_early_cut's samples
+// the split scan's block totals
 size_t split_scan_temp_bytes(int P) {
-    return std::max((size_t)std::max((P + kPairScanItems - 1) / kPairScanItems, 1) * sizeof(Quad),
-                    (size_t)kCutSamples * sizeof(uint2));
+    return (size_t)std::max((P + kPairScanItems - 1) / kPairScanItems, 1) * sizeof(Quad);
 }
 
 void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
-                       int direct_blocks, uint32_t* zero, int nzero, hipStream_t st, const CutArgs* cut) {
+                       int direct_blocks, uint32_t* zero, int nzero, const CutArgs& cut, hipStream_t st) {
     if (P <= 0) return;
     const int nb = (P + kPairScanItems - 1) / kPairScanItems;
     Quad* tot = static_cast<Quad*>(temp);
-    if (cut)
-        k_split_scan_totals<true><<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot, zero, nzero, *cut);
-    else
-        k_split_scan_totals<false><<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot, zero, nzero, CutArgs{});
+    k_split_scan_totals<<<nb, 256, 0, st>>>(tiles, keys, P, ft, tot, zero, nzero, cut);
     if (nb <= direct_blocks) {
         k_split_scan<false><<<nb, 256, 0, st>>>(tiles, keys, P, tot, lists, ft);
     } else {
@@ -432,38 +389,16 @@ void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLis
 }
 
 // ---- per bin: depth order + the four tile lists (rr_sortexpand.hpp) ----------------------------
-int g_sx_bucket = 1;  // rr_set_tuning "sx_bucket"
-int g_sx_lds_cap = kSxCap;  // rr_set_tuning "sx_lds_cap": longer runs take the global path (tests)
-int g_sx_b_threads = 1024;  // rr_set_tuning "sx_b_threads": phase B's sort-expand workgroup (256 / 1024)
-uint32_t sx_lds_cap() { return (uint32_t)g_sx_lds_cap; }
-
-// Every bin's run [start, end) of the bin-sorted keys into `bounds`, which the caller zeroed (it
-// lives in the image buffer's cleared block): the first item of a bin writes its start, the last its
-// end; a bin without pairs keeps {0, 0}.  One launch over the pairs instead of a binary search in
-// every k_sortexpand workgroup (and no loop over the empty bins between two keys: phase B's keys are
-// sparse, and such loops cost 24 us there).
-template <typename K>
-__global__ __launch_bounds__(256) void k_bin_bounds(uint32_t n_host, const uint32_t* __restrict__ n_dev,
-                                                    const K* __restrict__ keys, uint2* __restrict__ bounds) {
-    const uint32_t n = n_dev ? *n_dev : n_host;
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = (uint32_t)keys[i];
-    if (i == 0 || (uint32_t)keys[i - 1] != k) bounds[k].x = ~i;  // {~start, end}: rr_kernels.hpp
-    if (i + 1 == n || (uint32_t)keys[i + 1] != k) bounds[k].y = i + 1;
-}
-
-// Phase B's pair count to the host mailbox (word 5; rr_api.hip): the next frame chooses its phase-B
-// binning from it (a prediction only: both ways give the same lists).
-__device__ __forceinline__ void report_phase_b(uint32_t* box, uint32_t n) {
-    __hip_atomic_store(box + 5, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// per-bin runs longer than this go through the global path (Tuning::sx_lds_cap lowers it for tests)
+uint32_t sx_lds_cap(int cap) {
+    const int t = tuning().sx_lds_cap;
+    return (uint32_t)(t >= 1 && t < cap ? t : cap);
 }
 
 // Phase B of the gather path (k_dup_gather emitted its pairs densely, [0, n), in no particular
 // order): k_bin_count counts them per bin, k_bin_scatter turns the counts into every bin's run
 // (bounds) and drops each pair's value into its bin's run (order inside a bin arbitrary:
-// k_sortexpand restores (depth, index) order).  Two launches instead of the bin sort's five and the
-// bounds launch (a separate one-workgroup scan launch between them until round 5).  Count and
+// k_sortexpand restores (depth, index) order).  Two launches instead of the bin sort's five.  Count and
 // scatter run kBinGroups workgroups over the same
 // strided item sets; each aggregates its items per bin in LDS, so a global atomic is paid per
 // (workgroup, bin) and not per pair (per-pair atomics on a few hot bins serialise: +40 us).
@@ -552,28 +487,21 @@ __global__ __launch_bounds__(1024) void k_bin_scatter(const void* __restrict__ k
     }
 }
 
-// per bin: open test (phase B), the bin's run from k_bin_bounds, then sortexpand_run
-#ifndef RR_SX_OCC
-#define RR_SX_OCC 1  // a minimum of 6 workgroups per CU (69 VGPRs instead of 81) measured neutral:
-                     // ranges 0.0925 vs 0.0919 ms/step (profiles/r05_dup_big_sx_occ_ab.jsonl)
-#endif
+// per bin: open test (phase B), the bin's run (bounds: the bin sort's last scatter or k_bin_scatter),
+// then sortexpand_run
 template <typename K, int NT>
-__global__ __launch_bounds__(NT, NT == 256 ? RR_SX_OCC : 1) void k_sortexpand(const uint2* __restrict__ bounds,
+__global__ __launch_bounds__(NT) void k_sortexpand(const uint2* __restrict__ bounds,
                                                     const K* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ depth_keys,
                                                     const FrameTotals* __restrict__ ft, int gx, int gy,
                                                     uint32_t out_base, uint32_t* __restrict__ point_list,
                                                     uint2* __restrict__ ranges, const uint32_t* __restrict__ open_bits,
-                                                    uint32_t lds_cap, const uint32_t* __restrict__ n_dev,
-                                                    uint32_t* report,
-                                                    int ipasses, const uint32_t* __restrict__ out_base_dev,
-                                                    int bucket) {
+                                                    uint32_t lds_cap, int ipasses, int bucket) {
     constexpr int CAP = NT == 1024 ? kSxCapB : kSxCap;
     __shared__ SxSharedT<NT / 64, CAP> sh;
     const int bgx = bins_x(gx);
     const int bin = blockIdx.x;
     const int X = bin % bgx, Y = bin / bgx;
-    if (report && bin == 0 && threadIdx.x == 0) report_phase_b(report, *n_dev);
     if (open_bits) {  // phase B: a bin whose tiles all closed in phase A holds no pair, and its
                       // tiles' ranges were cleared with the frame's: nothing to search or write
         bool any = false;
@@ -589,34 +517,23 @@ __global__ __launch_bounds__(NT, NT == 256 ? RR_SX_OCC : 1) void k_sortexpand(co
     }
     const uint2 run = bounds[bin];  // the bin's run [lo, hi) of the bin-sorted pairs, {~lo, hi}
     const uint32_t lo = run.y ? ~run.x : 0u;
-    // out_base_dev: the lists start after the 4 slots per pair of an earlier phase (compact layout)
-    const uint32_t ob = out_base_dev ? out_base + 4u * *out_base_dev : out_base;
     sortexpand_run<NT, CAP>(sh, X, Y, gx, gy, lo, run.y - lo, vals, false, depth_keys, ft->wide != 0u, ipasses,
-                            ob, point_list, ranges, lds_cap, bucket != 0);
+                            out_base, point_list, ranges, lds_cap, bucket != 0);
 }
 
 template <typename K>
-void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
-                       const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
-                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* bounds,
-                       bool bounds_ready, uint32_t* report, hipStream_t st) {
+void launch_sortexpand(const K* keys, const uint32_t* vals, const uint32_t* depth_keys, const FrameTotals* ft, int gx,
+                       int gy, uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
+                       const uint2* bounds, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0) return;
-    if (L > 0 && !bounds_ready) k_bin_bounds<K><<<(L + 255) / 256, 256, 0, st>>>(L, n_dev, keys, bounds);
     k_sortexpand<K, 256><<<nb, 256, 0, st>>>(bounds, keys, vals, depth_keys, ft, gx, gy, out_base, point_list, ranges,
-                                        open_bits, sx_lds_cap(), n_dev, n_dev ? report : nullptr, 0, nullptr,
-                                        g_sx_bucket);
+                                             open_bits, sx_lds_cap(kSxCap), 0, tuning().sx_bucket);
 }
-template void launch_sortexpand<uint16_t>(uint32_t, const uint32_t*, const uint16_t*, const uint32_t*, const uint32_t*,
-                                          const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, bool, uint32_t*, hipStream_t);
-template void launch_sortexpand<uint32_t>(uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                                          const FrameTotals*, int, int, uint32_t, uint32_t*, uint2*, const uint32_t*,
-                                          uint2*, bool, uint32_t*, hipStream_t);
-
-void set_sx_bucket(bool on) { g_sx_bucket = on ? 1 : 0; }
-void set_sx_b_threads(int n) { g_sx_b_threads = n == 256 ? 256 : 1024; }
-void set_sx_lds_cap(int cap) { g_sx_lds_cap = (cap >= 1 && cap <= kSxCap) ? cap : kSxCap; }
+template void launch_sortexpand<uint16_t>(const uint16_t*, const uint32_t*, const uint32_t*, const FrameTotals*, int,
+                                          int, uint32_t, uint32_t*, uint2*, const uint32_t*, const uint2*, hipStream_t);
+template void launch_sortexpand<uint32_t>(const uint32_t*, const uint32_t*, const uint32_t*, const FrameTotals*, int,
+                                          int, uint32_t, uint32_t*, uint2*, const uint32_t*, const uint2*, hipStream_t);
 
 int index_passes(int P) {  // 9-bit passes covering the Gaussian indices [0, P)
     int b = 1;
@@ -628,34 +545,24 @@ template <typename K>
 bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
-                             uint2* bounds, uint32_t* report, hipStream_t st, const uint32_t* out_base_dev,
-                             uint32_t* kept) {
+                             uint2* bounds, uint32_t* kept, hipStream_t st) {
     const int nb = bins_x(gx) * bins_y(gy);
     if (nb <= 0 || nb > kBinScanMax) return false;
     const int wk = sizeof(K) == 4;
     k_bin_count<<<kBinGroups, 1024, 0, st>>>(keys, wk, n_dev, nb, bin_cnt);
     k_bin_scatter<<<kBinGroups, 1024, 0, st>>>(keys, wk, vals, n_dev, nb, bin_cnt, bounds, vals_sorted, kept);
-    // phase B (open_bits): few bins hold pairs, so a bin's latency sets the launch's time — 1024
-    // threads per bin (rr_set_tuning "sx_b_threads" 256: the phase-A shape)
-    // (its LDS runs hold kSxCapB pairs; a lowered "sx_lds_cap" applies to it too)
-    if (open_bits && g_sx_b_threads == 1024)
-        k_sortexpand<K, 1024><<<nb, 1024, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base,
-                                                   point_list, ranges, open_bits,
-                                                   g_sx_lds_cap == kSxCap ? (uint32_t)kSxCapB : sx_lds_cap(), n_dev, report,
-                                                   index_passes(P), out_base_dev, g_sx_bucket);
-    else
-        k_sortexpand<K, 256><<<nb, 256, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base,
-                                                 point_list, ranges, open_bits, sx_lds_cap(), n_dev, report,
-                                                 index_passes(P), out_base_dev, g_sx_bucket);
+    // phase B: few bins hold pairs, so a bin's latency sets the launch's time — 1024 threads per bin
+    // (its LDS runs hold kSxCapB pairs)
+    k_sortexpand<K, 1024><<<nb, 1024, 0, st>>>(bounds, keys, vals_sorted, depth_keys, ft, gx, gy, out_base, point_list,
+                                               ranges, open_bits, sx_lds_cap(kSxCapB), index_passes(P),
+                                               tuning().sx_bucket);
     return true;
 }
 template bool launch_sortexpand_small<uint16_t>(int, const uint16_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
-                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t,
-                                                const uint32_t*, uint32_t*);
+                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t);
 template bool launch_sortexpand_small<uint32_t>(int, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t*,
                                                 uint32_t*, const uint32_t*, const FrameTotals*, int, int, uint32_t,
-                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t,
-                                                const uint32_t*, uint32_t*);
+                                                uint32_t*, uint2*, const uint32_t*, uint2*, uint32_t*, hipStream_t);
 
 }  // namespace rr

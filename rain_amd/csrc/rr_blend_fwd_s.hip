@@ -55,7 +55,7 @@ __global__ __launch_bounds__(64 * NW, RR_FWD_S_OCC) void k_blend_fwd_s(BlendFwdA
         for (size_t i = i0 + threadIdx.x; i < a.clear_n4; i += nb * blockDim.x) a.clear[i] = z;
         return;
     }
-    const int tile = a.order ? (int)a.order[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
+    const int tile = xcd_tile(blockIdx.x, ntiles);
     if (a.phase == kBlendPhaseB && !a.open[tile]) return;  // finished in phase A
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int t = threadIdx.x;
@@ -320,31 +320,26 @@ uint32_t* g_fwd_trace = nullptr;
 }
 void set_fwd_trace(void* dev_buf) { g_fwd_trace = static_cast<uint32_t*>(dev_buf); }
 
-void launch_blend_fwd_s(const BlendFwdArgs& a_in, int waves, hipStream_t st) {
+// Phase A (or a single-phase frame): 2 waves per tile (2 pixels per lane); phase B, whose few open
+// tiles each set the launch's length: 4 (1 pixel per lane).
+void launch_blend_fwd(const BlendFwdArgs& a_in, hipStream_t st) {
     BlendFwdArgs a = a_in;
     a.trace = g_fwd_trace;
     const int T = a.gx * a.gy;
     if (T == 0) return;
     const bool aux = a.out_normal != nullptr;
+    const int waves = a.phase == kBlendPhaseB ? 4 : 2;
     // workspace clear: ~16 float4 stores per thread, at most 4096 extra workgroups
     const size_t per_block = (size_t)64 * waves * 16;
     const int nc = (a.clear && a.clear_n4) ? (int)std::min<size_t>((a.clear_n4 + per_block - 1) / per_block, 4096) : 0;
     const int nb = T + nc;
-    if (waves == 1) {
-        if (aux) k_blend_fwd_s<1, true><<<nb, 64, 0, st>>>(a);
-        else k_blend_fwd_s<1, false><<<nb, 64, 0, st>>>(a);
-    } else if (waves == 4) {
+    if (waves == 4) {
         if (aux) k_blend_fwd_s<4, true><<<nb, 256, 0, st>>>(a);
         else k_blend_fwd_s<4, false><<<nb, 256, 0, st>>>(a);
     } else {
         if (aux) k_blend_fwd_s<2, true><<<nb, 128, 0, st>>>(a);
         else k_blend_fwd_s<2, false><<<nb, 128, 0, st>>>(a);
     }
-}
-
-void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st) {
-    if (a.gx * a.gy == 0) return;
-    launch_blend_fwd_s(a, blend_fwd_s_waves(a.phase == kBlendPhaseB), st);
 }
 
 }  // namespace rr

@@ -151,12 +151,6 @@ void launch_unpack_rows(int world, int rows_per_rank, const char* recv, size_t c
 }
 
 
-namespace {
-int g_pair_scan_direct = kPairScanDirectBlocks;
-}
-void set_pair_scan_direct_blocks(int nb) { g_pair_scan_direct = nb >= 0 ? nb : kPairScanDirectBlocks; }
-int pair_scan_direct_blocks() { return g_pair_scan_direct; }
-
 // First list entry of every window of `win` consecutive pairs starting at pair0: window k =
 // [pair0 + k*win, pair0 + (k+1)*win) starts inside the pair range [a, b) of exactly one entry.
 // A second window set (over a second list: the phase-B windows; nwin_b = 0: none) is marked in the
@@ -370,24 +364,18 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
     for (int d = t; d < ndig; d += 256) counts[(size_t)d * units + wb] = hist[d];
 }
 
-// The gather path of the duplicate (rasterizer_impl.cu:59-100): one thread per Gaussian of the
-// frame instead of output-driven windows over an index-ordered pair list, so it needs no pair-offset
-// scan, no window starts and no stable bin sort after it.  Phase A (PHASE_B false; also the single
-// phase of a frame binned in one go) takes the Gaussians whose depth key is below the frame's cut
-// (FrameTotals::cut) with their every (bin, Gaussian) pair — tiles[i].x, the preprocess's count, is
-// exactly what the walk emits.  Phase B takes the others and keeps only the pairs on tiles phase A
-// left open: a Gaussian whose rectangle holds no open tile is done after one record load, the
-// others count their kept pairs with a first walk.  Each workgroup reserves its pairs with one
-// atomic on *n_total and writes them densely, in no particular order: the per-bin sort
-// (rr_bin.hip k_sortexpand) restores the reference's (depth, index) order.  The extra workgroup 0
-// of phase B computes the backward's tile order as k_duplicate's does.
-// Phase-B Gaussians whose bounding rect spans more than big_bins bins (default 32; rr_set_tuning
-// "dup_big_bins", 0: none) are emitted by their whole workgroup, 256 bins at a time.
+// Phase B of early-stop binning by the gather path (the duplicate, rasterizer_impl.cu:59-100): one
+// thread per Gaussian of the phase's list (the split scan's, in index order) instead of
+// output-driven windows over a pair list, so no window starts and no stable bin sort after it.  It
+// keeps only the pairs on tiles phase A left open: a Gaussian whose rectangle holds no open tile is
+// done after one record load; the others reserve min(their pair count, their clipped rectangle's
+// open bins) slots and fill them with one walk (slots the walk leaves get a key past the last bin,
+// which the bin count and scatter skip).  Each workgroup reserves its slots with one atomic on
+// *n_total and writes them densely, in no particular order: the per-bin sort (rr_bin.hip
+// k_sortexpand) restores the reference's (depth, index) order.  The extra workgroup 0 computes the
+// backward's tile order as k_duplicate's does.  Gaussians whose rectangle spans more than big_bins
+// bins (default 32) are emitted by their whole workgroup, 256 bins at a time.
 namespace {
-int g_dup_big_bins = 32;
-int g_dup_b_reserve = 1;  // rr_set_tuning "dup_b_reserve": phase B reserves the pair count (one walk)
-int g_dup_b_rows = 1;     // rr_set_tuning "dup_b_rows": phase B's open tiles as row masks (frames <= 128 tiles wide)
-constexpr int kDupReserve = 1, kDupRows = 2;  // k_dup_gather opts bits
 // bit i of the result: bit 2i or 2i+1 of x (tile columns -> bin columns)
 __device__ __forceinline__ uint32_t pair_bits(uint64_t x) {
     x = (x | (x >> 1)) & 0x5555555555555555ull;
@@ -406,14 +394,10 @@ __device__ __forceinline__ uint64_t span_bits(int a, int b, int base) {
     return (b == 64 ? ~0ull : (1ull << b) - 1ull) & ~((1ull << a) - 1ull);
 }
 }  // namespace
-void set_dup_big_bins(int n) { g_dup_big_bins = n >= 0 ? n : 32; }
-void set_dup_b_reserve(bool on) { g_dup_b_reserve = on ? 1 : 0; }
-void set_dup_b_rows(bool on) { g_dup_b_rows = on ? 1 : 0; }
-template <typename K, bool PHASE_B>
-__global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restrict__ tiles,
-                                                    const uint32_t* __restrict__ depth_keys,
-                                                    const FrameTotals* __restrict__ ft,
-                                                    const Splat* __restrict__ splats,
+// rows: phase B's open tiles as row masks (frames up to 128 tiles wide and 256 tall; Tuning::dup_b_rows
+// off forces the flat mask of wider frames onto small ones)
+template <typename K>
+__global__ __launch_bounds__(256) void k_dup_gather(const uint2* __restrict__ tiles, const Splat* __restrict__ splats,
                                                     const int* __restrict__ radii, int gx, int gy, int cull,
                                                     K* __restrict__ keys, uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ open_bits,
@@ -422,60 +406,44 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
                                                     uint32_t* __restrict__ order_out,
                                                     uint32_t* __restrict__ order_flag, int order_T,
                                                     const uint32_t* __restrict__ list_n,
-                                                    const uint32_t* __restrict__ list_idx, int big_bins,
-                                                    int opts) {
-    const bool reserve_n = (opts & kDupReserve) != 0;
-    if (PHASE_B && order_out && blockIdx.x == 0) {
+                                                    const uint32_t* __restrict__ list_idx, int big_bins, int rows,
+                                                    uint32_t* __restrict__ gather_mark) {
+    if (gather_mark && blockIdx.x == 0 && threadIdx.x == 0) *gather_mark = 1u;
+    if (order_out && blockIdx.x == 0) {
         tile_order_body256(order_T, order_cost, open_bits, order_out);
         if (threadIdx.x == 0) *order_flag = (uint32_t)order_T;
         return;
     }
-    const int wb = (PHASE_B && order_out) ? (int)blockIdx.x - 1 : (int)blockIdx.x;
-    // list mode: the grid covers every Gaussian, the list only the phase's (block-uniform exit
-    // before the open-tile mask is staged)
-    if (list_idx && wb * 256 >= (int)*list_n) return;
-    const bool mask_lds = PHASE_B && gx * gy <= 65536;
-    __shared__ uint32_t s_open[PHASE_B ? 2048 : 1];
+    const int wb = order_out ? (int)blockIdx.x - 1 : (int)blockIdx.x;
+    // the grid covers every Gaussian, the list only the phase's (block-uniform exit before the
+    // open-tile mask is staged)
+    if (wb * 256 >= (int)*list_n) return;
+    const bool mask_lds = gx * gy <= 65536;
+    __shared__ uint32_t s_open[2048];
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t s_base;
-    __shared__ uint32_t s_big[PHASE_B ? 256 : 1];  // phase B: Gaussians of > kDupBigBins bins, done by
-    __shared__ uint32_t s_nbig;                      // the whole workgroup after the per-thread walks
-    if (PHASE_B && threadIdx.x == 0) s_nbig = 0u;
+    __shared__ uint32_t s_big[256];  // Gaussians of > big_bins bins, done by the whole workgroup
+    __shared__ uint32_t s_nbig;      // after the per-thread walks
+    if (threadIdx.x == 0) s_nbig = 0u;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int s = wb * 256 + t;
-    // this thread's Gaussian and whether it is in the phase (loads first: they overlap the mask's):
-    // entry s of the phase's Gaussian list (the split scan's, in index order: dense lanes), or
-    // Gaussian s of the frame filtered by the depth cut
+    // this thread's Gaussian (entry s of the list: dense lanes) and its pair count (loads first:
+    // they overlap the mask's).  The reservation is bounded by the pair count: the counts of the
+    // phase's Gaussians sum to its share of the frame total L, so the reservations never pass the
+    // end of the phase's region [L, 2L) (a rectangle's open bins alone can: elongated Gaussians
+    // whose culled pairs are few, on a frame where phase A closed few tiles)
     uint32_t n = 0u, g = 0u;
-    bool in_phase;
-    if (list_idx && PHASE_B) {
-        // the list holds only Gaussians with pairs; phase B reserves from the rect alone (its open
-        // bins, or its bins), so the pair count is not loaded: one dependent load less per Gaussian
-        in_phase = s < (int)*list_n;
-        if (in_phase) g = list_idx[s];
-        n = 0xffffffffu;
-    } else if (list_idx) {
-        if (s < (int)*list_n) {
-            g = list_idx[s];
-            n = tiles[g].x;
-        }
-        in_phase = n > 0u;
-    } else {
-        const uint32_t cut = ft->cut;
-        uint32_t key = 0xffffffffu;
-        g = (uint32_t)s;
-        if (s < P) {
-            n = tiles[s].x;
-            key = depth_keys[s];
-        }
-        in_phase = n > 0u && (PHASE_B ? key >= cut : key < cut);
+    if (s < (int)*list_n) {
+        g = list_idx[s];
+        n = tiles[g].x;
     }
+    const bool in_phase = n > 0u;
     // phase B: the open tiles' bounding box [ox0, ox1) x [oy0, oy1) (phase A leaves a few tiles open,
     // usually in one corner): every Gaussian's rect is clipped to it first, so most are rejected
     // without a mask walk, and the walks and reservations cover only the clipped rect (the clipped
     // spans are the full ones intersected with the box; the tiles cut off are closed)
     int ox0 = 0, oy0 = 0, ox1 = gx, oy1 = gy;
-    if (PHASE_B) {
+    {
         __shared__ int s_box[4][4];
         int bx0 = gx, by0 = gy, bx1 = 0, by1 = 0;
         for (int i = t; i < (gx * gy + 31) / 32; i += 256) {
@@ -509,13 +477,13 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         ox1 = max(max(s_box[0][2], s_box[1][2]), max(s_box[2][2], s_box[3][2]));
         oy1 = max(max(s_box[0][3], s_box[1][3]), max(s_box[2][3], s_box[3][3]));
     }
-    // phase B, frames up to 128 tiles wide and 256 tall (opts kDupRows): the open tiles also as two
+    // frames up to 128 tiles wide and 256 tall (rows): the open tiles also as two
     // 64-bit words per tile row (s_trow) and one per bin row (s_brow, bit X: bin column X holds an
     // open tile), so a rect's open test is one masked word pair per tile row and the walk visits
     // only the bins holding an open tile
-    const bool rowm = PHASE_B && mask_lds && (opts & kDupRows) && gx <= 128 && gy <= 256;
-    __shared__ uint64_t s_trow[PHASE_B ? 512 : 1];
-    __shared__ uint64_t s_brow[PHASE_B ? 128 : 1];
+    const bool rowm = mask_lds && rows && gx <= 128 && gy <= 256;
+    __shared__ uint64_t s_trow[512];
+    __shared__ uint64_t s_brow[128];
     if (rowm) {  // block-uniform
         const uint32_t nw = (uint32_t)(gx * gy + 31) / 32;
         for (int r = t; r < 2 * gy; r += 256) {
@@ -595,7 +563,7 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
     uint32_t cnt = 0;
     CullEll ell{};
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0, nbins = 0;
-    uint32_t bound = 0;  // phase B: pairs reserved (reserve_n)
+    uint32_t bound = 0;  // the rectangle's open bins (row masks)
     bool live = false;
     if (in_phase) {
         const int r = radii[g];
@@ -603,19 +571,12 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         const float4 Bv = splats[g].b;
         asm volatile("" ::"v"(r), "v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(Bv.x), "v"(Bv.w));
         tile_rect(A.x, A.y, r, gx, gy, x0, y0, x1, y1);
-        if (PHASE_B) clip(x0, y0, x1, y1);
+        clip(x0, y0, x1, y1);
         nbins = (((x1 + 1) >> 1) - (x0 >> 1)) * (((y1 + 1) >> 1) - (y0 >> 1));
-#if defined(RR_DUP_PROBE) && RR_DUP_PROBE == 1  // timing probe only (drops pairs): the big path's cost
-        if (PHASE_B && big_bins > 0 && x0 < x1 && y0 < y1 && nbins > big_bins) {
-        } else
-#elif defined(RR_DUP_PROBE) && RR_DUP_PROBE == 2  // timing probe only: the open-tile tests and walks
-        if (PHASE_B) {
-        } else
-#endif
-        if (PHASE_B && big_bins > 0 && x0 < x1 && y0 < y1 && nbins > big_bins) {
+        if (big_bins > 0 && x0 < x1 && y0 < y1 && nbins > big_bins) {
             s_big[atomicAdd(&s_nbig, 1u)] = g;  // one thread's walk would hold up its workgroup
-        } else if (x0 < x1 && y0 < y1 &&
-                   (!PHASE_B || (rowm ? (bound = open_bins(x0, y0, x1, y1)) > 0u : true) && rect_open(x0, y0, x1, y1))) {
+        } else if (x0 < x1 && y0 < y1 && (rowm ? (bound = open_bins(x0, y0, x1, y1)) > 0u : true) &&
+                   rect_open(x0, y0, x1, y1)) {
             float ccx, ccy, ccz;
             splat_conic(A, Bv, ccx, ccy, ccz);
             ell = cull_setup(A.x, A.y, ccx, ccy, ccz, cull ? cull_qmax(Bv.w) : 0.f);
@@ -625,7 +586,7 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
     // Pair i of the workgroup's reservation (at s_base): with the row masks, the first kStage go
     // through LDS (the flat mask's words, no longer read) and out in coalesced rows — each thread's
     // pairs are contiguous, so direct stores scatter 64 runs per instruction — the rest directly
-    constexpr uint32_t kStage = PHASE_B ? 1024u : 0u;
+    constexpr uint32_t kStage = 1024u;
     uint32_t* const st_val = s_open;
     uint32_t* const st_key = s_open + kStage;
     auto put = [&](uint32_t i, K key, uint32_t val) {
@@ -637,9 +598,8 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
             vals[s_base + i] = val;
         }
     };
-    // the kept pairs, in the duplicate's enumeration (bin rows, then bin columns); phase B: pass 0
-    // counts, pass 1 writes; phase A writes its n pairs (never more: the reservation's bound)
-    auto walk = [&](bool emit, uint32_t pos, uint32_t cap) {
+    // the kept pairs, in the duplicate's enumeration (bin rows, then bin columns), at most cap
+    auto walk = [&](uint32_t pos, uint32_t cap) {
         uint32_t c = 0;
         if (rowm) {  // block-uniform: only the bin columns of each row that hold an open tile
             const uint64_t bm = span_bits(x0 >> 1, (x1 + 1) >> 1, 0);
@@ -653,35 +613,32 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
                     const int X = __builtin_ctzll(cm);
                     const uint32_t m = bin_mask(X, l0, h0, l1, h1) & open4(X, Y);
                     if (!m) continue;
-                    if (emit) put(pos + c, (K)(Y * bgx + X), g | (m << BIN_SHIFT));
+                    put(pos + c, (K)(Y * bgx + X), g | (m << BIN_SHIFT));
                     c++;
                 }
             }
             return c;
         }
         for (int Y = y0 >> 1; Y < (y1 + 1) >> 1 && c < cap; Y++) {
-            // phase B: a bin row whose two tile rows hold no open tile in [x0, x1) emits nothing
-            // (skipped before its culling spans are evaluated)
-            if (PHASE_B && !rect_open(x0, max(2 * Y, y0), x1, min(2 * Y + 2, y1))) continue;
+            // a bin row whose two tile rows hold no open tile in [x0, x1) emits nothing (skipped
+            // before its culling spans are evaluated)
+            if (!rect_open(x0, max(2 * Y, y0), x1, min(2 * Y + 2, y1))) continue;
             int l0, h0, l1, h1, Xa, Xb;
             bin_row_spans(ell, cull, Y, x0, x1, y0, y1, l0, h0, l1, h1);
             bin_cols(l0, h0, l1, h1, Xa, Xb);
             for (int X = Xa; X < Xb && c < cap; X++) {
                 uint32_t m = bin_mask(X, l0, h0, l1, h1);
-                if (PHASE_B) m &= open4(X, Y);
+                m &= open4(X, Y);
                 if (!m) continue;
-                if (emit) put(pos + c, (K)(Y * bgx + X), g | (m << BIN_SHIFT));
+                put(pos + c, (K)(Y * bgx + X), g | (m << BIN_SHIFT));
                 c++;
             }
         }
         return c;
     };
-    // phase B: the kept pairs counted by a first walk, or (reserve_n) an upper bound reserved (the
-    // clipped rect's open bins or bins, or the Gaussian's pair count if fewer and known), the slots the one walk leaves
-    // filled with a key past the last bin (the bin count and scatter skip them): one walk per
-    // Gaussian instead of two
-    if (live)
-        cnt = !PHASE_B ? n : !reserve_n ? walk(false, 0u, 0xffffffffu) : min(n, rowm ? bound : (uint32_t)nbins);
+    // an upper bound on the kept pairs reserved (the pair count, or the clipped rectangle's open
+    // bins or bins if fewer), the slots the one walk leaves filled with a key past the last bin
+    if (live) cnt = min(n, rowm ? bound : (uint32_t)nbins);
     // the workgroup's kept pairs: wave prefix sums, one reservation
     uint32_t incl = cnt;
 #pragma unroll
@@ -702,11 +659,8 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
         __syncthreads();
         if (cnt) {
             const uint32_t pos = pre + incl - cnt;  // in the workgroup's reservation
-            // phase A: the walk and the preprocess's count are the same closed form on the same
-            // record (rr_preprocess.hpp); should they ever disagree, the reserved slots left over get
-            // an empty tile mask, which the per-bin split writes to no tile list
-            const K fill = (PHASE_B && reserve_n) ? (K)(bgx * bins_y(gy)) : (K)0;
-            for (uint32_t c = walk(true, pos, cnt); c < cnt; c++) put(pos + c, fill, g);
+            const K fill = (K)(bgx * bins_y(gy));
+            for (uint32_t c = walk(pos, cnt); c < cnt; c++) put(pos + c, fill, g);
         }
         if (rowm) {  // block-uniform
             __syncthreads();
@@ -716,7 +670,7 @@ __global__ __launch_bounds__(256) void k_dup_gather(int P, const uint2* __restri
             }
         }
     }
-    if constexpr (PHASE_B) {
+    {
         // the large Gaussians: 256 bins of one Gaussian at a time, one per thread (its bin row's
         // spans, mask and open tiles), compacted by ballots, one reservation per round
         const uint32_t nbig = s_nbig;  // read after the barrier above (or the one at the top)
@@ -830,24 +784,17 @@ template bool launch_duplicate<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
 template bool launch_duplicate<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
 
 template <typename K>
-void launch_dup_gather(const DupArgs<K>& d, bool phase_b, hipStream_t st) {
+void launch_dup_gather(const DupArgs<K>& d, hipStream_t st) {
     if (d.P == 0) return;
-    if (!phase_b) {
-        k_dup_gather<K, false><<<blocks_for(d.P), 256, 0, st>>>(d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii,
-                                                                 d.gx, d.gy, d.cull, d.keys, d.vals, nullptr,
-                                                                 d.n_total, nullptr, nullptr, nullptr, 0,
-                                                                 d.idx ? d.n_list : nullptr, d.idx, 0, 0);
-        return;
-    }
     const bool ord = d.order_out && d.order_cost && d.order_flag && d.order_T > 0;
-    k_dup_gather<K, true><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
-        d.P, d.tiles, d.depth_keys, d.ft, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits,
-        d.n_total, ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T,
-        d.idx ? d.n_list : nullptr, d.idx, g_dup_big_bins,
-        (g_dup_b_reserve ? kDupReserve : 0) | (g_dup_b_rows ? kDupRows : 0));
+    const Tuning& tu = tuning();
+    k_dup_gather<K><<<blocks_for(d.P) + (ord ? 1 : 0), 256, 0, st>>>(
+        d.tiles, d.splats, d.radii, d.gx, d.gy, d.cull, d.keys, d.vals, d.open_bits, d.n_total,
+        ord ? d.order_cost : nullptr, ord ? d.order_out : nullptr, d.order_flag, d.order_T, d.n_list, d.idx,
+        tu.dup_big_bins, tu.dup_b_rows ? 1 : 0, d.gather_mark);
 }
-template void launch_dup_gather<uint16_t>(const DupArgs<uint16_t>&, bool, hipStream_t);
-template void launch_dup_gather<uint32_t>(const DupArgs<uint32_t>&, bool, hipStream_t);
+template void launch_dup_gather<uint16_t>(const DupArgs<uint16_t>&, hipStream_t);
+template void launch_dup_gather<uint32_t>(const DupArgs<uint32_t>&, hipStream_t);
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;

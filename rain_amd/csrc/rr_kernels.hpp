@@ -110,7 +110,6 @@ struct BlendFwdArgs {
     int phase;              // BlendPhase
     const float4* normals;  // aux normal output (RR_FLAG_AUX_NORMAL): per-Gaussian normals and
     float* out_normal;      // the blended normal map [3,H,W]; both null otherwise
-    const uint32_t* order;  // [T] tile of each workgroup, longest list first; null: XCD order
     uint32_t* trace;        // RR_FWD_TRACE builds only: per-wave timing records (rr_debug_set_fwd_trace)
     // the backward's accumulator workspace (rr_set_forward_workspace), zero-filled by extra
     // workgroups after the tiles' (dispatched last: they run in the blend's drain); null: none
@@ -192,22 +191,15 @@ void launch_preprocess_views(const PreArgs& a, const PreViews& vs, hipStream_t s
 // The pair-count scan (rasterizer_impl.cu:269; rr_bin.hip launch_split_scan) in blocks of
 // kPairScanItems: per-block totals, then each block scans its items on top of the sum of the earlier
 // totals: up to kPairScanDirectBlocks blocks (P <= 1,048,576) every block sums those totals itself
-// (2 launches), above it one workgroup scans them first (3 launches; rr_set_tuning
-// "pair_scan_direct_blocks" moves the cut-over, tests force both paths).
+// (2 launches), above it one workgroup scans them first (3 launches; Tuning::pair_scan_direct_blocks
+// moves the cut-over, tests force both paths).
 constexpr int kPairScanItems = 2048;                 // items per block (256 threads x 8)
 constexpr int kPairScanDirectBlocks = 512;
-void set_pair_scan_direct_blocks(int nb);
-int pair_scan_direct_blocks();
 // rr_bin.hip: the depth-sort-free binning
-// zero (optional): nzero words cleared by the same launch (the image buffer's per-frame block)
-void launch_early_cut(int P, const uint32_t* keys, const uint2* tiles, const uint2* block_sums,
-                      const uint32_t* block_wide, uint32_t den, uint32_t min_pairs, FrameTotals* ft, void* temp,
-                      uint32_t* box, uint32_t seq, uint32_t* zero, int nzero,
-                      hipStream_t st);  // temp: split_scan_temp_bytes(P)
-// The phases' Gaussian lists (PhaseLists, ft->GA / GB entries); the last thread publishes {LA, rect,
-// seq, wide, LB} to box (may be null) and ft.  temp: split_scan_temp_bytes(P)
+// The phases' Gaussian lists (PhaseLists, ft->GA / GB entries) and, computed by every workgroup of
+// its first launch, the frame's totals and early-stop depth cut (published to the host mailbox);
+// the last thread leaves {LA, LB, GA, GB} in ft.  temp: split_scan_temp_bytes(P)
 size_t split_scan_temp_bytes(int P);
-// The depth cut's inputs when the split scan's first launch computes it (instead of k_early_cut)
 struct CutArgs {
     const uint2* block_sums;
     const uint32_t* block_wide;
@@ -216,28 +208,24 @@ struct CutArgs {
     uint32_t seq;
 };
 void launch_split_scan(const uint2* tiles, const uint32_t* keys, int P, PhaseLists lists, FrameTotals* ft, void* temp,
-                       int direct_blocks, uint32_t* zero, int nzero, hipStream_t st,
-                       const CutArgs* cut = nullptr);  // zero (optional): nzero words cleared by its first launch
+                       int direct_blocks, uint32_t* zero, int nzero, const CutArgs& cut,
+                       hipStream_t st);  // zero (optional): nzero words cleared by its first launch
+// Per bin: the depth order of its run of the bin-sorted pairs and its four tiles' lists (bounds:
+// the bins' runs, from the bin sort's last scatter).  Runs longer than the LDS cap are sorted in
+// their own point_list region and written back over vals.
 template <typename K>
-void launch_sortexpand(uint32_t L, const uint32_t* n_dev, const K* keys, const uint32_t* vals,
-                       const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy, uint32_t out_base,
-                       uint32_t* point_list, uint2* ranges, const uint32_t* open_bits, uint2* bounds,
-                       bool bounds_ready, uint32_t* report,
-                       hipStream_t st);  // bounds: [bins], zero on entry, or filled by the sort (bounds_ready)
-// Runs longer than the LDS cap are sorted in their own point_list region and written back over
-// vals (launch_sortexpand*: vals is overwritten for those runs).
-// Phase B of the gather path (rr_bin.hip k_bin_count + k_bin_scan + k_bin_scatter + k_sortexpand):
-// the densely emitted, unordered phase-B pairs (k_duplicate_b_gather) counted per bin (bin_cnt, zero
-// on entry) and dropped into their bins' runs — no bin sort, no bounds launch.  report:
-// optional host-mapped mailbox; word 5 receives the phase's pair count.  false: more bins than one
-// workgroup scans (nothing launched).
+void launch_sortexpand(const K* keys, const uint32_t* vals, const uint32_t* depth_keys, const FrameTotals* ft, int gx,
+                       int gy, uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
+                       const uint2* bounds, hipStream_t st);
+// Phase B of the gather path (rr_bin.hip k_bin_count + k_bin_scatter + k_sortexpand): the densely
+// emitted, unordered phase-B pairs (k_dup_gather) counted per bin (bin_cnt, zero on entry) and
+// dropped into their bins' runs — no bin sort.  kept: receives the pairs the bins hold.  false:
+// more bins than one workgroup scans (nothing launched).
 template <typename K>
 bool launch_sortexpand_small(int P, const K* keys, const uint32_t* vals, const uint32_t* n_dev, uint32_t* bin_cnt,
                              uint32_t* vals_sorted, const uint32_t* depth_keys, const FrameTotals* ft, int gx, int gy,
                              uint32_t out_base, uint32_t* point_list, uint2* ranges, const uint32_t* open_bits,
-                             uint2* bounds, uint32_t* report, hipStream_t st,
-                             const uint32_t* out_base_dev = nullptr,  // lists at out_base + 4 * *out_base_dev
-                             uint32_t* kept = nullptr);  // receives the pairs the bins hold
+                             uint2* bounds, uint32_t* kept, hipStream_t st);
 template <typename K>
 struct DupArgs {
     int P;                       // capacity of the lists (the frame's Gaussians)
@@ -281,22 +269,19 @@ struct DupArgs {
     const uint32_t* n_list_b;
     const uint32_t* off_b;
     bool starts_done;
-    // the gather path (launch_dup_gather): every Gaussian's {pairs, rect tiles}, depth key, and the
-    // frame's depth cut (FrameTotals::cut) choose the phase's Gaussians; n_total receives the
-    // phase's pair count (zero on entry)
+    // the gather path (launch_dup_gather): every Gaussian's {pairs, rect tiles}; n_total receives
+    // the phase's reserved slots (zero on entry)
     const uint2* tiles;
-    const uint32_t* depth_keys;
-    const FrameTotals* ft;
+    uint32_t* gather_mark;  // set to 1 by the gather path (the frame statistics read which path ran)
 };
 // returns whether the window starts (both sets) were computed
 template <typename K>
 bool launch_duplicate(const DupArgs<K>& d, hipStream_t st);
-// the gather path: one thread per Gaussian of the phase — entry of the split scan's list (d.idx, with
-// d.n_list entries) or, with d.idx null, every Gaussian of the frame (d.P) filtered by the depth cut —
-// the phase's pairs (phase A: every pair; phase B: pairs on open tiles only) written densely and
-// unordered at d.keys / d.vals, their count added to *d.n_total (rr_forward.hip k_dup_gather)
+// phase B by the gather path: one thread per entry of the split scan's phase-B list (d.idx, with
+// d.n_list entries), its pairs on open tiles written densely and unordered at d.keys / d.vals,
+// the slots reserved added to *d.n_total (rr_forward.hip k_dup_gather)
 template <typename K>
-void launch_dup_gather(const DupArgs<K>& d, bool phase_b, hipStream_t st);
+void launch_dup_gather(const DupArgs<K>& d, hipStream_t st);
 void launch_blend_fwd(const BlendFwdArgs& a, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
@@ -330,11 +315,7 @@ hipError_t radix_sort_pairs(void* temp, size_t temp_bytes, const K* keys_in, K* 
 // bounds (optional, [1 << (end_bit - begin_bit)], zero on entry): each key's run in the sorted output,
 // encoded {~start, end} (a key without items keeps {0, 0}; rr_bin.hip k_sortexpand decodes), written by
 // the last pass's scatter
-const char* radix_sort_last_error();
-void set_sort_min_units(int units);  // sort unit-count target (tuning; 0 = default)
-void set_sort_min_units_tile(int units);  // the same for the bin sorts (<= 16-bit keys; default 1024)
-void set_wide_bin_keys(bool on);     // tuning: 32-bit bin keys at any bin count (rr_api.hip)
-void set_sort_max_rounds(int r);     // rounds cap per wave (tuning; 0 = default 16)  // which check failed in the last radix_sort_pairs call
+const char* radix_sort_last_error();  // which check failed in the last radix_sort_pairs call
 // Unit geometry of a sort and where its first-pass digit counts live, so that a producer kernel
 // can emit counts[digit * units + unit] for the lowest dbits0 bits itself (then pass
 // first_counts_ready = true).
@@ -362,20 +343,26 @@ void launch_pack_records(const float* gacc, const int* radii, int P, int Q, int 
 }  // namespace rr
 
 namespace rr {
-// Tuning knob: waves per tile (1, 2, 4) of the blend kernels; 0 = default / env override.
-void set_blend_config(int fwd_waves, int bwd_waves);
-bool bwd_tile_order();  // backward blend dispatches tiles heaviest first (rr_set_tuning "bwd_tile_order")
-bool dup_tile_order();  // the phase-B duplicate computes the backward's tile order (rr_set_tuning "dup_tile_order")
-bool fwd_tile_order();  // forward blends dispatch tiles longest list first (rr_set_tuning "fwd_tile_order")
-int blend_fwd_s_waves(bool phase_b);  // waves per tile of the forward blend ("fwd_s_waves" / "fwd_b_waves")
+// Runtime tuning (include/rain_raster.h rr_set_tuning / rr_set_binning_config): the early-stop
+// split, and knobs that force a product path of larger frames or scenes onto the small frames of
+// the tests (every setting gives the same lists, images and gradients).  One record per HIP device
+// (the device current at the call; rr_api.hip tuning()), so that a process driving several GPUs
+// does not share them across devices.
+constexpr int kMaxDevices = 64;
+struct Tuning {
+    uint32_t early_den = 3;          // early-stop split: phase A holds ~1/early_den of the pairs
+    uint32_t early_min = 1u << 16;   // frames below this many pairs are binned in one phase
+    int pair_scan_direct_blocks = kPairScanDirectBlocks;  // 3-launch pair-count scan above it
+    bool wide_bin_keys = false;      // 32-bit bin keys (frames of > 65536 bins)
+    bool b_gather = true;            // phase B by the gather path (false: the windowed path of > 16384 bins)
+    bool dup_b_rows = true;          // phase-B gather: row masks (false: the flat mask of > 128 tiles wide)
+    int dup_big_bins = 32;           // phase-B gather: Gaussians over this many bins emitted per workgroup
+    bool sx_bucket = true;           // per-bin order by the bucket sort (false: LSD passes only)
+    int sx_lds_cap = 0;              // per-bin runs over this many pairs through the global path (0: LDS cap)
+    int sort_min_units = 128;        // radix sorts: target unit count
+    int sort_min_units_tile = 1024;  // the same for the bin sorts (<= 16-bit keys)
+    int sort_max_rounds = 16;        // cap on 64-item rounds per wave in a sort unit
+};
+Tuning& tuning();  // the current device's
 void set_fwd_trace(void* dev_buf);
-void launch_blend_fwd_s(const BlendFwdArgs& a, int waves, hipStream_t st);
-void launch_tile_order_by_length(int T, const uint2* ranges, uint32_t* order, hipStream_t st);
-int set_tuning(const char* key, int value);  // 0 = ok, 1 = unknown key
-void set_sx_bucket(bool on);  // rr_bin.hip: per-bin bucket sort (default) or LSD passes only
-void set_sx_lds_cap(int cap);  // runs longer than cap (1..2048; other values: the default) take the global path
-void set_sx_b_threads(int n);  // phase B's sort-expand workgroup: 1024 threads (default) or 256
-void set_dup_big_bins(int n);  // rr_forward.hip: phase-B Gaussians over n bins emitted per workgroup (0: none)
-void set_dup_b_reserve(bool on);  // phase-B gather: one walk, the pair count reserved (fill keys skipped)
-void set_dup_b_rows(bool on);     // phase-B gather: open tiles as row masks (frames <= 128 x 256 tiles)
 }  // namespace rr

@@ -321,25 +321,18 @@ struct SortLayout {
     size_t total;
 };
 
-// rounds per wave: full 16 for large inputs, fewer for small ones so that there are >= ~g_min_units
-// units (rr_set_tuning "sort_min_units"; interleaved A/B on the bench step: with 8-bit digits 512
-// beat 1024 by 1.7%; the 3-pass 9-bit depth sort of 1M keys: 0.100 ms/step with 256 (2048-item
-// units), 0.109 with 128 or 512, 0.132 with 1024)
-// With the 8-wave scatter (round 3) the depth sort prefers its largest units: 128 (4096-item
-// units, 245 for 1M keys) 0.086 vs 0.088 ms/step with 256 and 0.102 with 512; the bin sorts keep
-// 1024 (512: 0.090 / 2048: 0.093 duplicate vs 0.086), profiles/r03_sort_units_ab.jsonl
-constexpr int kMinUnitsDefault = 128;
-// Sorts of <= 16-bit keys (the bin sorts) target more, smaller units: their first pass's units are
-// the duplicate's windows, whose workgroups are latency-bound (interleaved A/B on the bench step:
-// duplicate 0.098 -> 0.092, bin sort 0.087 -> 0.077 ms/step with 1024; the depth sort keeps
-// kMinUnitsDefault (128 since the 8-wave scatter; 0.109 vs 0.129 ms with 1024 back at 256))
-constexpr int kMinUnitsTileDefault = 1024;
-int g_min_units = kMinUnitsDefault;
-int g_min_units_tile = kMinUnitsTileDefault;
-int g_max_rounds = kMaxRounds;  // rr_set_tuning "sort_max_rounds" (power of two <= 16)
+// rounds per wave: full 16 for large inputs, fewer for small ones so that there are >= ~min_units
+// units (Tuning::sort_min_units, default 128; interleaved A/B on the bench step: with 8-bit digits
+// 512 beat 1024 by 1.7%; with the 8-wave scatter (round 3) the 3-pass depth sort of 1M keys
+// preferred its largest units: 128 (4096-item units) 0.086 vs 0.088 ms/step with 256 and 0.102
+// with 512, profiles/r03_sort_units_ab.jsonl).  Sorts of <= 16-bit keys (the bin sorts) target
+// more, smaller units (Tuning::sort_min_units_tile, default 1024): their first pass's units are the
+// duplicate's windows, whose workgroups are latency-bound (duplicate 0.098 -> 0.092, bin sort 0.087
+// -> 0.077 ms/step with 1024).  Tuning::sort_max_rounds caps the rounds (tests: 2048-item units).
 int rounds_for(size_t n, int bits) {
-    const size_t mu = (size_t)(bits <= 16 ? g_min_units_tile : g_min_units);
-    int r = g_max_rounds;
+    const Tuning& tu = tuning();
+    const size_t mu = (size_t)(bits <= 16 ? tu.sort_min_units_tile : tu.sort_min_units);
+    int r = std::min(tu.sort_max_rounds, kMaxRounds);
     while (r > 1 && (n + (size_t)64 * kWaves * r - 1) / ((size_t)64 * kWaves * r) < mu) r >>= 1;
     return r;
 }
@@ -391,10 +384,6 @@ RadixPlan radix_sort_plan(void* temp, size_t n, int begin_bit, int end_bit, size
     p.counts = s.counts;
     return p;
 }
-
-void set_sort_min_units(int units) { g_min_units = units > 0 ? units : kMinUnitsDefault; }
-void set_sort_min_units_tile(int units) { g_min_units_tile = units > 0 ? units : kMinUnitsTileDefault; }
-void set_sort_max_rounds(int r) { g_max_rounds = (r == 1 || r == 2 || r == 4 || r == 8) ? r : kMaxRounds; }
 
 thread_local const char* g_why = "";
 const char* radix_sort_last_error() { return g_why; }

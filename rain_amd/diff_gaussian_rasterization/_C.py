@@ -233,4 +233,5 @@ def frame_stats(geomBuffer, imageBuffer, P, W, H):
     N.check(N.raster().rr_read_frame_stats(ctypes.byref(f), _ptr(geomBuffer), _ptr(imageBuffer), ctypes.byref(st),
                                            N.stream_of(geomBuffer)), "frame_stats")
     return dict(num_rendered=st.num_rendered, num_visible=st.num_visible, l_eff=st.l_eff, tiles=st.tiles,
-                num_pairs=st.num_pairs, num_binned=st.num_binned)
+                num_pairs=st.num_pairs, num_binned=st.num_binned, phase_b_pairs=st.phase_b_pairs,
+                phase_b_slots=st.phase_b_slots)

@@ -296,21 +296,30 @@ class RasterizeRawParams(torch.autograd.Function):
                                                  tanfovx, tanfovy, viewmatrix, projmatrix, campos, bg, low_pass,
                                                  scale_modifier)
         # the parameters as saved tensors (the reference saves its inputs, __init__.py:85-87): autograd's
-        # version check then rejects a backward after they were modified in place
-        ctx.save_for_backward(xyz, f_dc, f_rest, opacity, scaling, rotation)
-        ctx.st = st  # scratch buffers: held until the graph is freed (a retained graph's second backward)
+        # version check then rejects a backward after they were modified in place.  The scratch
+        # buffers and camera tensors are saved too, so that autograd frees them after a backward
+        # that does not retain the graph; ctx keeps only the descriptors (plain structs).
+        keep, _p6 = st.keep
+        ctx.save_for_backward(xyz, f_dc, f_rest, opacity, scaling, rotation, st.radii, st.geom, st.img, st.binning,
+                              st.ws, *keep)
+        ctx.desc = (st.frame, st.cam, st.gs, st.num_rendered, st.P, st.M)
         ctx.mark_non_differentiable(radii, depth)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for radii / depth (two fills)
         return color, radii, depth
 
     @staticmethod
     def backward(ctx, grad_color, _grad_radii, _grad_depth):
-        ctx.saved_tensors  # noqa: B018 — raises if a parameter changed in place since the forward
-        st = ctx.st
+        # (raises if a parameter changed in place since the forward)
+        xyz, f_dc, f_rest, opacity, scaling, rotation, radii, geom, img, binning, ws, *keep = ctx.saved_tensors
+        frame, cam, gs, num_rendered, P, M = ctx.desc
+        p = (xyz, f_dc, opacity, scaling, rotation, f_rest)  # kernel order
+        # the zero-filled workspace serves the first backward only (a retained graph's second one
+        # allocates and clears its own)
+        ws_first = ws if not getattr(ctx, "ws_used", False) else None
+        ctx.ws_used = True
+        st = RawFrame(frame, cam, gs, (tuple(keep), p), radii, geom, img, binning, num_rendered, P, M, ws_first)
         if grad_color is None:  # the image unused by the loss (materialize_grads off)
-            grad_color = torch.zeros((3, st.frame.height, st.frame.width), dtype=torch.float32,
-                                     device=st.keep[1][0].device)
-        _keep, p = st.keep  # kernel order: xyz, f_dc, opacity, scaling, rotation, f_rest
+            grad_color = torch.zeros((3, frame.height, frame.width), dtype=torch.float32, device=xyz.device)
         grads = dict(xyz=torch.empty_like(p[0]), f_dc=torch.empty_like(p[1]), opacity=torch.empty_like(p[2]),
                      scaling=torch.empty_like(p[3]), rotation=torch.empty_like(p[4]), f_rest=torch.empty_like(p[5]))
         d2 = torch.empty((st.P, 3), dtype=torch.float32, device=p[0].device)

@@ -112,61 +112,6 @@ def l1_ssim_forward_backward(img, gt, lambda_dssim, grad_loss=None):
     return loss, parts, dimg
 
 
-class OverlappedLoss:
-    """l1_ssim_forward_backward of a frame rendered with early-stop binning, split around its phase B
-    (include/rain_loss.h rl_l1_ssim_forward_backward_part, include/rain_raster.h
-    rr_set_phase_a_event): the bands whose rows phase A finished run on a side stream as soon as the
-    render's phase-A event fires — concurrently with phase B, which leaves most of the GPU idle —
-    and the rest on the current stream after the render.  The result is bitwise
-    l1_ssim_forward_backward's.  The buffers are reused from step to step (the side stream's first
-    write of step s+1 follows step s's last read in stream order: it waits for step s+1's render)."""
-
-    def __init__(self, device):
-        from . import _native as N
-
-        self.device = device
-        self.side = torch.cuda.Stream(device=device)
-        self._bufs = None
-        N.check(N.raster().rr_set_phase_a_event(1), "rr_set_phase_a_event")
-
-    def _buffers(self, img):
-        from . import _native as N
-
-        C, H, W = img.shape[-3:]
-        if self._bufs is None or self._bufs[0] != (C, H, W):
-            ws = torch.empty((N.loss_lib().rl_workspace_bytes(C, H, W),), dtype=torch.uint8, device=img.device)
-            self._bufs = ((C, H, W), ws, torch.empty((), dtype=torch.float32, device=img.device),
-                          torch.empty((3,), dtype=torch.float32, device=img.device), torch.empty_like(img),
-                          _ones(img.device).reshape(1).contiguous().float())
-        return self._bufs
-
-    def __call__(self, img, gt, lambda_dssim, frame, image_buffer):
-        """(loss, parts, dimg) of the frame just rendered into image_buffer (RawFrame.frame / .img)."""
-        from . import _native as N
-
-        L, R = N.loss_lib(), N.raster()
-        img = img.contiguous()
-        gt = gt.contiguous()
-        C, H, W = img.shape[-3:]
-        _shape, ws, loss, parts, dimg, g = self._buffers(img)
-        bits, tx, ty = ctypes.c_void_p(), ctypes.c_int(0), ctypes.c_int(0)
-        N.check(R.rr_frame_open_tiles(ctypes.byref(frame), image_buffer.data_ptr(), ctypes.byref(bits),
-                                      ctypes.byref(tx), ctypes.byref(ty)), "rr_frame_open_tiles")
-        main = torch.cuda.current_stream(img.device)
-        args = (img.data_ptr(), gt.data_ptr(), C, H, W, float(lambda_dssim), _window_host(), ws.data_ptr(), ws.numel(),
-                loss.data_ptr(), parts.data_ptr(), g.data_ptr(), dimg.data_ptr(), bits.value, tx.value, ty.value)
-        rc = L.rl_l1_ssim_forward_backward_part(*args, 1, R.rr_phase_a_event(), ctypes.c_void_p(self.side.cuda_stream))
-        if rc:
-            raise RuntimeError(L.rl_last_error().decode())
-        done = torch.cuda.Event()
-        done.record(self.side)
-        main.wait_event(done)
-        rc = L.rl_l1_ssim_forward_backward_part(*args, 2, None, N.stream_of(img))
-        if rc:
-            raise RuntimeError(L.rl_last_error().decode())
-        return loss, parts, dimg
-
-
 class _FusedL1SSIM(torch.autograd.Function):
     """(1-λ)·L1 + λ·(1-SSIM) in two HIP kernels (rain_amd/csrc/loss.hip, include/rain_loss.h)."""
 

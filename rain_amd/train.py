@@ -223,14 +223,6 @@ class Trainer:
         # (replaced tensors, or in-place edits such as a manual reset or a checkpoint restore: the
         # tensors' version counters), and step s+1 then preprocesses normally.
         self.fuse_next = True
-        # fused step, single GPU: the loss of the image rows early-stop phase A finished on a side
-        # stream while phase B renders the rest (rain_amd.loss.OverlappedLoss; bitwise the same loss
-        # and gradient).  Off by default: measured slower on the bench step, 1.0883 / 1.0876 vs
-        # 1.0614 / 1.0595 ms — the SSIM blocks crowd out phase B's latency-bound chain (its
-        # duplicate stage 0.073 -> 0.116 ms), which is the step's critical path
-        # (profiles/r05_overlap_loss_ab.jsonl)
-        self.overlap_loss = False
-        self._ov_loss = None
         self._pending = None  # (iteration, view index, camera, low_pass, NextFrame or None, params signature)
         self._shard = None
         # the fused step on N > 1 ranks (or a forced exchange): Gaussian-sharded, view-parallel
@@ -428,15 +420,8 @@ class Trainer:
                 image, radii, _depth, st = fused.forward_next(nxt, g, cache=cache)
             else:
                 image, radii, _depth, st = fused.forward(g, cam, self.background, self.low_pass, cache=cache)
-            # loss and dL/dimage in one call (bitwise the separate forward / backward), or in two
-            # parts around the render's phase B
-            if self.overlap_loss:
-                if self._ov_loss is None:
-                    from .loss import OverlappedLoss
-                    self._ov_loss = OverlappedLoss(image.device)
-                loss, _parts, dimg = self._ov_loss(image, gt, opt.lambda_dssim, st.frame, st.img)
-            else:
-                loss, _parts, dimg = l1_ssim_forward_backward(image, gt, opt.lambda_dssim)
+            # loss and dL/dimage in one call (bitwise the separate forward / backward)
+            loss, _parts, dimg = l1_ssim_forward_backward(image, gt, opt.lambda_dssim)
             fused.backward(st, dimg, grads, stats, adam=adam, next_frame=next_frame)
             densified = self._finish(iteration, flat, densify_now, reset_now, adam_done=fuse_adam)
         if self._pending is not None:  # the parameters the pending geometry was computed from

@@ -1,10 +1,10 @@
-"""Every binning path of the forward (rr_api.hip render_tiles; include/rain_raster.h rr_set_tuning)
-gives the reference's per-tile lists: phase A by the windowed duplicate + bin sort (default) or by
-the gather paths (every Gaussian / the split scan's list); phase B by the gather path over its list
-(default), over every Gaussian, or by the windowed path; per-bin order by the bucket sort (default)
-or by the LSD passes only; bin runs from the bin sort's last scatter (default) or a bounds launch;
-the windowed duplicate's window starts from the split scan's marks or from their own launch; long
-runs depth-sorted in LDS or through their own output region (sx_lds_cap).
+"""Every binning path of the forward (rr_api.hip render_tiles) gives the reference's per-tile
+lists: phase A by the windowed duplicate + bin sort; phase B by the gather path over its list
+(default) or by the windowed path (frames of > 16384 bins); per-bin order by the bucket sort
+(default) or by the LSD passes only; the phase-B gather's row masks or flat mask (frames over 128
+tiles wide), its big-Gaussian workgroup path; windows of 2048 pairs with their starts marked by the
+split scan; long runs depth-sorted in LDS or through their own output region (sx_lds_cap).  Each
+path is forced onto a small frame by its tuning knob (include/rain_raster.h rr_set_tuning).
 
 For each path: the exact (depth, index) lists of the reference's 64-bit-key sort with culling and
 early stop off (tests/test_parity_gpu.py::_check_pair_order, against the oracle), the two-phase
@@ -23,30 +23,17 @@ pytestmark = pytest.mark.gpu
 PATHS = {
     "default": {},
     "lsd_only": {"sx_bucket": (0, 1)},
-    "gather_a_all": {"phase_a_gather": (1, 0), "phase_b_gather": (2, 1)},
-    "gather_a_list": {"phase_a_gather": (2, 0)},
-    "gather_a_list_lsd": {"phase_a_gather": (2, 0), "sx_bucket": (0, 1)},
-    "count_a": {"phase_a_gather": (3, 0)},  # windowed duplicate, count / scatter bin sort
-    "count_a_global_runs": {"phase_a_gather": (3, 0), "sx_lds_cap": (64, 0)},
     "windowed_b": {"phase_b_gather": (0, 1)},
-    "bin_bounds_launch": {"bounds_in_sort": (0, 1)},
     # units of kSplitWin (2048) pairs at these sizes: window starts from the split scan's marks
     "split_marks": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16)},
     "split_marks_windowed_b": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16),
                                "phase_b_gather": (0, 1)},
     # runs over 64 pairs through the global path (their own point_list region as scratch)
     "global_runs": {"sx_lds_cap": (64, 0)},
-    "global_runs_gather_a": {"sx_lds_cap": (64, 0), "phase_a_gather": (2, 0)},
     "global_runs_windowed_b": {"sx_lds_cap": (64, 0), "phase_b_gather": (0, 1), "sx_bucket": (0, 1)},
-    "cut_kernel": {"cut_in_scan": (0, 1)},  # the depth cut by its own one-workgroup launch
     "dup_big_serial": {"dup_big_bins": (0, 32)},  # every phase-B Gaussian by its own thread
-    "dup_b_count_walk": {"dup_b_reserve": (0, 1)},  # phase B counts its kept pairs first
     "dup_b_flat_mask": {"dup_b_rows": (0, 1)},  # phase B tests the flat open-tile mask (wide frames' path)
-    "sx_b_256": {"sx_b_threads": (256, 1024)},  # phase B's sort-expand in 256-thread workgroups
-    "global_runs_b1024": {"sx_lds_cap": (64, 0), "sx_b_threads": (1024, 1024)},
     "dup_big_all": {"dup_big_bins": (1, 32)},  # every phase-B Gaussian of > 1 bin per workgroup
-    "window_starts_launch": {"sort_min_units_tile": (1, 1024), "sort_max_rounds": (8, 16),
-                             "phase_b_gather": (0, 1), "split_marks": (0, 1)},
 }
 
 @pytest.fixture(params=list(PATHS))

@@ -142,3 +142,59 @@ def test_two_phase_equal_depths(gpu, split, monkeypatch, copies):
     assert s["num_binned"] > s["num_pairs"] // 4, s  # phase B binned pairs
     np.testing.assert_array_equal(early["color"], full["color"])
     np.testing.assert_array_equal(early["depth"], full["depth"])
+
+
+def test_phase_b_reservation_stays_in_its_region(gpu, split):
+    """Phase B's gather duplicate reserves slots per Gaussian (rr_forward.hip k_dup_gather): on a
+    frame where phase A closes no tile (faint Gaussians) and the Gaussians are elongated (their
+    bounding rectangles hold many bins their ellipses never reach), the reservations must stay
+    within the phase's pairs, the size of its region of the pair arrays — and the outputs equal
+    full binning's."""
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    inp, st = make_scene(P=4000, W=256, H=192, sh_degree=1, scale_mult=1.0)
+    P = inp["means3D"].shape[0]
+    g = torch.Generator().manual_seed(11)
+    sc = inp["scales"]
+    sc[:, 0] = sc[:, 0] * 12.0  # long thin ellipses at random orientations
+    sc[:, 1:] = sc[:, 1:] * 0.3
+    inp["opacities"] = torch.full_like(inp["opacities"], 0.02)
+    q = torch.randn(P, 4, generator=g)
+    inp["rotations"] = (q / q.norm(dim=1, keepdim=True)).to(inp["rotations"].dtype)
+    from unittest import mock
+
+    with mock.patch.object(_C, "EARLY_STOP", False):
+        full = gpu_run(inp, st, gpu)
+    split(3)
+    early = gpu_run(inp, st, gpu)
+    s = _stats(early, P, st)
+    assert s["phase_b_pairs"] > 0, s
+    assert s["phase_b_slots"] <= s["phase_b_pairs"], s
+    assert s["num_binned"] == s["num_pairs"], s  # nothing saturated: every pair binned
+    np.testing.assert_array_equal(early["color"], full["color"])
+    np.testing.assert_array_equal(early["depth"], full["depth"])
+
+
+def test_second_render_without_a_pair_count_fails(gpu):
+    """One render per pair count (rr_api.hip g_counted_img): rendering a frame again from the same
+    geometry call would start the gather counters where the first render's ended."""
+    import ctypes
+
+    from rain_amd import _native as N
+    from rain_amd.diff_gaussian_rasterization import _C
+
+    inp, st = make_scene(P=2000, W=128, H=96, sh_degree=3)
+    out = gpu_run(inp, st, gpu)
+    geom, binning, img = out["buffers"]
+    L = N.raster()
+    f = _C._frame(2000, 3, 16, st["image_width"], st["image_height"], 1.0, 1.0, 1.0, 0.3, False, False)
+    # non-null stand-ins pass the argument checks; the render fails at the pair-count guard, before
+    # any launch reads them
+    x = geom.data_ptr()
+    cam = N.RRCamera(x, x, x, x)
+    g = N.RRGaussians(x, x, None, x, x, x, None, None)
+    color = torch.empty(3, st["image_height"], st["image_width"], device=gpu)
+    rc = L.rr_forward_render(ctypes.byref(f), ctypes.byref(cam), ctypes.byref(g), x, geom.data_ptr(),
+                             img.data_ptr(), binning.data_ptr(), binning.numel(), out["num_rendered"],
+                             color.data_ptr(), color.data_ptr(), None)
+    assert rc == 1 and b"pair count" in L.rr_last_error()

@@ -335,78 +335,6 @@ def test_trainer_next_frame_fusion_matches_unfused(gpu):
     assert torch.equal(ga.max_radii2D, gb.max_radii2D)
 
 
-@pytest.mark.parametrize("min_pairs", [1, 0])
-def test_trainer_overlapped_loss_is_bitwise(gpu, min_pairs):
-    """Trainer.overlap_loss (the loss of the rows early-stop phase A finished runs on a side stream
-    during phase B: rain_amd.loss.OverlappedLoss) against the loss after the whole render, over a
-    run with a densify event: every frame two-phase (min_pairs 1) and the default threshold (these
-    small frames then render in one phase: the event fires after the whole render)."""
-    from rain_amd import _native as N
-
-    P, W, H, V = 20_000, 160, 120, 6
-    cams = [c.to("cuda") for c in cameras.fibonacci_cameras(V, W, H)]
-    gts = [torch.rand(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(40 + i))
-           for i in range(V)]
-    res = []
-    N.check(N.raster().rr_set_binning_config(3, min_pairs), "binning config")
-    try:
-        for overlap in (False, True):
-            g = _model(P, 3, 1, seed=5)
-            opt = OptimizationParams(densify_from_iter=2, densification_interval=5, opacity_reset_interval=8)
-            g.training_setup(opt)
-            t = Trainer(g, cams, gts, opt, cfg=TrainConfig(c2f=True, seed=3), scene_extent=4.4, fused=True)
-            t.overlap_loss = overlap
-            losses = [t.step(it, sync_loss=True).loss for it in range(995, 1006)]
-            res.append((g, losses))
-    finally:
-        N.check(N.raster().rr_set_binning_config(0, 0), "binning config")
-    (ga, la), (gb, lb) = res
-    # (two runs of the step differ in float rounding anyway: the blend backward's gradient atomics
-    # sum in arrival order — the per-frame bitwise check is test_overlapped_loss_of_a_render_is_bitwise)
-    for x, y in zip(la, lb):
-        assert abs(x - y) <= 1e-5 * abs(y)
-    assert ga.get_xyz.shape == gb.get_xyz.shape
-    for k, x in _params(ga).items():
-        y = _params(gb)[k]
-        assert rel_l1(x.detach(), y.detach()) < 1e-5, (k, rel_l1(x.detach(), y.detach()))
-
-
-def test_overlapped_loss_of_a_render_is_bitwise(gpu):
-    """OverlappedLoss right after a two-phase render (part 1 on the side stream as soon as the
-    render's phase-A event fires, i.e. while phase B still renders the open tiles) gives bitwise the
-    loss, parts and dimg of l1_ssim_forward_backward over the finished image, frame after frame."""
-    from rain_amd import _native as N
-    from rain_amd.loss import OverlappedLoss, l1_ssim_forward_backward
-
-    P, W, H, V = 150_000, 640, 480, 4
-    cams = [c.to("cuda") for c in cameras.fibonacci_cameras(V, W, H)]
-    bg = torch.zeros(3, device="cuda")
-    g = _model(P, 3, 3, seed=8)
-    ov = OverlappedLoss(torch.device("cuda"))
-    N.check(N.raster().rr_set_binning_config(3, 1), "binning config")
-    try:
-        opened = 0
-        for it in range(2 * V):
-            gt = torch.rand(3, H, W, device="cuda", generator=torch.Generator("cuda").manual_seed(60 + it))
-            color, _r, _d, st = fused.forward(g, cams[it % V], bg, 0.3)
-            loss, parts, dimg = ov(color, gt, 0.2, st.frame, st.img)
-            loss, parts, dimg = loss.clone(), parts.clone(), dimg.clone()
-            torch.cuda.synchronize()
-            ref = l1_ssim_forward_backward(color, gt, 0.2)
-            assert torch.equal(loss, ref[0]) and torch.equal(parts, ref[1]), it
-            assert torch.equal(dimg, ref[2]), it
-            # the frame's open tiles (phase B had work): its open-tile mask in the image buffer
-            bits, tx, ty = ctypes.c_void_p(), ctypes.c_int(0), ctypes.c_int(0)
-            N.check(N.raster().rr_frame_open_tiles(ctypes.byref(st.frame), st.img.data_ptr(), ctypes.byref(bits),
-                                                   ctypes.byref(tx), ctypes.byref(ty)), "open tiles")
-            off = bits.value - st.img.data_ptr()
-            nw = (tx.value * ty.value + 31) // 32
-            opened += int(st.img[off:off + 4 * nw].view(torch.int32).ne(0).any())
-        assert opened > 0  # at least one frame rendered a phase B concurrently with part 1
-    finally:
-        N.check(N.raster().rr_set_binning_config(0, 0), "binning config")
-
-
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_adam_equals_full_step(world):
     """rain_amd.optim.sharded_adam_step over every rank's slice (run here one after another in one

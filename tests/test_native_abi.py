@@ -101,8 +101,6 @@ def test_validation_errors_without_gpu():
     rc = L.rr_forward_geometry(ctypes.byref(f), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
                                ctypes.byref(nr), ctypes.byref(nr), None)
     assert rc == 1 and b"exactly one of either SHs" in L.rr_last_error().replace(b"excatly", b"exactly")
-    assert L.rr_set_blend_config(3, 1) == 1
-    assert L.rr_set_blend_config(0, 0) == 0
     # P == 0 is a no-op success (rasterize_points.cu:72)
     f0 = N.RRFrame(0, 0, 0, 64, 48, 0.5, 0.4, 1.0, 0.3, 0, 0)
     assert L.rr_forward_geometry(ctypes.byref(f0), ctypes.byref(cam), ctypes.byref(g), None, None, 0, None, 0,
@@ -111,13 +109,17 @@ def test_validation_errors_without_gpu():
 
 def test_forward_workspace_registration_validation():
     """rr_set_forward_workspace (no device call): 16-B alignment and size, NULL drops it; the
-    tuning keys of round 5 exist."""
+    tuning keys exist, and a removed A/B key is refused."""
     L = N.raster()
     assert L.rr_set_forward_workspace(8, 64) == 1 and b"16-byte" in L.rr_last_error()
     assert L.rr_set_forward_workspace(16, 40) == 1
     assert L.rr_set_forward_workspace(None, 0) == 0
-    for key, dflt in (("split_marks", 1), ("sx_lds_cap", 0), ("forward_clear", 1), ("cut_in_scan", 1)):
+    for key, dflt in (("sx_lds_cap", 0), ("phase_b_gather", 1), ("dup_b_rows", 1), ("dup_big_bins", 32),
+                      ("sx_bucket", 1), ("wide_bin_keys", 0), ("pair_scan_direct_blocks", -1),
+                      ("sort_min_units", 0), ("sort_min_units_tile", 0), ("sort_max_rounds", 0), ("early_den", 0)):
         assert L.rr_set_tuning(key.encode(), dflt) == 0, key
+    for key in ("phase_a_gather", "cut_in_scan", "forward_clear", "bwd_waves"):
+        assert L.rr_set_tuning(key.encode(), 0) == 1 and b"unknown tuning key" in L.rr_last_error()
     assert N.RR_FLAG_WORKSPACE_REGISTERED == 16
 
 

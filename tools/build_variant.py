@@ -4,6 +4,7 @@ gpurun_variants/<name>.so (git-ignored; travels to the GPU box with the snapshot
 
     python tools/build_variant.py nostage -DRR_STAGE_SH=0
     python tools/build_variant.py prev --rev HEAD      (the sources of a git revision)
+    python tools/build_variant.py probe --src DIR -DX  (sources from DIR/rain_amd/csrc, DIR/include)
 """
 import os
 import subprocess
@@ -26,6 +27,9 @@ def main():
         arc = subprocess.run(["git", "-C", ROOT, "archive", rev, "rain_amd/csrc", "include"],
                              capture_output=True, check=True).stdout
         subprocess.run(["tar", "-x", "-C", tmp], input=arc, check=True)
+        csrc, inc = os.path.join(tmp, "rain_amd", "csrc"), os.path.join(tmp, "include")
+    elif flags[:1] == ["--src"]:
+        tmp, flags = flags[1], flags[2:]
         csrc, inc = os.path.join(tmp, "rain_amd", "csrc"), os.path.join(tmp, "include")
     pre = ["-I", inc, "-I", csrc] if csrc != B.CSRC else []  # ahead of the tree's own include dirs
     out = os.path.join(ROOT, "gpurun_variants")

@@ -23,17 +23,11 @@ def main():
     ap.add_argument("--api", action="store_true", help="also time the reference-API step (Trainer(fused=False))")
     ap.add_argument("--pack", action="store_true", help="parameters and moments in three flat buffers (pack_flat_state)")
     ap.add_argument("--tune", action="append", default=[], help="rr_set_tuning key=value (repeatable)")
-    ap.add_argument("--overlap-loss", action="store_true",
-                    help="the loss of phase A's rows on a side stream during phase B (Trainer.overlap_loss)")
     ap.add_argument("--no-fuse-next", action="store_true",
                     help="the next frame's preprocess as its own launch (Trainer.fuse_next = False)")
     ap.add_argument("--skew-state", type=int, default=0,
                     help="re-place each Adam moment at an offset of this many KiB (+ 1/2 MiB steps) from "
                          "its parameter's alignment (HBM channel-placement probe)")
-    ap.add_argument("--ssim-band", type=int, default=0,
-                    help="rl_l1_ssim_forward_backward as one band walk of this many rows (rl_set_fused_band)")
-    ap.add_argument("--loss-split", action="store_true",
-                    help="the trainer's loss as two calls (forward, backward) instead of rl_l1_ssim_forward_backward")
     a = ap.parse_args()
     import torch
 
@@ -43,16 +37,6 @@ def main():
     from rain_amd.renderer import PipelineParams, render
     from rain_amd.train import TrainConfig, Trainer
 
-    if a.loss_split:
-        import rain_amd.loss as RL
-
-        def split(img, gt, lam, grad_loss=None):
-            loss, parts, ws = RL.l1_ssim_forward(img, gt, lam)
-            return loss, parts, RL.l1_ssim_backward(img, gt, lam, ws, grad_loss)
-
-        RL.l1_ssim_forward_backward = split
-    if a.ssim_band:
-        _native.check(_native.loss_lib().rl_set_fused_band(a.ssim_band), "rl_set_fused_band")
     for kv in a.tune:
         k, v = kv.split("=")
         _native.check(_native.raster().rr_set_tuning(k.encode(), int(v)), "rr_set_tuning " + kv)
@@ -75,8 +59,6 @@ def main():
     tr = Trainer(g, cams, gts, opt, PipelineParams(), TrainConfig(seed=0), scene_extent=4.4)
     if a.no_fuse_next:
         tr.fuse_next = False
-    if a.overlap_loss:
-        tr.overlap_loss = True
     if a.pack:
         g.optimizer.fused_step(g)  # creates the moment state the packing moves
         g.pack_flat_state(1)
