@@ -111,7 +111,20 @@ __device__ __forceinline__ void put(float* grad, size_t e, float g) {
 // stores, so that the lines leave the XCD's L2 instead of staying dirty until the kernel-end
 // write-back, the kernel took 0.66 vs 0.37 ms: profiles/r05_gauss_bwd_variants_ab.jsonl.)
 __device__ __forceinline__ void st_state(float* p, float v) { *p = v; }
-__device__ __forceinline__ void st_state4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+// The SH groups' Adam stream (59 % of the kernel's bytes, each read once and written once) goes
+// through non-temporal loads and stores: its lines no longer displace what the caches hold for
+// the rest of the step, and the kernel runs 0.369 -> 0.326 ms with batches of one float4 per
+// array (0.346 at two), step 1.0406 -> 0.9847 ms; non-temporal loads of the coefficient staging
+// or of the small groups' state measured slower (profiles/r06f_gauss_bwd_nt_ab.jsonl).
+typedef float nt4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_ld4(const float* p) {
+    const nt4f v = __builtin_nontemporal_load(reinterpret_cast<const nt4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_state4(float* p, float4 v) {
+    const nt4f w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<nt4f*>(p));
+}
 
 // Adam over n elements whose (param, moment) addresses are given: all loads first, then the
 // math, then the stores (the compiler cannot batch them itself: the arrays may alias).
@@ -513,7 +526,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_views(GaussBwdViewsArgs va) {
 template <int DEG, bool MULTI, int KGB>
 __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const GaussBwdViewsArgs* va, float* s_sh,
                                                 float* s_gr) {
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int t = threadIdx.x, lane = t & 63;
     const int i0 = blockIdx.x * KGB;
     const int nvalid = min(KGB, a.P - i0);
     const int M = a.M, nf = 3 * M;  // floats per Gaussian
@@ -620,7 +633,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                                               a.adam.beta2, a.adam.eps)
                                 : AdamC{};
 #ifndef RR_GB_ADAM_BATCH
-#define RR_GB_ADAM_BATCH 8
+#define RR_GB_ADAM_BATCH 4
 #endif
             constexpr int kB = RR_GB_ADAM_BATCH;  // Adam elements per batch of loads
             auto grad_at = [&](int e) {
@@ -651,14 +664,9 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const Gau
                         const int i = min(v0 + q * KGB, nv - 1);  // clamped duplicates are not stored
                         g4[q] = make_float4(grad_at(4 * i), grad_at(4 * i + 1), grad_at(4 * i + 2), grad_at(4 * i + 3));
                         if (grp) {
-#ifdef RR_GB_TIMING_NO_PARAM_LOAD  // timing experiment only (wrong values): the parameter re-read
-                                   // (the LDS rows hold gradients by now) costs <= 5 us per step
-                            p4[q] = g4[q];
-#else
-                            p4[q] = reinterpret_cast<const float4*>(grp->param + gb)[i];
-#endif
-                            m4[q] = reinterpret_cast<const float4*>(grp->exp_avg + gb)[i];
-                            s4[q] = reinterpret_cast<const float4*>(grp->exp_avg_sq + gb)[i];
+                            p4[q] = nt_ld4(grp->param + gb + 4 * (size_t)i);
+                            m4[q] = nt_ld4(grp->exp_avg + gb + 4 * (size_t)i);
+                            s4[q] = nt_ld4(grp->exp_avg_sq + gb + 4 * (size_t)i);
                         }
                     }
 #pragma unroll

@@ -46,6 +46,19 @@ struct AdamArgs {
     float grad_scale;  // applied to every gradient element first (1/N for an N-rank gradient sum)
 };
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+// Non-temporal 16-B accesses: every element is read once and written once per step, and the
+// stream would otherwise displace the caches' contents for the rest of the step (the same choice
+// as the fused step's SH stream, rr_backward.hip st_state4).
+__device__ __forceinline__ float4 nt_ld4(const float* p) {
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_st4(float* p, float4 v) {
+    const v4f w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<v4f*>(p));
+}
+
 __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
     const int b = blockIdx.x;
     int gi = 0;
@@ -57,20 +70,20 @@ __global__ __launch_bounds__(kThreads) void k_adam(AdamArgs a) {
     if (e0 >= G.n) return;
     const AdamC c = adam_consts(G.lr, G.bc1, G.bc2s, a.beta1, a.beta2, a.eps);
     if (G.vec && e0 + kPerThread <= G.n) {
-        float4 p = *reinterpret_cast<const float4*>(G.p + e0);
-        float4 g = *reinterpret_cast<const float4*>(G.g + e0);
+        float4 p = nt_ld4(G.p + e0);
+        float4 g = nt_ld4(G.g + e0);
         // rounded product (no fma contraction into the update): bitwise torch's grad.mul_(scale) + step
         g.x = mul_rounded(g.x, a.grad_scale); g.y = mul_rounded(g.y, a.grad_scale);
         g.z = mul_rounded(g.z, a.grad_scale); g.w = mul_rounded(g.w, a.grad_scale);
-        float4 m = *reinterpret_cast<const float4*>(G.m + e0);
-        float4 v = *reinterpret_cast<const float4*>(G.v + e0);
+        float4 m = nt_ld4(G.m + e0);
+        float4 v = nt_ld4(G.v + e0);
         adam_elem(p.x, g.x, m.x, v.x, c);
         adam_elem(p.y, g.y, m.y, v.y, c);
         adam_elem(p.z, g.z, m.z, v.z, c);
         adam_elem(p.w, g.w, m.w, v.w, c);
-        *reinterpret_cast<float4*>(G.p + e0) = p;
-        *reinterpret_cast<float4*>(G.m + e0) = m;
-        *reinterpret_cast<float4*>(G.v + e0) = v;
+        nt_st4(G.p + e0, p);
+        nt_st4(G.m + e0, m);
+        nt_st4(G.v + e0, v);
     } else {
         for (int k = 0; k < kPerThread && e0 + k < G.n; k++) {
             const int64_t e = e0 + k;
@@ -87,7 +100,6 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 
 // float4 copy, one 16-B element per lane, non-temporal loads/stores (tools/copy_probe.hip on
 // MI355X: 6.6 TB/s read + write, vs 6.3 TB/s plain, 5.0 TB/s hipMemcpy, <= 5.8 TB/s grid-stride)
-typedef float v4f __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void k_stream_copy(v4f* __restrict__ dst, const v4f* __restrict__ src, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -95,17 +107,19 @@ __global__ __launch_bounds__(256) void k_stream_copy(v4f* __restrict__ dst, cons
 }
 
 // Adam's access pattern with the arithmetic reduced to a few FMAs: three arrays read and written
-// back in place, one float4 of each per lane (the best of the layouts tools/rmw_probe.hip tried).
+// back in place, one float4 of each per lane (the best of the layouts tools/rmw_probe.hip tried),
+// non-temporal like the optimizer streams it stands for.
 __global__ __launch_bounds__(256) void k_stream_rmw(v4f* __restrict__ p, v4f* __restrict__ m, v4f* __restrict__ v,
                                                     int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    v4f a = p[i], b = m[i], c = v[i];
+    v4f a = __builtin_nontemporal_load(p + i), b = __builtin_nontemporal_load(m + i),
+        c = __builtin_nontemporal_load(v + i);
     b = b * 0.9f + a * 0.1f;
     c = c * 0.999f + a * a * 0.001f;
-    p[i] = a - b * 1e-3f;
-    m[i] = b;
-    v[i] = c;
+    __builtin_nontemporal_store(a - b * 1e-3f, p + i);
+    __builtin_nontemporal_store(b, m + i);
+    __builtin_nontemporal_store(c, v + i);
 }
 
 }  // namespace

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-pair instruction budget of the backward blend's pair loop (k_blend_bwd<1,3>), from the
+"""Per-pair instruction budget of the backward blend's pair loop (k_blend_bwd), from the
 gfx950 assembly of rain_amd/csrc/rr_blend.hip.
 
 The pair loop is the innermost loop of the kernel.  Its basic blocks are sorted into roles:
@@ -27,7 +27,7 @@ from collections import Counter
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KERNEL = "_ZN2rr11k_blend_bwdILi1ELi3EEEvNS_12BlendBwdArgsE"
+KERNEL = "_ZN2rr11k_blend_bwdENS_12BlendBwdArgsE"
 
 
 def opclass(op):
