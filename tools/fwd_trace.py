@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--points", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frames", type=int, default=1, help="traced frames (gpurun_out/fwd_trace[_k].npy)")
     a = ap.parse_args()
     import torch
 
@@ -109,15 +110,18 @@ def main():
     for it in range(901, 901 + a.steps):
         tr.step(it)
     torch.cuda.synchronize()
-    lib.rr_debug_set_fwd_trace(ctypes.c_void_p(buf.data_ptr()))
-    tr.step(901 + a.steps)
-    torch.cuda.synchronize()
-    lib.rr_debug_set_fwd_trace(ctypes.c_void_p(0))
-    rec = buf.view(-1, 8).cpu().numpy().view(np.uint32)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    np.save(os.path.join(ROOT, "gpurun_out", "fwd_trace.npy"), rec)
-    for phase in (0, 1, 2):  # single-phase, early-stop phase A, phase B
-        analyse(rec, phase)
+    for k in range(a.frames):
+        buf.zero_()
+        lib.rr_debug_set_fwd_trace(ctypes.c_void_p(buf.data_ptr()))
+        tr.step(901 + a.steps + k)
+        torch.cuda.synchronize()
+        lib.rr_debug_set_fwd_trace(ctypes.c_void_p(0))
+        rec = buf.view(-1, 8).cpu().numpy().view(np.uint32)
+        np.save(os.path.join(ROOT, "gpurun_out", "fwd_trace.npy" if k == 0 else f"fwd_trace_{k}.npy"), rec)
+        print(f"frame {k}:")
+        for phase in (0, 1, 2):  # single-phase, early-stop phase A, phase B
+            analyse(rec, phase)
 
 
 if __name__ == "__main__":

@@ -16,6 +16,7 @@
 #   prof                  rocprofv3 kernel trace + stats of the default bench, timed-window summary
 #   stalls=PATTERN        one SQ stall-counter pass, summarised for the kernels matching PATTERN
 #   pbprof                phase-B kernel durations per view vs the open-tile region (tools/phaseb_profile.py)
+#   fwdtrace              per-wave forward-blend timelines (tools/fwd_trace.py, gpurun_variants/trace.so)
 #   owner                 owner-kernel time of the sharded step for N = 1, 2, 4, 8 (tools/owner_bench.py)
 #   pmc                   PMC passes (tools/profile_round.sh without the trace) -> pmc_traffic.json
 # Output: gpurun_out/TAG_*.
@@ -80,6 +81,11 @@ for STEP in "$@"; do
         || { tail -20 ${P}.err; exit 1; }
       python3 tools/phaseb_profile.py join $P ${P}_views.jsonl > ${P}_profile.jsonl
       grep -v '"open_tiles": 0,' ${P}_profile.jsonl | head -40 ;;
+    fwdtrace)
+      # per-wave forward-blend timelines of 6 bench frames (gpurun_variants/trace.so, -DRR_FWD_TRACE=1)
+      RAIN_RASTER_LIB=gpurun_variants/trace.so timeout -k 10 300 python3 -u tools/fwd_trace.py --frames 6 \
+        > ${OUT}_fwd_trace.txt 2> ${OUT}_fwd_trace.err || { tail -20 ${OUT}_fwd_trace.err; exit 1; }
+      cat ${OUT}_fwd_trace.txt ;;
     owner)
       # owner-kernel time of the Gaussian-sharded step by N (tools/owner_bench.py)
       timeout -k 10 400 python3 -u tools/owner_bench.py > ${OUT}_owner.jsonl 2> ${OUT}_owner.err \
