@@ -78,12 +78,14 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
-def launch_plan(gpus, env):
+def launch_plan(gpus, env, force_dist=False):
     """What this invocation does with `--gpus`: ("run", world) runs the benchmark in this process as
     one rank of `world`; ("spawn", n) starts n ranks through torch.distributed.run as a child process;
     ("error", msg) refuses.  Pure (no torch, no GPU), so the parent of a spawn never touches the GPU
     before the ranks do (an exec from a GPU-initialised process is forbidden on the box, and a
-    parent holding the device would count against the box's per-card process limit)."""
+    parent holding the device would count against the box's per-card process limit).
+    force_dist: the one-rank process group needs the launcher's environment too (RANK, MASTER_*),
+    so a forced exchange without a launcher spawns one rank."""
     ws = env.get("WORLD_SIZE")
     if ws is not None:
         try:
@@ -96,7 +98,7 @@ def launch_plan(gpus, env):
     n = 1 if gpus is None else gpus
     if n < 1:
         return ("error", f"--gpus {n}: need at least one GPU")
-    return ("spawn", n) if n > 1 else ("run", 1)
+    return ("spawn", n) if n > 1 or force_dist else ("run", 1)
 
 
 def spawn_command(n, argv, port, script=None):
@@ -180,7 +182,7 @@ def gauss_bwd_bytes(P, V, K, M, fused_adam=True, next_frame=False):
 
 def main():
     args = parse()
-    what, val = launch_plan(args.gpus, os.environ)
+    what, val = launch_plan(args.gpus, os.environ, args.force_dist)
     if what == "error":
         print(f"bench.py: {val}", file=sys.stderr)
         return 2

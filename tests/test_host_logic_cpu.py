@@ -70,6 +70,15 @@ def test_bench_launch_plan(gpus, env, plan):
     assert _bench().launch_plan(gpus, env) == plan
 
 
+def test_bench_launch_plan_forced_exchange():
+    """--force-dist (the Gaussian-sharded step at world 1) needs a launcher's environment for its
+    process group: without one it spawns one rank; under a launcher it runs in place."""
+    b = _bench()
+    assert b.launch_plan(1, {}, force_dist=True) == ("spawn", 1)
+    assert b.launch_plan(None, {}, force_dist=True) == ("spawn", 1)
+    assert b.launch_plan(1, {"WORLD_SIZE": "1", "RANK": "0"}, force_dist=True) == ("run", 1)
+
+
 @pytest.mark.parametrize("gpus,env", [(4, {"WORLD_SIZE": "2"}), (1, {"WORLD_SIZE": "8"}), (0, {}),
                                       (2, {"WORLD_SIZE": "x"})])
 def test_bench_launch_plan_refuses(gpus, env):
