@@ -189,6 +189,11 @@ def main():
     if what == "spawn":
         rc = _spawn(val, sys.argv[1:])
         return rc if rc >= 0 else 128 - rc
+    # The JSON line is the only thing on stdout: native libraries' banners (RCCL prints its version
+    # block at communicator creation) go to stderr with everything else.
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -507,7 +512,7 @@ def main():
         "cpu_baseline": cpu,
     }
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
     if world > 1 or force:
         dist.destroy_process_group()
 
