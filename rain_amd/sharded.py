@@ -146,6 +146,10 @@ class ShardedStep:
         if binning is None or binning.device != dev:
             binning = torch.empty((0,), dtype=u8, device=dev)
         nr, npairs, need = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_size_t(0)
+        # the blend backward's accumulators, zero-filled by this render's blend launch
+        # (rr_set_forward_workspace): the backward then skips its 64-MB clear
+        ws = self._buf("ws", int(L.rr_backward_workspace_bytes(P_pad)), u8, dev)
+        N.check(L.rr_set_forward_workspace(_p(ws), ws.numel()), "register workspace")
         r = L.rr_forward_from_geometry(ctypes.byref(fr), ctypes.byref(rc), _p(radii), _p(geom), geom.numel(), _p(img),
                                        img.numel(), _p(binning), binning.numel(), ctypes.byref(nr),
                                        ctypes.byref(npairs), ctypes.byref(need), _p(color), _p(depth), stream)
@@ -153,14 +157,17 @@ class ShardedStep:
             binning = self._bufs["binning"] = torch.empty((int(need.value * 1.25) + 4096,), dtype=u8, device=dev)
             r = L.rr_forward_render_geometry(ctypes.byref(fr), ctypes.byref(rc), _p(radii), _p(geom), _p(img),
                                              _p(binning), binning.numel(), npairs.value, _p(color), _p(depth), stream)
+        if r not in (0, N.RR_INCOMPLETE):
+            L.rr_set_forward_workspace(None, 0)  # a failed render must not leave the registration behind
         N.check(r, "sharded forward")
         self.last = dict(num_rendered=nr.value, num_pairs=npairs.value, P_pad=P_pad, Q=Q)
         dimg, loss = loss_fn(color)
         dimg = dimg.contiguous()
-        ws = self._buf("ws", int(L.rr_backward_workspace_bytes(P_pad)), u8, dev)
         recs = self._buf("recs", P_pad * REC_FLOATS, torch.float32, dev)
         CR = self.chunk_rows(Q)
-        N.check(L.rr_backward_records(ctypes.byref(fr), ctypes.byref(rc), _p(radii), _p(geom), _p(img), _p(binning),
+        frb = N.RRFrame.from_buffer_copy(fr)
+        frb.flags |= N.RR_FLAG_WORKSPACE_REGISTERED
+        N.check(L.rr_backward_records(ctypes.byref(frb), ctypes.byref(rc), _p(radii), _p(geom), _p(img), _p(binning),
                                       nr.value, _p(dimg), _p(ws), ws.numel(), Q, CR, _p(recs), stream),
                 "sharded backward")
 

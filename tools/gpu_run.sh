@@ -13,7 +13,7 @@
 #                         Ti = a list of rr_set_tuning key=value (or variant_step.py --options)
 #                         joined by '+', or 'base'
 #   abv=V1,V2[,..]        the same over librain_raster.so variants (tools/build_variant.py names)
-#   prof                  rocprofv3 kernel trace + stats of the default bench, timed-window summary
+#   prof[=ARGS]           rocprofv3 kernel trace + stats of the bench (default arguments + ARGS), timed-window summary
 #   stalls=PATTERN        one SQ stall-counter pass, summarised for the kernels matching PATTERN
 #   pbprof                phase-B kernel durations per view vs the open-tile region (tools/phaseb_profile.py)
 #   fwdtrace              per-wave forward-blend timelines (tools/fwd_trace.py, gpurun_variants/trace.so)
@@ -91,9 +91,12 @@ for STEP in "$@"; do
       timeout -k 10 400 python3 -u tools/owner_bench.py > ${OUT}_owner.jsonl 2> ${OUT}_owner.err \
         || { tail -20 ${OUT}_owner.err; exit 1; }
       cat ${OUT}_owner.jsonl ;;
-    prof)
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${OUT}_prof -o run --output-format csv \
-        -- python3 bench.py --no-cpu-baseline > ${OUT}_prof_bench.json 2> ${OUT}_prof.err \
+    prof|prof=*)
+      # one rank in this process (the launcher's variables set here): bench.py must not spawn a
+      # child under the profiler
+      A=""; [ "$STEP" != prof ] && A="${STEP#prof=}"
+      RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29531 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${OUT}_prof -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline $A > ${OUT}_prof_bench.json 2> ${OUT}_prof.err \
         || { tail -20 ${OUT}_prof.err; exit 1; }
       python3 tools/step_breakdown.py ${OUT}_prof --window > ${OUT}_timed_kernels.txt 2>&1
       python3 tools/step_breakdown.py ${OUT}_prof --window --seq | tail -40 > ${OUT}_launch_sequence.txt 2>&1
