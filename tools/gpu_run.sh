@@ -17,6 +17,7 @@
 #   stalls=PATTERN        one SQ stall-counter pass, summarised for the kernels matching PATTERN
 #   pbprof                phase-B kernel durations per view vs the open-tile region (tools/phaseb_profile.py)
 #   fwdtrace              per-wave forward-blend timelines (tools/fwd_trace.py, gpurun_variants/trace.so)
+#   hostprobe[=ARGS]      host time of the training step under cProfile (tools/host_probe.py ARGS)
 #   owner                 owner-kernel time of the sharded step for N = 1, 2, 4, 8 (tools/owner_bench.py)
 #   pmc                   PMC passes (tools/profile_round.sh without the trace) -> pmc_traffic.json
 # Output: gpurun_out/TAG_*.
@@ -86,6 +87,13 @@ for STEP in "$@"; do
       RAIN_RASTER_LIB=gpurun_variants/trace.so timeout -k 10 300 python3 -u tools/fwd_trace.py --frames 6 \
         > ${OUT}_fwd_trace.txt 2> ${OUT}_fwd_trace.err || { tail -20 ${OUT}_fwd_trace.err; exit 1; }
       cat ${OUT}_fwd_trace.txt ;;
+    hostprobe|hostprobe=*)
+      # host (Python + driver) time of the training step under cProfile (tools/host_probe.py)
+      A=""; [ "$STEP" != hostprobe ] && A="${STEP#hostprobe=}"
+      RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29532 timeout -k 10 400 \
+        python3 -u tools/host_probe.py $A > ${OUT}_host_probe.txt 2> ${OUT}_host_probe.err \
+        || { tail -20 ${OUT}_host_probe.err; exit 1; }
+      head -60 ${OUT}_host_probe.txt ;;
     owner)
       # owner-kernel time of the Gaussian-sharded step by N (tools/owner_bench.py)
       timeout -k 10 400 python3 -u tools/owner_bench.py > ${OUT}_owner.jsonl 2> ${OUT}_owner.err \
