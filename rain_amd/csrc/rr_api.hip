@@ -201,7 +201,8 @@ struct Bin {
     size_t total;
 };
 // Window (= sort unit) length of each phase's sort, chosen for the pairs it is expected to hold
-// (k_early_cut aims phase A at ~1/den of the pairs) while its windows cover the capacity L.
+// (the split scan's depth cut aims phase A at ~1/den of the pairs) while its windows cover the
+// capacity L.
 struct PhaseHints {
     size_t a, b;
 };
@@ -326,10 +327,11 @@ int check(const rr_frame* f, hipStream_t st, const char* what) {
 // ---------------------------------------------------------------------------------------
 // Readback of the forward's pair counts.  A hipMemcpyAsync into pageable host memory + stream
 // synchronise after the scan costs a blit kernel and the runtime's blocking wait (measured 30-140
-// us of idle GPU per frame before the binning launches).  Instead the depth-cut kernel (rr_bin.hip
-// k_early_cut, the first launch after the preprocess; the split scan runs on while the host reads)
-// stores the counts and a sequence number into a coherent pinned host
-// mailbox (system-scope release store) and the host thread spins on the sequence number.  Once the
+// us of idle GPU per frame before the binning launches).  Instead the split scan's first launch
+// (rr_bin.hip k_split_scan_totals: workgroup 0, once the frame's totals and depth cut are known;
+// the scan runs on while the host reads) stores the counts and a sequence number into a coherent
+// pinned host mailbox (system-scope stores, the sequence number last) and the host thread spins on
+// the sequence number.  Once the
 // wait has outlasted any frame the stream is queried: a launch / kernel error is reported, and a
 // stream that went idle without the sequence number becoming visible falls back to the plain copy.
 struct Mailbox {

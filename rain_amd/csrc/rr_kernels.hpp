@@ -6,8 +6,8 @@
 namespace rr {
 
 // Per-frame scalars of the depth-sort-free binning (rr_bin.hip), in the geometry buffer: written by
-// k_early_cut (L, rect, wide, cut; it also copies L, rect and wide to the host mailbox) and by the
-// split scan's last thread (LA, LB, GA, GB: read on the device only).  Also the device copy the
+// the split scan's first launch (L, rect, wide, cut; it also copies L, rect and wide to the host
+// mailbox) and by the split scan's last thread (LA, LB, GA, GB: read on the device only).  Also the device copy the
 // no-mailbox read-back path reads.
 struct FrameTotals {
     unsigned long long L;     // (bin, Gaussian) pairs of the frame

@@ -215,7 +215,7 @@ def debug_views(geomBuffer, binningBuffer, imageBuffer, num_rendered, P, W, H):
 
     return dict(
         # per-tile lists live at the ranges' absolute positions: 4 slots per (bin, Gaussian) pair
-        # (the compact layout of the all-gather binning holds 4 L slots: clamped to the buffer)
+        # (phase A's region [0, 4L) and phase B's [4L, 8L); clamped to the buffer)
         point_list=grab(v.point_list, min(8 * num_rendered, (binningBuffer.numel() - (v.point_list -
                                           binningBuffer.data_ptr())) // 4), torch.int32, binningBuffer)
         if num_rendered else torch.empty((0,), dtype=torch.int32, device=dev),

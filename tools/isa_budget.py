@@ -14,7 +14,7 @@ a pixel body runs when any lane of the wave has that pixel active.  With the mea
 instructions per (tile, pair) from the PMC pass (SQ_INSTS_VALU / L_eff) the number of pixel
 bodies a pair executes on average follows:  valu = per_pair_valu + k * body_valu.
 
-    python tools/isa_budget.py [--valu-per-pair 158.6] [--define RR_BWD_DEFER=0] [--out FILE]
+    python tools/isa_budget.py [--valu-per-pair 158.6] [--define MACRO=VALUE] [--out FILE]
 """
 import argparse
 import os
