@@ -29,10 +29,13 @@ def gpu():
     return torch.device("cuda:0")
 
 
+SPAWNING = ("test_multirank_gpu", "test_bench_gpu")
+
+
 def pytest_collection_modifyitems(config, items):
-    """Multi-process GPU tests spawn their ranks before this process initialises the GPU: run them
-    first in the session."""
-    first = [it for it in items if "test_multirank_gpu" in it.nodeid]
+    """Multi-process GPU tests (ranks, bench.py subprocesses) start their processes before this
+    process initialises the GPU: run them first in the session."""
+    first = [it for it in items if any(m in it.nodeid for m in SPAWNING)]
     if first:
-        rest = [it for it in items if "test_multirank_gpu" not in it.nodeid]
+        rest = [it for it in items if not any(m in it.nodeid for m in SPAWNING)]
         items[:] = first + rest
