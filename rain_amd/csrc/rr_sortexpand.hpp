@@ -317,13 +317,8 @@ __device__ __forceinline__ void sortexpand_run(SxSharedT<NT / 64, CAP>& sh, int 
         }
         bool sorted = false;
         if (bucket) {
-#ifdef RR_SX_TIMING_NO_GATHER  // timing experiment only (wrong order): the depth-key gathers' cost
-#pragma unroll
-            for (int r = 0; r < MR; r++) kr[r] = vr[r] & BIN_ID_MASK;
-#else
 #pragma unroll
             for (int r = 0; r < MR; r++) kr[r] = depth_keys[vr[r] & BIN_ID_MASK];  // all gathers in flight
-#endif
             sorted = bucket_sort_run<NT, CAP>(sh, kr, vr, R, len);  // block-uniform
         }
         for (int attempt = 0; !sorted; attempt++) {
