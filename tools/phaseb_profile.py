@@ -21,7 +21,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASE_B = {"dup_B": r"k_dup_gather<.*true>", "count": r"k_bin_count", "scatter": r"k_bin_scatter",
+PHASE_B = {"dup_B": r"k_dup_gather<", "count": r"k_bin_count", "scatter": r"k_bin_scatter",
            "sort_B": r"k_sortexpand<.*1024>", "blend_B": r"k_blend_fwd_s<4"}
 
 
