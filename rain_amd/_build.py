@@ -43,14 +43,21 @@ LIBS = {
 # frame's preprocess inside the per-Gaussian backward (rr_preprocess.hpp, include/rain_raster.h
 # rr_next_frame) then compile the same arithmetic to the same fma sequence in both kernels, so the
 # fused geometry is bitwise the forward's.
+# rr_blend.hip / rr_backward.hip: LLVM's max-ILP machine scheduler instead of the default
+# occupancy-driven one (same VGPR budget here: both kernels' occupancy is set elsewhere — the
+# backward blend's 4 waves, the Gaussian backward's LDS rows); it interleaves the independent chains
+# of a pair's alphas and a row's terms further: blend bwd 0.227 -> 0.221 ms, Gaussian bwd 0.326 ->
+# 0.324, step -8 us (profiles/r06ah_sched_ilp_ab.jsonl; on the forward blend, the binning and the
+# SSIM sources it measured neutral or slower, r06ag / r06ah)
+MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 CONTRACT_ON = ["-ffp-contract=on"]
 EXTRA = {
     "rr_forward.hip": CONTRACT_ON,
-    "rr_backward.hip": CONTRACT_ON,
+    "rr_backward.hip": CONTRACT_ON + MAX_ILP,
     # rr_blend_fwd_s.hip: machine sinking would move the software-pipelined next-group record loads
     # below the blend (next to their use in the loop latch), serialising them again
     "rr_blend_fwd_s.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-mllvm", "-disable-machine-sink"],
-    "rr_blend.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
+    "rr_blend.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"] + MAX_ILP,
     "loss.hip": ["-mllvm", "-pragma-unroll-threshold=200000",
                  "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"],
 }
@@ -89,7 +96,7 @@ def build(force: bool = False, verbose: bool = False) -> dict:
             if not os.path.exists(src):
                 continue
             obj = os.path.join(OBJDIR, s.replace(".hip", ".o"))
-            if force or _stale(obj, [src, *headers]):
+            if force or _stale(obj, [src, *headers, os.path.abspath(__file__)]):  # flags live here
                 jobs.append((src, obj))
     if jobs:
         with ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:

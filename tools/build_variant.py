@@ -5,6 +5,10 @@ gpurun_variants/<name>.so (git-ignored; travels to the GPU box with the snapshot
     python tools/build_variant.py nostage -DRR_STAGE_SH=0
     python tools/build_variant.py prev --rev HEAD      (the sources of a git revision)
     python tools/build_variant.py probe --src DIR -DX  (sources from DIR/rain_amd/csrc, DIR/include)
+    python tools/build_variant.py ilp @rr_blend.hip=-mllvm,-amdgpu-sched-strategy=max-ilp
+                                                       (flags for one source only)
+    python tools/build_variant.py lossx --lib librain_loss.so -DX   (another library of rain_amd/_build.py;
+                                                       RAIN_LOSS_LIB selects it)
 """
 import os
 import subprocess
@@ -31,16 +35,24 @@ def main():
     elif flags[:1] == ["--src"]:
         tmp, flags = flags[1], flags[2:]
         csrc, inc = os.path.join(tmp, "rain_amd", "csrc"), os.path.join(tmp, "include")
+    lib = "librain_raster.so"
+    if flags[:1] == ["--lib"]:
+        lib, flags = flags[1], flags[2:]
+    per_file = {}  # @source=flag,flag: extra flags for that source only
+    for f in [f for f in flags if f.startswith("@")]:
+        src, _, fl = f[1:].partition("=")
+        per_file.setdefault(src, []).extend(fl.split(","))
+    flags = [f for f in flags if not f.startswith("@")]
     pre = ["-I", inc, "-I", csrc] if csrc != B.CSRC else []  # ahead of the tree's own include dirs
     out = os.path.join(ROOT, "gpurun_variants")
     objdir = os.path.join(out, name + "_obj")
     os.makedirs(objdir, exist_ok=True)
-    srcs = B.LIBS["librain_raster.so"]
+    srcs = B.LIBS[lib]
 
     def cc(s):
         src = os.path.join(csrc, s)
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
-        cmd = [B.HIPCC, *pre, *B.CXXFLAGS, *B.EXTRA.get(s, []), *flags, "-c", src, "-o", obj]
+        cmd = [B.HIPCC, *pre, *B.CXXFLAGS, *B.EXTRA.get(s, []), *flags, *per_file.get(s, []), "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             raise SystemExit(r.stderr)

@@ -13,6 +13,7 @@
 #                         Ti = a list of rr_set_tuning key=value (or variant_step.py --options)
 #                         joined by '+', or 'base'
 #   abv=V1,V2[,..]        the same over librain_raster.so variants (tools/build_variant.py names)
+#   abl=V1,V2[,..]        the same over librain_loss.so variants (build_variant.py --lib librain_loss.so)
 #   prof[=ARGS]           rocprofv3 kernel trace + stats of the bench (default arguments + ARGS), timed-window summary
 #   stalls=PATTERN        one SQ stall-counter pass, summarised for the kernels matching PATTERN
 #   pbprof                phase-B kernel durations per view vs the open-tile region (tools/phaseb_profile.py)
@@ -64,6 +65,16 @@ for STEP in "$@"; do
         for v in "${VS[@]}"; do
           LIB=""; [ "$v" != base ] && LIB=gpurun_variants/$v.so
           RAIN_RASTER_LIB=$LIB timeout -k 10 300 python3 -u tools/variant_step.py --tag="$v" >> ${OUT}_ab.jsonl \
+            2>> ${OUT}_ab.err || { tail -20 ${OUT}_ab.err; exit 1; }
+        done
+      done
+      cat ${OUT}_ab.jsonl ;;
+    abl=*)
+      IFS=',' read -ra VS <<< "${STEP#abl=}"
+      for r in 1 2; do
+        for v in "${VS[@]}"; do
+          LIB=""; [ "$v" != base ] && LIB=gpurun_variants/$v.so
+          RAIN_LOSS_LIB=$LIB timeout -k 10 300 python3 -u tools/variant_step.py --tag="$v" >> ${OUT}_ab.jsonl \
             2>> ${OUT}_ab.err || { tail -20 ${OUT}_ab.err; exit 1; }
         done
       done
